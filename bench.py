@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Benchmark: BLS12-381 pairings/sec at batch 2^16 per GPU (BASELINE.json).
+
+  python bench.py --gpus N --steps K --warmup W
+  (N > 1: launched by torch.distributed.run, one rank per GPU over RCCL)
+
+A step = one batch of 2^16 independent pairings e(P_i, Q_i) per GPU, inputs
+(G1Affine, G2Affine records) already resident in HBM: the fused
+prepare+Miller-loop kernel, then the final-exponentiation kernel, then (N > 1)
+one RCCL gather of every rank's 2^16 Fq12 results to rank 0 -- the shard is
+independent work (weak scaling), the gather is the path's only exchange.
+
+Rank 0 prints one JSON line with the driver's fields plus
+  roofline      -- the dominant kernel's algorithmic HBM bytes per launch over
+                   its HIP-event-measured average duration, vs 8 TB/s;
+                   `traffic` = PMC-measured HBM bytes per launch from
+                   profiles/ when that summary exists.
+  cpu_baseline  -- the C restatement of the reference (oracle/, the CPU path
+                   of the reference's algorithms) timed on this host's cores
+                   over a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FQ12_BYTES = 576
+G1A_BYTES, G2A_BYTES = 104, 200  # ABI records (coordinates + infinity flag + pad)
+# algorithmic HBM bytes per pairing, per kernel (DESIGN.md "Roofline")
+ML_BYTES = 96 + 192 + 2 + FQ12_BYTES   # P, Q coordinates + flags in, f out
+FE_BYTES = FQ12_BYTES + FQ12_BYTES     # f in, e(P,Q) out
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1 << 16, help="pairings per GPU per step")
+    ap.add_argument("--workload", choices=["pairing", "fq_mul"], default="pairing")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def make_pairs(n, rank, seed=0):
+    """2^16 pairs tiled from a pool of 256 x 256 distinct point combinations,
+    1/128 of them with an infinity side (mod.rs:50-54)."""
+    d = np.load(os.path.join(ROOT, "tests", "golden", "bench_points.npz"))
+    g1, g2 = d["g1"], d["g2"]
+    idx = np.arange(n, dtype=np.int64) + rank * n + seed
+    p = g1[idx % 256].copy()
+    q = g2[(idx // 256 + idx * 7) % 256].copy()
+    inf = np.nonzero(idx % 128 == 5)[0]
+    p[inf, :] = 0
+    p[inf, 6] = 0x760900000002fffd  # y = one (low limb), rest below
+    one = [0x760900000002fffd, 0xebf4000bc40c0002, 0x5f48985753c758ba,
+           0x77ce585370525745, 0x5c071a97a256ec6d, 0x15f65ec3fa80e493]
+    p[inf, 6:12] = np.array(one, dtype=np.uint64)
+    p[inf, 12] = 1
+    return p, q
+
+
+def cpu_baseline_pairing(p, q, seconds):
+    """Time the oracle (C restatement of the reference) on this host."""
+    from oracle import binding as oracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))
+    # calibrate on a small sample, then size the sample to ~`seconds` of CPU work
+    t0 = time.perf_counter()
+    oracle.pairing(p[:threads], q[:threads], threads)
+    dt = time.perf_counter() - t0
+    per_pair_cpu = dt * threads / threads  # wall per pair-per-thread
+    n = int(max(threads, min(len(p), seconds / max(per_pair_cpu, 1e-4))))
+    t0 = time.perf_counter()
+    oracle.pairing(p[:n], q[:n], threads)
+    wall = time.perf_counter() - t0
+    return {"value": n / wall, "unit": "pairings/s", "cores": threads, "kind": "port",
+            "sample": "%d pairings of the same synthetic batch, C restatement of the reference "
+                      "(oracle/), OpenMP over pairs, %.1f s wall" % (n, wall)}
+
+
+def cpu_baseline_fq_mul(a, b, seconds):
+    from oracle import binding as oracle
+    n = min(len(a), 1 << 20)
+    t0 = time.perf_counter()
+    oracle.fq_mul(a[:n], b[:n])
+    wall = time.perf_counter() - t0
+    return {"value": n / wall, "unit": "muls/s", "cores": 1, "kind": "port",
+            "sample": "%d Fq::mul_assign, C restatement (oracle/), 1 thread" % n}
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_env()
+    import torch
+    import torch.distributed as dist
+    import pairing_amd
+    import pairing_amd.device as pdev
+
+    torch.cuda.set_device(local)
+    pairing_amd.set_device(local)
+    dev = torch.device("cuda", local)
+    if ws > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    n = args.batch
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    k_ms = {"a": [], "b": []}
+
+    if args.workload == "pairing":
+        p_np, q_np = make_pairs(n, rank)
+        p = torch.from_numpy(p_np.view(np.int64)).to(dev)
+        q = torch.from_numpy(q_np.view(np.int64)).to(dev)
+        out = pdev.empty_records(n, 72, dev)
+        scratch = pdev.empty_records(n, 72, dev)
+        gather_list = [pdev.empty_records(n, 72, dev) for _ in range(ws)] if (ws > 1 and rank == 0) else None
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            pdev.miller_loop(p, q, scratch, stream)
+            if timed:
+                ev[1].record(stream)
+            pdev.final_exponentiation(scratch, out, None, stream)
+            if timed:
+                ev[2].record(stream)
+            if ws > 1:
+                dist.gather(out, gather_list, dst=0)
+    else:
+        g = np.random.default_rng(rank)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from helpers import random_fq
+        n = args.batch if args.batch != (1 << 16) else (1 << 20)
+        a_np = random_fq(g, 4096)[np.arange(n) % 4096]
+        b_np = random_fq(g, 4096)[(np.arange(n) * 7 + 3) % 4096]
+        a = torch.from_numpy(a_np.view(np.int64)).to(dev)
+        b = torch.from_numpy(b_np.view(np.int64)).to(dev)
+        out = pdev.empty_records(n, 6, dev)
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            pdev.fq_mul(a, b, out, stream)
+            if timed:
+                ev[1].record(stream)
+
+    for _ in range(args.warmup):
+        step(False)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+        # per-kernel durations from HIP events on the launch stream
+        torch.cuda.synchronize()
+        k_ms["a"].append(ev[0].elapsed_time(ev[1]))
+        if args.workload == "pairing":
+            k_ms["b"].append(ev[1].elapsed_time(ev[2]))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if ws > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    if rank == 0:
+        if args.workload == "pairing":
+            ml = float(np.mean(k_ms["a"]))
+            fe = float(np.mean(k_ms["b"]))
+            dom_name, dom_ms, dom_bytes = ("final_exponentiation", fe, FE_BYTES) if fe >= ml else \
+                ("miller_loop_fused", ml, ML_BYTES)
+            value = ws * n * args.steps / elapsed
+            metric, unit = "BLS12-381 pairings/sec at batch 2^16", "pairings/s"
+            config = {"workload": "bls12_381 e(P_i,Q_i) batch (fused G2 prepare + Miller loop + final exp)",
+                      "batch_per_gpu": n, "global_batch": n * ws, "parallelism": "shard%d+rccl_gather" % ws
+                      if ws > 1 else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
+                                                             "final_exponentiation": round(fe, 3)}}
+        else:
+            dom_name, dom_ms, dom_bytes = "fq_mul_batch", float(np.mean(k_ms["a"])), 144
+            value = ws * n * args.steps / elapsed
+            metric, unit = "Fq::mul_assign per second at batch 2^20", "muls/s"
+            config = {"workload": "2^20 Fq Montgomery multiplications (AoS 6x u64)", "batch_per_gpu": n,
+                      "global_batch": n * ws}
+        achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9
+        traffic = None
+        tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tr_path):
+            with open(tr_path) as f:
+                traffic = json.load(f).get(dom_name)
+        roof = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "bytes_per_unit": dom_bytes, "avg_launch_ms": round(dom_ms, 4)}
+        cpu = None
+        if not args.no_cpu_baseline and ws == 1:
+            if args.workload == "pairing":
+                cpu = cpu_baseline_pairing(p_np, q_np, args.cpu_seconds)
+            else:
+                cpu = cpu_baseline_fq_mul(a_np, b_np, args.cpu_seconds)
+        line = {"metric": metric, "value": value, "unit": unit, "n_gpus": ws, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "u32 (384-bit Montgomery, 12 x u32 limbs)",
+                "data": "synthetic (seeded random points k*G)", "config": config,
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

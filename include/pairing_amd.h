@@ -1,0 +1,128 @@
+/*
+ * pairing_amd -- MI355X-native batched BLS12-381 engine, C ABI.
+ *
+ * This is the drop-in boundary for the hot path of the Rust crate `pairing`
+ * v0.14.2 (dignifiedquire/pairing).  The reference has no FFI of its own: its
+ * interface is the Rust trait surface in src/lib.rs.  Each entry point below
+ * names the trait method (reference file:line) it replaces, batched over n
+ * independent items.  INTEGRATION.md shows the Rust `extern "C"` block a
+ * maintainer would add to bind it.
+ *
+ * Data layout (host and device) is the Rust in-memory order of the reference
+ * types, so a `&[G1Affine]` can be passed by pointer:
+ *   Fq        = 6 x u64, little-endian limbs, Montgomery form (R = 2^384), < q
+ *               (src/bls12_381/fq.rs:699-700)
+ *   Fq2       = {c0, c1}            Fq6 = {c0, c1, c2}       Fq12 = {c0, c1}
+ *   G1Affine  = {Fq x, Fq y, u8 infinity, 7 pad}   (104 B)   ec.rs:13-18
+ *   G2Affine  = {Fq2 x, Fq2 y, u8 infinity, 7 pad} (200 B)
+ *   G1 / G2   = Jacobian {x, y, z}, zero iff z == 0 (144 B / 288 B) ec.rs:31-36
+ *   FrRepr    = 4 x u64 little-endian, canonical (not Montgomery) fr.rs:58
+ *   G2Prepared= 68 x (Fq2, Fq2, Fq2) line coefficients + u8 infinity + 7 pad
+ *               (ec.rs:1615-1619, built by mod.rs:168-358) = 19 592 B
+ *
+ * Conventions
+ *   - Every function returns 0 (PA_OK) or a negative PA_ERR_* code; nothing
+ *     aborts across the ABI.  pa_last_error() describes the last failure on
+ *     the calling thread.
+ *   - Per-item Option results (reference returns None) are reported through a
+ *     caller-provided u8 `ok` array: 1 = Some, 0 = None.
+ *   - Host-pointer functions (no suffix) are synchronous: they copy inputs to
+ *     the current device, run, and copy outputs back.  The caller owns all
+ *     buffers; nothing is retained after return.  `out` may alias an input of
+ *     the same type (giving the reference's *_assign in-place semantics).
+ *   - `_device` functions take device pointers and a hipStream_t (as void*,
+ *     NULL = default stream) and return after enqueueing; inputs must stay
+ *     valid until the stream reaches the work.
+ *   - Thread safety: all entry points are reentrant (the reference traits are
+ *     Send + Sync, lib.rs:114-121, 185-186).  The device used is the calling
+ *     thread's current HIP device (pa_set_device).
+ */
+#ifndef PAIRING_AMD_H
+#define PAIRING_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PA_OK 0
+#define PA_ERR_INVALID_ARGUMENT (-1)
+#define PA_ERR_HIP (-2)
+#define PA_ERR_OUT_OF_MEMORY (-3)
+#define PA_ERR_NO_DEVICE (-4)
+
+#define PA_G2_PREPARED_COEFFS 68
+
+typedef struct { uint64_t l[6]; } pa_fq;
+typedef struct { pa_fq c0, c1; } pa_fq2;
+typedef struct { pa_fq2 c0, c1, c2; } pa_fq6;
+typedef struct { pa_fq6 c0, c1; } pa_fq12;
+typedef struct { uint64_t l[4]; } pa_fr_repr;
+typedef struct { pa_fq x, y; uint8_t infinity; uint8_t _pad[7]; } pa_g1_affine;
+typedef struct { pa_fq2 x, y; uint8_t infinity; uint8_t _pad[7]; } pa_g2_affine;
+typedef struct { pa_fq x, y, z; } pa_g1;
+typedef struct { pa_fq2 x, y, z; } pa_g2;
+typedef struct {
+    pa_fq2 coeffs[PA_G2_PREPARED_COEFFS][3];
+    uint8_t infinity;
+    uint8_t _pad[7];
+} pa_g2_prepared;
+
+/* ---- runtime ---- */
+const char *pa_version(void);
+const char *pa_last_error(void);
+int pa_device_count(int *count);
+int pa_set_device(int device);
+int pa_synchronize(void);
+
+/* ---- Fq (src/bls12_381/fq.rs, Field trait src/lib.rs:267-325) ---- */
+/* Field::mul_assign, fq.rs:909-960 + mont_reduce fq.rs:1036-1122 */
+int pa_fq_mul_batch(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n);
+/* Field::square, fq.rs:962-1016 */
+int pa_fq_square_batch(const pa_fq *a, pa_fq *out, size_t n);
+/* Field::add_assign / sub_assign, fq.rs:812-838 */
+int pa_fq_add_batch(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n);
+int pa_fq_sub_batch(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n);
+/* Field::inverse, fq.rs:849-902 (ok[i] = 0 for a zero input) */
+int pa_fq_inverse_batch(const pa_fq *a, pa_fq *out, uint8_t *ok, size_t n);
+
+/* ---- tower (fq2.rs, fq6.rs, fq12.rs) ---- */
+int pa_fq2_mul_batch(const pa_fq2 *a, const pa_fq2 *b, pa_fq2 *out, size_t n);     /* fq2.rs:123-136 */
+int pa_fq2_square_batch(const pa_fq2 *a, pa_fq2 *out, size_t n);                   /* fq2.rs:87-101 */
+int pa_fq6_mul_batch(const pa_fq6 *a, const pa_fq6 *b, pa_fq6 *out, size_t n);     /* fq6.rs:199-248 */
+int pa_fq12_mul_batch(const pa_fq12 *a, const pa_fq12 *b, pa_fq12 *out, size_t n); /* fq12.rs:116-130 */
+int pa_fq12_square_batch(const pa_fq12 *a, pa_fq12 *out, size_t n);                /* fq12.rs:99-114 */
+int pa_fq12_inverse_batch(const pa_fq12 *a, pa_fq12 *out, uint8_t *ok, size_t n);  /* fq12.rs:132-148 */
+int pa_fq12_frobenius_map_batch(const pa_fq12 *a, pa_fq12 *out, size_t n, size_t power); /* fq12.rs:90-97 */
+/* Fq12::mul_by_014, fq12.rs:34-48 */
+int pa_fq12_mul_by_014_batch(const pa_fq12 *a, const pa_fq2 *c0, const pa_fq2 *c1, const pa_fq2 *c4,
+                             pa_fq12 *out, size_t n);
+
+/* ---- G2 line precomputation: G2Prepared::from_affine, mod.rs:168-358 ---- */
+int pa_g2_prepare_batch(const pa_g2_affine *q, pa_g2_prepared *out, size_t n);
+
+/* ---- Engine (src/lib.rs:34-110, src/bls12_381/mod.rs:30-161) ---- */
+/* n independent single-pair loops: out[i] = Bls12::miller_loop([(p[i], q[i])]) (mod.rs:40-102) */
+int pa_miller_loop_batch(const pa_g1_affine *p, const pa_g2_prepared *q, pa_fq12 *out, size_t n);
+/* Engine::miller_loop over n pairs: the product semantics of mod.rs:40-102 */
+int pa_multi_miller_loop(const pa_g1_affine *p, const pa_g2_prepared *q, size_t n, pa_fq12 *out);
+/* Engine::final_exponentiation, mod.rs:104-160; ok[i] = 0 iff in[i] == 0 */
+int pa_final_exponentiation_batch(const pa_fq12 *in, pa_fq12 *out, uint8_t *ok, size_t n);
+/* Engine::pairing, lib.rs:101-109: out[i] = e(p[i], q[i]) (prepare fused on device) */
+int pa_pairing_batch(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n);
+
+/* ---- device-resident variants (pointers are device memory) ---- */
+int pa_fq_mul_batch_device(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n, void *stream);
+int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
+                                      void *stream);
+int pa_final_exponentiation_batch_device(const pa_fq12 *in, pa_fq12 *out, uint8_t *ok, size_t n, void *stream);
+/* e(p[i], q[i]); `scratch` must hold n pa_fq12 (the Miller-loop values) */
+int pa_pairing_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, pa_fq12 *scratch,
+                            size_t n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PAIRING_AMD_H */

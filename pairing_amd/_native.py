@@ -1,0 +1,115 @@
+"""ctypes binding of the HIP library pairing_amd/lib/libpairing_amd.so.
+
+This is the only way the Python package reaches compute: every function
+below ends in a HIP kernel on the current device.  There is no CPU fallback;
+if the library is missing or fails to load, import raises.
+
+Array convention (numpy uint64, C-contiguous, the ABI layout of
+include/pairing_amd.h):
+  Fq (n,6)  Fq2 (n,12)  Fq6 (n,36)  Fq12 (n,72)
+  G1Affine (n,13)  G2Affine (n,25)  G1 (n,18)  G2 (n,36)  G2Prepared (n,2449)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libpairing_amd.so")
+
+W_FQ, W_FQ2, W_FQ6, W_FQ12 = 6, 12, 36, 72
+W_G1A, W_G1, W_G2A, W_G2 = 13, 18, 25, 36
+W_G2P = 68 * 3 * 12 + 1
+
+PA_OK = 0
+
+
+class PairingError(RuntimeError):
+    """A negative status code from the C ABI (see include/pairing_amd.h)."""
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "pairing_amd: HIP library %s is missing -- build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)" % LIB_PATH)
+    return ctypes.CDLL(LIB_PATH)
+
+
+_lib = _load()
+_P = ctypes.c_void_p
+_N = ctypes.c_size_t
+
+# Every exported entry point with its argument types (all return int).
+_SIGS = {
+    "pa_device_count": [ctypes.POINTER(ctypes.c_int)],
+    "pa_set_device": [ctypes.c_int],
+    "pa_synchronize": [],
+    "pa_fq_mul_batch": [_P, _P, _P, _N],
+    "pa_fq_square_batch": [_P, _P, _N],
+    "pa_fq_add_batch": [_P, _P, _P, _N],
+    "pa_fq_sub_batch": [_P, _P, _P, _N],
+    "pa_fq_inverse_batch": [_P, _P, _P, _N],
+    "pa_fq2_mul_batch": [_P, _P, _P, _N],
+    "pa_fq2_square_batch": [_P, _P, _N],
+    "pa_fq6_mul_batch": [_P, _P, _P, _N],
+    "pa_fq12_mul_batch": [_P, _P, _P, _N],
+    "pa_fq12_square_batch": [_P, _P, _N],
+    "pa_fq12_inverse_batch": [_P, _P, _P, _N],
+    "pa_fq12_frobenius_map_batch": [_P, _P, _N, _N],
+    "pa_fq12_cyclotomic_square_batch": [_P, _P, _N],
+    "pa_fq12_mul_by_014_batch": [_P, _P, _P, _P, _P, _N],
+    "pa_g2_prepare_batch": [_P, _P, _N],
+    "pa_miller_loop_batch": [_P, _P, _P, _N],
+    "pa_multi_miller_loop": [_P, _P, _N, _P],
+    "pa_final_exponentiation_batch": [_P, _P, _P, _N],
+    "pa_pairing_batch": [_P, _P, _P, _N],
+    "pa_fq_mul_batch_device": [_P, _P, _P, _N, _P],
+    "pa_miller_loop_fused_batch_device": [_P, _P, _P, _N, _P],
+    "pa_final_exponentiation_batch_device": [_P, _P, _P, _N, _P],
+    "pa_pairing_batch_device": [_P, _P, _P, _P, _N, _P],
+}
+for _name, _args in _SIGS.items():
+    _fn = getattr(_lib, _name)
+    _fn.argtypes = _args
+    _fn.restype = ctypes.c_int
+_lib.pa_version.restype = ctypes.c_char_p
+_lib.pa_last_error.restype = ctypes.c_char_p
+
+
+def version():
+    return _lib.pa_version().decode()
+
+
+def _check(rc, what):
+    if rc != PA_OK:
+        raise PairingError("%s failed (%d): %s" % (what, rc, _lib.pa_last_error().decode()))
+
+
+def call(name, *args):
+    _check(getattr(_lib, name)(*args), name)
+
+
+def device_count():
+    c = ctypes.c_int(0)
+    rc = _lib.pa_device_count(ctypes.byref(c))
+    return c.value if rc == PA_OK else 0
+
+
+def set_device(dev):
+    call("pa_set_device", dev)
+
+
+def ptr(a):
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("arrays must be C-contiguous")
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def as_rows(a, width, name="array"):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    if a.ndim == 1:
+        a = a.reshape(1, -1)
+    if a.ndim != 2 or a.shape[1] != width:
+        raise ValueError("%s must have shape (n, %d), got %s" % (name, width, a.shape))
+    return a

@@ -1,0 +1,288 @@
+// C ABI of pairing_amd (include/pairing_amd.h): argument checking, device
+// buffers for the host-pointer entry points, error reporting.  No compute
+// happens here; every entry point ends in a HIP kernel from
+// kernels_field.hip / kernels_pairing.hip.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/pairing_amd.h"
+#include "launch.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* what, hipError_t e = hipSuccess) {
+    char buf[256];
+    if (e != hipSuccess)
+        snprintf(buf, sizeof buf, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    else
+        snprintf(buf, sizeof buf, "%s", what);
+    g_last_error = buf;
+    return code;
+}
+
+int hip_code(hipError_t e) {
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return PA_ERR_OUT_OF_MEMORY;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return PA_ERR_NO_DEVICE;
+    return PA_ERR_HIP;
+}
+
+#define PA_TRY(expr, what)                                          \
+    do {                                                            \
+        hipError_t _e = (expr);                                     \
+        if (_e != hipSuccess) return fail(hip_code(_e), what, _e);  \
+    } while (0)
+
+// RAII device buffer for the synchronous host-pointer entry points.
+struct DevBuf {
+    void* p = nullptr;
+    hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 1); }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+// Copy `count` host inputs of `bytes_each` into fresh device buffers.
+int upload(DevBuf& d, const void* host, size_t bytes) {
+    PA_TRY(d.alloc(bytes), "hipMalloc");
+    if (bytes) PA_TRY(hipMemcpy(d.p, host, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
+    return PA_OK;
+}
+int download(void* host, const DevBuf& d, size_t bytes) {
+    if (bytes) PA_TRY(hipMemcpy(host, d.p, bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+    return PA_OK;
+}
+
+bool op_needs_b(int op) {
+    return op == pa::OP_FQ_MUL || op == pa::OP_FQ_ADD || op == pa::OP_FQ_SUB || op == pa::OP_FQ2_MUL ||
+           op == pa::OP_FQ6_MUL || op == pa::OP_FQ12_MUL;
+}
+
+// Elementwise field op on host buffers: out = op(a, b).
+int host_field_op(int op, const void* a, const void* b, void* out, uint8_t* ok, size_t n, size_t in_bytes,
+                  size_t out_bytes, int param) {
+    if (n == 0) return PA_OK;
+    if (!a || !out || (op_needs_b(op) && !b)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf da, db, dout, dok;
+    int rc;
+    if ((rc = upload(da, a, in_bytes * n))) return rc;
+    if (b && (rc = upload(db, b, in_bytes * n))) return rc;
+    PA_TRY(dout.alloc(out_bytes * n), "hipMalloc");
+    if (ok) PA_TRY(dok.alloc(n), "hipMalloc");
+    PA_TRY(pa::launch_field_op(op, da.as<uint64_t>(), db.as<uint64_t>(), dout.as<uint64_t>(), dok.as<uint8_t>(), n,
+                               param, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    if ((rc = download(out, dout, out_bytes * n))) return rc;
+    if (ok && (rc = download(ok, dok, n))) return rc;
+    return PA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pa_version(void) { return "pairing_amd 0.1.0 (gfx950)"; }
+const char* pa_last_error(void) { return g_last_error.c_str(); }
+
+int pa_device_count(int* count) {
+    if (!count) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(PA_ERR_NO_DEVICE, "hipGetDeviceCount", e);
+    }
+    return PA_OK;
+}
+int pa_set_device(int device) {
+    PA_TRY(hipSetDevice(device), "hipSetDevice");
+    return PA_OK;
+}
+int pa_synchronize(void) {
+    PA_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    return PA_OK;
+}
+
+int pa_fq_mul_batch(const pa_fq* a, const pa_fq* b, pa_fq* out, size_t n) {
+    return host_field_op(pa::OP_FQ_MUL, a, b, out, nullptr, n, 48, 48, 0);
+}
+int pa_fq_square_batch(const pa_fq* a, pa_fq* out, size_t n) {
+    return host_field_op(pa::OP_FQ_SQR, a, nullptr, out, nullptr, n, 48, 48, 0);
+}
+int pa_fq_add_batch(const pa_fq* a, const pa_fq* b, pa_fq* out, size_t n) {
+    return host_field_op(pa::OP_FQ_ADD, a, b, out, nullptr, n, 48, 48, 0);
+}
+int pa_fq_sub_batch(const pa_fq* a, const pa_fq* b, pa_fq* out, size_t n) {
+    return host_field_op(pa::OP_FQ_SUB, a, b, out, nullptr, n, 48, 48, 0);
+}
+int pa_fq_inverse_batch(const pa_fq* a, pa_fq* out, uint8_t* ok, size_t n) {
+    if (n && !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null ok");
+    return host_field_op(pa::OP_FQ_INV, a, nullptr, out, ok, n, 48, 48, 0);
+}
+int pa_fq2_mul_batch(const pa_fq2* a, const pa_fq2* b, pa_fq2* out, size_t n) {
+    return host_field_op(pa::OP_FQ2_MUL, a, b, out, nullptr, n, 96, 96, 0);
+}
+int pa_fq2_square_batch(const pa_fq2* a, pa_fq2* out, size_t n) {
+    return host_field_op(pa::OP_FQ2_SQR, a, nullptr, out, nullptr, n, 96, 96, 0);
+}
+int pa_fq6_mul_batch(const pa_fq6* a, const pa_fq6* b, pa_fq6* out, size_t n) {
+    return host_field_op(pa::OP_FQ6_MUL, a, b, out, nullptr, n, 288, 288, 0);
+}
+int pa_fq12_mul_batch(const pa_fq12* a, const pa_fq12* b, pa_fq12* out, size_t n) {
+    return host_field_op(pa::OP_FQ12_MUL, a, b, out, nullptr, n, 576, 576, 0);
+}
+int pa_fq12_square_batch(const pa_fq12* a, pa_fq12* out, size_t n) {
+    return host_field_op(pa::OP_FQ12_SQR, a, nullptr, out, nullptr, n, 576, 576, 0);
+}
+int pa_fq12_inverse_batch(const pa_fq12* a, pa_fq12* out, uint8_t* ok, size_t n) {
+    if (n && !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null ok");
+    return host_field_op(pa::OP_FQ12_INV, a, nullptr, out, ok, n, 576, 576, 0);
+}
+int pa_fq12_frobenius_map_batch(const pa_fq12* a, pa_fq12* out, size_t n, size_t power) {
+    return host_field_op(pa::OP_FQ12_FROB, a, nullptr, out, nullptr, n, 576, 576, (int)(power % 12));
+}
+// not in the public header: cyclotomic squaring, exposed for the parity tests
+int pa_fq12_cyclotomic_square_batch(const pa_fq12* a, pa_fq12* out, size_t n) {
+    return host_field_op(pa::OP_FQ12_CYC_SQR, a, nullptr, out, nullptr, n, 576, 576, 0);
+}
+
+int pa_fq12_mul_by_014_batch(const pa_fq12* a, const pa_fq2* c0, const pa_fq2* c1, const pa_fq2* c4,
+                             pa_fq12* out, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!a || !c0 || !c1 || !c4 || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf da, d0, d1, d4, dout;
+    int rc;
+    if ((rc = upload(da, a, 576 * n)) || (rc = upload(d0, c0, 96 * n)) || (rc = upload(d1, c1, 96 * n)) ||
+        (rc = upload(d4, c4, 96 * n)))
+        return rc;
+    PA_TRY(dout.alloc(576 * n), "hipMalloc");
+    PA_TRY(pa::launch_fq12_mul_by_014(da.as<uint64_t>(), d0.as<uint64_t>(), d1.as<uint64_t>(), d4.as<uint64_t>(),
+                                      dout.as<uint64_t>(), n, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, 576 * n);
+}
+
+int pa_g2_prepare_batch(const pa_g2_affine* q, pa_g2_prepared* out, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!q || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf dq, dout;
+    int rc;
+    if ((rc = upload(dq, q, sizeof(pa_g2_affine) * n))) return rc;
+    PA_TRY(dout.alloc(sizeof(pa_g2_prepared) * n), "hipMalloc");
+    PA_TRY(pa::launch_g2_prepare(dq.as<uint64_t>(), dout.as<uint64_t>(), n, nullptr), "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, sizeof(pa_g2_prepared) * n);
+}
+
+int pa_miller_loop_batch(const pa_g1_affine* p, const pa_g2_prepared* q, pa_fq12* out, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!p || !q || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf dp, dq, dout;
+    int rc;
+    if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_prepared) * n)))
+        return rc;
+    PA_TRY(dout.alloc(576 * n), "hipMalloc");
+    PA_TRY(pa::launch_miller_loop_prepared(dp.as<uint64_t>(), dq.as<uint64_t>(), dout.as<uint64_t>(), n, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, 576 * n);
+}
+
+int pa_multi_miller_loop(const pa_g1_affine* p, const pa_g2_prepared* q, size_t n, pa_fq12* out) {
+    if (!out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (n == 0) {
+        // empty product: Fq12::one() (mod.rs:71 with no pairs), conjugated = one
+        memset(out, 0, sizeof(pa_fq12));
+        const uint64_t r[6] = {0x760900000002fffdULL, 0xebf4000bc40c0002ULL, 0x5f48985753c758baULL,
+                               0x77ce585370525745ULL, 0x5c071a97a256ec6dULL, 0x15f65ec3fa80e493ULL};
+        memcpy(out->c0.c0.c0.l, r, sizeof r);
+        return PA_OK;
+    }
+    if (!p || !q) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf dp, dq, dwork, dout;
+    int rc;
+    if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_prepared) * n)))
+        return rc;
+    PA_TRY(dwork.alloc(576 * n), "hipMalloc");
+    PA_TRY(dout.alloc(576), "hipMalloc");
+    PA_TRY(pa::launch_miller_loop_prepared(dp.as<uint64_t>(), dq.as<uint64_t>(), dwork.as<uint64_t>(), n, nullptr),
+           "kernel launch");
+    PA_TRY(pa::launch_fq12_product(dwork.as<uint64_t>(), n, dout.as<uint64_t>(), nullptr), "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, 576);
+}
+
+int pa_final_exponentiation_batch(const pa_fq12* in, pa_fq12* out, uint8_t* ok, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!in || !out || !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf din, dout, dok;
+    int rc;
+    if ((rc = upload(din, in, 576 * n))) return rc;
+    PA_TRY(dout.alloc(576 * n), "hipMalloc");
+    PA_TRY(dok.alloc(n), "hipMalloc");
+    PA_TRY(pa::launch_final_exponentiation(din.as<uint64_t>(), dout.as<uint64_t>(), dok.as<uint8_t>(), n, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    if ((rc = download(out, dout, 576 * n))) return rc;
+    return download(ok, dok, n);
+}
+
+int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!p || !q || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf dp, dq, dml, dout;
+    int rc;
+    if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_affine) * n)))
+        return rc;
+    PA_TRY(dml.alloc(576 * n), "hipMalloc");
+    PA_TRY(dout.alloc(576 * n), "hipMalloc");
+    PA_TRY(pa::launch_miller_loop_fused(dp.as<uint64_t>(), dq.as<uint64_t>(), dml.as<uint64_t>(), n, nullptr),
+           "kernel launch");
+    // Engine::pairing unwraps: a Miller-loop value is never zero, ok is not reported
+    PA_TRY(pa::launch_final_exponentiation(dml.as<uint64_t>(), dout.as<uint64_t>(), nullptr, n, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, 576 * n);
+}
+
+// ---- device-resident variants ----
+int pa_fq_mul_batch_device(const pa_fq* a, const pa_fq* b, pa_fq* out, size_t n, void* stream) {
+    if (n && (!a || !b || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_fq_mul_batch((const uint64_t*)a, (const uint64_t*)b, (uint64_t*)out, n, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+int pa_miller_loop_fused_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n,
+                                      void* stream) {
+    if (n && (!p || !q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_miller_loop_fused((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n,
+                                        (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+int pa_final_exponentiation_batch_device(const pa_fq12* in, pa_fq12* out, uint8_t* ok, size_t n, void* stream) {
+    if (n && (!in || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_final_exponentiation((const uint64_t*)in, (uint64_t*)out, ok, n, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+int pa_pairing_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, pa_fq12* scratch,
+                            size_t n, void* stream) {
+    if (n && (!p || !q || !out || !scratch)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_miller_loop_fused((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)scratch, n,
+                                        (hipStream_t)stream),
+           "kernel launch");
+    PA_TRY(pa::launch_final_exponentiation((const uint64_t*)scratch, (uint64_t*)out, nullptr, n,
+                                           (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+
+}  // extern "C"

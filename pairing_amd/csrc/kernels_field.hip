@@ -1,0 +1,151 @@
+// Field-level kernels: the Fq::mul_assign batch kernel (BASELINE config 2)
+// and elementwise tower kernels used by the parity tests and the C ABI.
+//
+// Layout: every operand is the reference's in-memory order (AoS, 6 x u64
+// per Fq), read with 16-byte loads: a wave reads 64 contiguous 48-byte
+// records = 3 KiB with three dwordx4 instructions, every byte used.
+#include "launch.h"
+#include "pairing.h"
+
+namespace pa {
+
+// Fq::mul_assign over a batch, fq.rs:909-960.  Grid-stride so one launch
+// covers any n with a chip-filling grid.
+__global__ void __launch_bounds__(256) k_fq_mul_batch(const uint64_t* __restrict__ a,
+                                                       const uint64_t* __restrict__ b,
+                                                       uint64_t* __restrict__ out, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        Fq x, y, z;
+        fq_load(x, a + 6 * i);
+        fq_load(y, b + 6 * i);
+        fq_mul(z, x, y);
+        fq_store(out + 6 * i, z);
+    }
+}
+
+template <int OP>
+__global__ void __launch_bounds__(64) k_field_op(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
+                                                 uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                 size_t n, int param) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if constexpr (OP == OP_FQ_MUL || OP == OP_FQ_ADD || OP == OP_FQ_SUB) {
+        Fq x, y, z;
+        fq_load(x, a + 6 * i);
+        fq_load(y, b + 6 * i);
+        if constexpr (OP == OP_FQ_MUL) fq_mul(z, x, y);
+        if constexpr (OP == OP_FQ_ADD) fq_add(z, x, y);
+        if constexpr (OP == OP_FQ_SUB) fq_sub(z, x, y);
+        fq_store(out + 6 * i, z);
+    } else if constexpr (OP == OP_FQ_SQR || OP == OP_FQ_INV) {
+        Fq x, z;
+        fq_load(x, a + 6 * i);
+        if constexpr (OP == OP_FQ_SQR) fq_sqr(z, x);
+        if constexpr (OP == OP_FQ_INV) {
+            bool k = fq_inv(z, x);
+            if (!k) fq_zero(z);
+            ok[i] = k ? 1 : 0;
+        }
+        fq_store(out + 6 * i, z);
+    } else if constexpr (OP == OP_FQ2_MUL || OP == OP_FQ2_SQR) {
+        Fq2 x, y, z;
+        load(x, a + 12 * i);
+        if constexpr (OP == OP_FQ2_MUL) {
+            load(y, b + 12 * i);
+            mul(z, x, y);
+        } else {
+            sqr(z, x);
+        }
+        store(out + 12 * i, z);
+    } else if constexpr (OP == OP_FQ6_MUL) {
+        Fq6 x, y, z;
+        load(x, a + 36 * i);
+        load(y, b + 36 * i);
+        mul(z, x, y);
+        store(out + 36 * i, z);
+    } else {
+        Fq12 x, z;
+        load(x, a + 72 * i);
+        if constexpr (OP == OP_FQ12_MUL) {
+            Fq12 y;
+            load(y, b + 72 * i);
+            mul(z, x, y);
+        } else if constexpr (OP == OP_FQ12_SQR) {
+            sqr(z, x);
+        } else if constexpr (OP == OP_FQ12_INV) {
+            bool k = inverse(z, x);
+            if (!k) { zero(z.c0); zero(z.c1); }
+            ok[i] = k ? 1 : 0;
+        } else if constexpr (OP == OP_FQ12_FROB) {
+            frobenius_map(z, x, param);
+        } else if constexpr (OP == OP_FQ12_CYC_SQR) {
+            cyclotomic_sqr(z, x);
+        }
+        store(out + 72 * i, z);
+    }
+}
+
+__global__ void __launch_bounds__(64) k_fq12_mul_by_014(const uint64_t* __restrict__ a,
+                                                        const uint64_t* __restrict__ c0,
+                                                        const uint64_t* __restrict__ c1,
+                                                        const uint64_t* __restrict__ c4,
+                                                        uint64_t* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fq12 x, z;
+    Fq2 d0, d1, d4;
+    load(x, a + 72 * i);
+    load(d0, c0 + 12 * i);
+    load(d1, c1 + 12 * i);
+    load(d4, c4 + 12 * i);
+    mul_by_014(z, x, d0, d1, d4);
+    store(out + 72 * i, z);
+}
+
+static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
+                               hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    // 256 CUs x 8 blocks of 256 threads, grid-stride beyond that
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(k_fq_mul_batch, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_field_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, uint8_t* ok,
+                           size_t n, int param, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const dim3 g(blocks_for(n, 64)), bl(64);
+    switch (op) {
+#define PA_CASE(OPV) \
+    case OPV: hipLaunchKernelGGL(k_field_op<OPV>, g, bl, 0, stream, a, b, out, ok, n, param); break;
+        PA_CASE(OP_FQ_MUL)
+        PA_CASE(OP_FQ_SQR)
+        PA_CASE(OP_FQ_ADD)
+        PA_CASE(OP_FQ_SUB)
+        PA_CASE(OP_FQ_INV)
+        PA_CASE(OP_FQ2_MUL)
+        PA_CASE(OP_FQ2_SQR)
+        PA_CASE(OP_FQ6_MUL)
+        PA_CASE(OP_FQ12_MUL)
+        PA_CASE(OP_FQ12_SQR)
+        PA_CASE(OP_FQ12_INV)
+        PA_CASE(OP_FQ12_FROB)
+        PA_CASE(OP_FQ12_CYC_SQR)
+#undef PA_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_fq12_mul_by_014(const uint64_t* a, const uint64_t* c0, const uint64_t* c1,
+                                  const uint64_t* c4, uint64_t* out, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fq12_mul_by_014, dim3(blocks_for(n, 64)), dim3(64), 0, stream, a, c0, c1, c4, out, n);
+    return hipGetLastError();
+}
+
+}  // namespace pa

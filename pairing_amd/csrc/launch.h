@@ -1,0 +1,47 @@
+// Internal host-side launchers shared between the kernel translation units
+// and the C ABI (capi.hip).  All pointers are device pointers; all launches
+// are asynchronous on `stream`.  Sizes are element counts.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace pa {
+
+enum FieldOp : int {
+    OP_FQ_MUL = 0,
+    OP_FQ_SQR,
+    OP_FQ_ADD,
+    OP_FQ_SUB,
+    OP_FQ_INV,
+    OP_FQ2_MUL,
+    OP_FQ2_SQR,
+    OP_FQ6_MUL,
+    OP_FQ12_MUL,
+    OP_FQ12_SQR,
+    OP_FQ12_INV,
+    OP_FQ12_FROB,
+    OP_FQ12_CYC_SQR,
+};
+
+// Generic elementwise field op: out[i] = op(a[i], b[i]); `ok` (may be null)
+// receives the Option flag of inversions; `param` is the Frobenius power.
+hipError_t launch_field_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, uint8_t* ok,
+                           size_t n, int param, hipStream_t stream);
+hipError_t launch_fq12_mul_by_014(const uint64_t* a, const uint64_t* c0, const uint64_t* c1,
+                                  const uint64_t* c4, uint64_t* out, size_t n, hipStream_t stream);
+// Fq::mul_assign batch, 6 x u64 AoS in and out (config 2 kernel)
+hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
+                               hipStream_t stream);
+
+hipError_t launch_g2_prepare(const uint64_t* q_aff, uint64_t* prepared, size_t n, hipStream_t stream);
+hipError_t launch_miller_loop_prepared(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out,
+                                       size_t n, hipStream_t stream);
+hipError_t launch_miller_loop_fused(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+                                    hipStream_t stream);
+hipError_t launch_final_exponentiation(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
+                                       hipStream_t stream);
+// out[0] = prod_i in[i] (Fq12), in-place tree reduction over `work` (n entries, clobbered)
+hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
+
+}  // namespace pa

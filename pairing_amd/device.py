@@ -1,0 +1,54 @@
+"""Device-resident entry points over torch tensors (HBM in, HBM out).
+
+torch is plumbing here: it owns the device allocations and the stream; the
+work is the C ABI's `_device` functions (HIP kernels) enqueued on that
+stream.  Tensors hold the raw ABI records as int64 words (torch has no full
+uint64 support), shape (n, words) exactly as the numpy layer.
+"""
+import ctypes
+
+import torch
+
+from ._native import W_FQ, W_FQ12, W_G1A, W_G2A, call
+
+
+def _stream_ptr(stream):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _dptr(t, width, name):
+    if not t.is_cuda or not t.is_contiguous() or t.dtype != torch.int64:
+        raise ValueError("%s must be a contiguous int64 CUDA tensor" % name)
+    if t.dim() != 2 or t.shape[1] != width:
+        raise ValueError("%s must have shape (n, %d), got %s" % (name, width, tuple(t.shape)))
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def empty_records(n, width, device):
+    return torch.empty((n, width), dtype=torch.int64, device=device)
+
+
+def fq_mul(a, b, out, stream=None):
+    """Fq::mul_assign over a batch resident in HBM (BASELINE config 2)."""
+    n = a.shape[0]
+    call("pa_fq_mul_batch_device", _dptr(a, W_FQ, "a"), _dptr(b, W_FQ, "b"), _dptr(out, W_FQ, "out"), n,
+         _stream_ptr(stream))
+
+
+def miller_loop(p, q, out, stream=None):
+    """Fused-prepare single-pair Miller loops: out[i] = miller_loop([(p[i], q[i].prepare())])."""
+    call("pa_miller_loop_fused_batch_device", _dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"),
+         _dptr(out, W_FQ12, "out"), p.shape[0], _stream_ptr(stream))
+
+
+def final_exponentiation(f, out, ok=None, stream=None):
+    okp = ctypes.c_void_p(ok.data_ptr()) if ok is not None else ctypes.c_void_p(0)
+    call("pa_final_exponentiation_batch_device", _dptr(f, W_FQ12, "f"), _dptr(out, W_FQ12, "out"), okp,
+         f.shape[0], _stream_ptr(stream))
+
+
+def pairing(p, q, out, scratch, stream=None):
+    """out[i] = e(p[i], q[i]) for a batch resident in HBM (BASELINE config 4)."""
+    call("pa_pairing_batch_device", _dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"), _dptr(out, W_FQ12, "out"),
+         _dptr(scratch, W_FQ12, "scratch"), p.shape[0], _stream_ptr(stream))

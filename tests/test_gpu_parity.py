@@ -1,0 +1,185 @@
+"""GPU parity: every HIP kernel behind the C ABI against the C oracle
+(oracle/, the restatement of the reference) on identical seeded inputs.
+The bar is bit-exact: all of this is integer arithmetic with canonical
+(fully reduced) outputs."""
+import numpy as np
+import pytest
+
+from helpers import (Q, R_ORDER, RMONT, fq12_one, hexlimbs, limbs, load_json, random_fq, random_scalars,
+                     relic_fq12, rng, set_infinity, small_scalars)
+
+pytestmark = pytest.mark.gpu
+
+NT = 8  # oracle threads for the larger reference computations
+
+
+def _edge_fq():
+    vals = [0, 1, 2, Q - 1, Q - 2, (Q - 1) // 2, RMONT, (1 << 380) - 1]
+    return np.array([limbs(v % Q) for v in vals], dtype=np.uint64)
+
+
+def _fq_inputs(seed, n):
+    g = rng(seed)
+    a = np.concatenate([_edge_fq(), random_fq(g, n)])
+    b = np.concatenate([_edge_fq()[::-1], random_fq(g, n)])
+    return a, b
+
+
+def test_fq_mul_matches_oracle(gpu, oracle):
+    a, b = _fq_inputs(1, 4096)
+    np.testing.assert_array_equal(gpu.fq_mul(a, b), oracle.fq_mul(a, b))
+
+
+def test_fq_mul_reference_kat(gpu):
+    # test_fq_mul_assign, fq.rs:2558-2584 (raw Montgomery limbs)
+    kat = [hexlimbs(v) for v in load_json("kat_limbs.json")["test_fq_mul_assign"]]
+    a = np.array([kat[0]], np.uint64)
+    b = np.array([kat[1]], np.uint64)
+    np.testing.assert_array_equal(gpu.fq_mul(a, b)[0], np.array(kat[2], np.uint64))
+
+
+def test_fq_square_add_sub_match_oracle(gpu, oracle):
+    a, b = _fq_inputs(2, 2048)
+    np.testing.assert_array_equal(gpu.fq_square(a), oracle.fq_square(a))
+    np.testing.assert_array_equal(gpu.fq_add(a, b), oracle.fq_add(a, b))
+    np.testing.assert_array_equal(gpu.fq_sub(a, b), oracle.fq_sub(a, b))
+
+
+def test_fq_inverse_matches_oracle(gpu, oracle):
+    a, _ = _fq_inputs(3, 256)
+    got, ok = gpu.fq_inverse(a)
+    exp, eok = oracle.fq_inverse(a)
+    np.testing.assert_array_equal(ok, eok.astype(bool))
+    assert not ok[0]  # inverse of zero is None (fq.rs:850-851)
+    np.testing.assert_array_equal(got[ok], exp[ok])
+
+
+def _rand_tower(seed, n, width):
+    g = rng(seed)
+    return random_fq(g, n * width // 6).reshape(n, width)
+
+
+def test_fq2_ops_match_oracle(gpu, oracle):
+    a = _rand_tower(4, 1024, 12)
+    b = _rand_tower(5, 1024, 12)
+    np.testing.assert_array_equal(gpu.fq2_mul(a, b), oracle.fq2_mul(a, b))
+    np.testing.assert_array_equal(gpu.fq2_square(a), oracle.fq2_square(a))
+
+
+def test_fq6_fq12_mul_square_match_oracle(gpu, oracle):
+    a6, b6 = _rand_tower(6, 256, 36), _rand_tower(7, 256, 36)
+    np.testing.assert_array_equal(gpu.fq6_mul(a6, b6), oracle.fq6_mul(a6, b6))
+    a, b = _rand_tower(8, 256, 72), _rand_tower(9, 256, 72)
+    np.testing.assert_array_equal(gpu.fq12_mul(a, b), oracle.fq12_mul(a, b))
+    np.testing.assert_array_equal(gpu.fq12_square(a), oracle.fq12_square(a))
+
+
+def test_fq12_inverse_frobenius_match_oracle(gpu, oracle):
+    a = _rand_tower(10, 64, 72)
+    a[3] = 0  # zero has no inverse
+    got, ok = gpu.fq12_inverse(a)
+    exp, eok = oracle.fq12_inverse(a)
+    np.testing.assert_array_equal(ok, eok.astype(bool))
+    assert not ok[3]
+    np.testing.assert_array_equal(got[ok], exp[ok])
+    for power in range(12):
+        np.testing.assert_array_equal(gpu.fq12_frobenius_map(a, power), oracle.fq12_frobenius(a, power))
+
+
+def test_fq12_mul_by_014_matches_oracle(gpu, oracle):
+    a = _rand_tower(11, 256, 72)
+    c0, c1, c4 = (_rand_tower(s, 256, 12) for s in (12, 13, 14))
+    np.testing.assert_array_equal(gpu.fq12_mul_by_014(a, c0, c1, c4), oracle.fq12_mul_by_014(a, c0, c1, c4))
+
+
+def _cyclotomic(oracle, f):
+    """f^((q^6-1)(q^2+1)): the easy part of mod.rs:105-114."""
+    inv, ok = oracle.fq12_inverse(f)
+    conj = f.copy()
+    conj[:, 36:] = oracle.fq_sub(np.zeros((f.shape[0] * 6, 6), np.uint64),
+                                 f[:, 36:].reshape(-1, 6)).reshape(-1, 36)
+    r = oracle.fq12_mul(conj, inv)
+    return oracle.fq12_mul(oracle.fq12_frobenius(r, 2), r)
+
+
+def test_cyclotomic_square_equals_square_in_subgroup(gpu, oracle):
+    f = _cyclotomic(oracle, _rand_tower(15, 128, 72))
+    np.testing.assert_array_equal(gpu.fq12_cyclotomic_square(f), oracle.fq12_square(f))
+
+
+def _points(seed, n, inf_every=0):
+    g = rng(seed)
+    s1 = random_scalars(g, n)
+    s2 = random_scalars(g, n)
+    return s1, s2
+
+
+@pytest.fixture(scope="module")
+def pairs(oracle):
+    s1, s2 = _points(21, 96)
+    p = oracle.g1_mul_generator(s1, NT)
+    q = oracle.g2_mul_generator(s2, NT)
+    # sprinkle infinity on either side (mod.rs:50-54)
+    set_infinity(p, [5, 40])
+    set_infinity(q, [17, 40, 77])
+    return p, q
+
+
+def test_g2_prepare_matches_oracle_bit_exact(gpu, oracle, pairs):
+    _, q = pairs
+    np.testing.assert_array_equal(gpu.g2_prepare(q), oracle.g2_prepare(q, NT))
+
+
+def test_miller_loop_batch_matches_oracle(gpu, oracle, pairs):
+    p, q = pairs
+    prep = oracle.g2_prepare(q, NT)
+    np.testing.assert_array_equal(gpu.miller_loop_batch(p, prep), oracle.miller_loop_batch(p, prep, NT))
+
+
+def test_multi_miller_loop_is_product(gpu, oracle, pairs):
+    p, q = pairs
+    prep = oracle.g2_prepare(q[:9], NT)
+    exp = oracle.miller_loop(p[:9], prep)
+    np.testing.assert_array_equal(gpu.multi_miller_loop(p[:9], prep), exp)
+    # empty product is one
+    np.testing.assert_array_equal(gpu.multi_miller_loop(p[:0], prep[:0]), fq12_one()[0])
+
+
+def test_final_exponentiation_matches_oracle(gpu, oracle, pairs):
+    p, q = pairs
+    f = oracle.miller_loop_batch(p[:32], oracle.g2_prepare(q[:32], NT), NT)
+    f[7] = 0  # final_exponentiation(0) is None (mod.rs:108, 157-158)
+    got, ok = gpu.final_exponentiation(f)
+    exp, eok = oracle.final_exponentiation(f, NT)
+    np.testing.assert_array_equal(ok, eok.astype(bool))
+    assert not ok[7] and ok.sum() == 31
+    np.testing.assert_array_equal(got[ok], exp[ok])
+
+
+def test_pairing_matches_oracle(gpu, oracle, pairs):
+    p, q = pairs
+    np.testing.assert_array_equal(gpu.pairing(p, q), oracle.pairing(p, q, NT))
+
+
+def test_pairing_relic_kat(gpu, oracle):
+    one = small_scalars([1])
+    p = oracle.g1_mul_generator(one)
+    q = oracle.g2_mul_generator(one)
+    np.testing.assert_array_equal(gpu.pairing(p, q), relic_fq12())
+
+
+def test_pairing_bilinearity(gpu, oracle):
+    # e(aP, bQ) == e(abP, Q) == e(P, abQ) (engine.rs:93-126), all on the GPU
+    g = rng(33)
+    a = random_scalars(g, 16)
+    b = random_scalars(g, 16)
+    ab = np.array([limbs(
+        (int(sum(int(x) << (64 * i) for i, x in enumerate(a[k])))
+         * int(sum(int(x) << (64 * i) for i, x in enumerate(b[k])))) % R_ORDER, 4) for k in range(16)],
+        np.uint64)
+    one = np.tile(small_scalars([1]), (16, 1))
+    e1 = gpu.pairing(oracle.g1_mul_generator(a, NT), oracle.g2_mul_generator(b, NT))
+    e2 = gpu.pairing(oracle.g1_mul_generator(ab, NT), oracle.g2_mul_generator(one, NT))
+    e3 = gpu.pairing(oracle.g1_mul_generator(one, NT), oracle.g2_mul_generator(ab, NT))
+    np.testing.assert_array_equal(e1, e2)
+    np.testing.assert_array_equal(e1, e3)

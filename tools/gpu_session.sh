@@ -1,0 +1,37 @@
+#!/bin/bash
+# One GPU-box session: each GPU step under its own time limit; a fault,
+# abort, segfault or timeout ends the session (no further GPU work), a plain
+# test failure (exit 1) does not.  Usage: tools/gpu_session.sh STEP...
+#   steps: valu | tests | smoke | bench | prof | pmc | fqbench
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name limit cmd...
+    local name=$1 limit=$2
+    shift 2
+    echo "=== $name: $*" | tee -a gpurun_out/session.log
+    local t0=$(date +%s)
+    timeout -k 10 "$limit" "$@" > "gpurun_out/$name.txt" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc ($(( $(date +%s) - t0 )) s)" | tee -a gpurun_out/session.log
+    tail -5 "gpurun_out/$name.txt"
+    case $rc in
+        0|1) return 0 ;;
+        *) echo "=== stopping after $name (rc=$rc)" | tee -a gpurun_out/session.log; exit $rc ;;
+    esac
+}
+for step in "$@"; do
+    case $step in
+        valu) run valu 120 ./tools/valu_rates ;;
+        tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        alltests) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run bench 600 python bench.py ;;
+        fqbench) run bench_fq 300 python bench.py --workload fq_mul --steps 20 --warmup 3 --no-cpu-baseline ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        proffq) run prof_fq 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fq -o run -- python bench.py --workload fq_mul --steps 10 --warmup 2 --no-cpu-baseline ;;
+        pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline &&
+             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
