@@ -1,0 +1,76 @@
+"""Multi-GPU sharding of a pairing batch.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm).
+Pairings are independent, so a global batch is split into contiguous shards,
+one per rank, with no collective on the data path; the only exchange is a
+single gather of the Fq12 results to the root.  For the trait's multi-pair
+semantics (Engine::miller_loop over all pairs = the product of per-pair
+Miller values, mod.rs:40-102) each rank reduces its shard to one Fq12 and
+the root gathers 576 B per rank.
+
+The functions are backend-agnostic (they take the local compute as a
+callable and use torch.distributed collectives), so the same code path runs
+with RCCL on MI355X and with gloo on CPU in tests/test_distributed.py.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n, world, rank):
+    """Contiguous [start, stop) of rank's shard: sizes differ by at most one."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank %d/%d" % (world, rank))
+    base, rem = divmod(n, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def gather_rows_to_root(local, n_global, root=0, group=None):
+    """Gather every rank's (n_r, w) row block to `root` in rank order.
+    Ragged shards are padded to the largest shard for the collective.
+    Returns the (n_global, w) tensor on root, None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = [b - a for a, b in (shard_range(n_global, world, r) for r in range(world))]
+    width = local.shape[1]
+    cap = max(sizes)
+    if local.shape[0] != sizes[rank]:
+        raise ValueError("rank %d holds %d rows, shard is %d" % (rank, local.shape[0], sizes[rank]))
+    send = local
+    if local.shape[0] < cap:
+        send = torch.zeros((cap, width), dtype=local.dtype, device=local.device)
+        send[:local.shape[0]] = local
+    bufs = [torch.empty((cap, width), dtype=local.dtype, device=local.device) for _ in range(world)] \
+        if rank == root else None
+    dist.gather(send.contiguous(), bufs, dst=root, group=group)
+    if rank != root:
+        return None
+    return torch.cat([bufs[r][:sizes[r]] for r in range(world)], dim=0)
+
+
+def sharded_batch(p, q, compute, root=0, group=None):
+    """out[i] = compute(p, q)[i] over the global batch, sharded across ranks.
+
+    p, q: the full global batch on every rank (each rank reads only its
+    shard), compute: (p_shard, q_shard) -> (n_shard, w) tensor on this rank's
+    device.  Returns the (n, w) result on root, None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    a, b = shard_range(p.shape[0], world, rank)
+    local = compute(p[a:b], q[a:b])
+    return gather_rows_to_root(local, p.shape[0], root=root, group=group)
+
+
+def sharded_product(p, q, local_product, combine, root=0, group=None):
+    """The multi-pair Miller loop across ranks: each rank reduces its shard to
+    one Fq12 with `local_product(p_shard, q_shard) -> (1, 72)`, the root
+    gathers one row per rank and folds them with `combine((world, 72)) -> (1, 72)`."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    a, b = shard_range(p.shape[0], world, rank)
+    local = local_product(p[a:b], q[a:b])
+    rows = [torch.empty_like(local) for _ in range(world)] if rank == root else None
+    dist.gather(local.contiguous(), rows, dst=root, group=group)
+    if rank != root:
+        return None
+    return combine(torch.cat(rows, dim=0))

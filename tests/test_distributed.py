@@ -1,0 +1,86 @@
+"""The multi-rank path (pairing_amd/shard.py) with world_size 2 on CPU (gloo):
+sharded batch == unsharded batch, sharded multi-pair product == single
+product, ragged shards handled.  The per-rank compute is the oracle here
+(CPU); on MI355X the same code runs with RCCL and the HIP kernels
+(bench.py --gpus N)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pairing_amd.shard import shard_range
+
+
+def test_shard_range_covers_exactly():
+    for n in (0, 1, 7, 64, 65536, 65537):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from oracle import binding as oracle
+    from pairing_amd.shard import sharded_batch, sharded_product
+
+    d = np.load(os.path.join(root, "tests", "golden", "bench_points.npz"))
+    p = torch.from_numpy(d["g1"][:n].view(np.int64).copy())
+    q = torch.from_numpy(d["g2"][:n].view(np.int64).copy())
+
+    def compute(ps, qs):
+        out = oracle.pairing(ps.numpy().view(np.uint64), qs.numpy().view(np.uint64), 2)
+        return torch.from_numpy(out.view(np.int64))
+
+    def local_product(ps, qs):
+        prep = oracle.g2_prepare(qs.numpy().view(np.uint64))
+        f = oracle.miller_loop(ps.numpy().view(np.uint64).copy(), prep)
+        return torch.from_numpy(f.reshape(1, 72).view(np.int64).copy())
+
+    def combine(rows):
+        acc = rows[0:1].numpy().view(np.uint64)
+        for r in range(1, rows.shape[0]):
+            acc = oracle.fq12_mul(acc, rows[r:r + 1].numpy().view(np.uint64).copy())
+        return torch.from_numpy(acc.view(np.int64))
+
+    out = sharded_batch(p, q, compute)
+    prod = sharded_product(p, q, local_product, combine)
+    if rank == 0:
+        np.savez(result_path, out=out.numpy(), prod=prod.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [8, 11])  # even and ragged shards
+def test_sharded_pairing_world2_gloo(tmp_path, oracle, n):
+    world = 2
+    path = str(tmp_path / "res.npz")
+    mp.spawn(_worker, args=(world, _free_port(), n, path), nprocs=world, join=True)
+    res = np.load(path)
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "bench_points.npz"))
+    p, q = d["g1"][:n].copy(), d["g2"][:n].copy()
+    np.testing.assert_array_equal(res["out"].view(np.uint64), oracle.pairing(p, q, 4))
+    single = oracle.miller_loop(p, oracle.g2_prepare(q))
+    np.testing.assert_array_equal(res["prod"].view(np.uint64)[0], single)
