@@ -13,7 +13,7 @@
 // them.  That keeps the code footprint of the pairing kernels inside the
 // instruction cache while each call still does ~2k VALU instructions.
 #pragma once
-#include "fq.h"
+#include "fq_mul_gen.h"
 #include "bls_consts.h"
 
 #define PA_NOINLINE __device__ __noinline__
@@ -44,30 +44,26 @@ PA_DEV void mul_by_nonresidue(Fq2& r, const Fq2& a) {
 }
 // Karatsuba, fq2.rs:123-136 (3 Fq multiplies)
 PA_NOINLINE void mul(Fq2& r, const Fq2& a, const Fq2& b) {
-    Fq aa, bb, o, s;
-    fq_mul(aa, a.c0, b.c0);
-    fq_mul(bb, a.c1, b.c1);
+    Fq aa, bb, o, s, x;
     fq_add(o, b.c0, b.c1);
     fq_add(s, a.c1, a.c0);
-    fq_mul(s, s, o);
-    fq_sub(s, s, aa);
+    fq_mul_x3(aa, a.c0, b.c0, bb, a.c1, b.c1, x, s, o);
+    fq_sub(s, x, aa);
     fq_sub(r.c1, s, bb);
     fq_sub(r.c0, aa, bb);
 }
 // complex squaring, fq2.rs:87-101 (2 Fq multiplies)
 PA_NOINLINE void sqr(Fq2& r, const Fq2& a) {
-    Fq ab, c0c1, c0;
-    fq_mul(ab, a.c0, a.c1);
+    Fq ab, c0c1, c0m, c0;
     fq_add(c0c1, a.c0, a.c1);
-    fq_sub(c0, a.c0, a.c1);
-    fq_mul(c0, c0, c0c1);
+    fq_sub(c0m, a.c0, a.c1);
+    fq_mul_x2(ab, a.c0, a.c1, c0, c0m, c0c1);
     fq_dbl(r.c1, ab);
     r.c0 = c0;
 }
 // Fq2 x Fq (used by ell, mod.rs:61-65)
 PA_DEV void mul_by_fq(Fq2& r, const Fq2& a, const Fq& b) {
-    fq_mul(r.c0, a.c0, b);
-    fq_mul(r.c1, a.c1, b);
+    fq_mul_x2(r.c0, a.c0, b, r.c1, a.c1, b);
 }
 PA_DEV void frobenius_map(Fq2& r, const Fq2& a, int power) {  // fq2.rs:157-159
     Fq c;

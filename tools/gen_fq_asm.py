@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Generate pairing_amd/csrc/fq_mul_gen.h: hazard-free product-scanning (FIPS)
+Montgomery multiplication for gfx950 with the v_mad_u64_u32 carry-out.
+
+Why generated: each 32x32 product is `v_mad_u64_u32 acc, c, x, y, acc`
+(carry-out to an SGPR pair) + `v_addc_co_u32 ov, c, 0, ov, c`, 2 VALU
+instructions against ~4.5 for the compiler's CIOS lowering.  gfx950 needs
+one wait state between a VALU writing a carry SGPR and the VALU reading it
+(hipcc pads its own carry chains with `s_nop 0`), so products of N >= 2
+independent chains are interleaved round-robin, each chain with its own
+carry pair: every carry read is >= 1 instruction after its write.  hipcc
+pads one `s_nop 0` after every asm statement, so each statement carries
+up to PER_BLOCK products per chain.  Asm statements stay small (< 40
+operands): very large operand lists make the register allocator blow up.
+
+Functions:
+  fq_mul_x1(r, a, b)               one product, split into an a*b chain and
+                                   an m*q chain merged once per column
+  fq_mul_x2(r0,a0,b0, r1,a1,b1)    two independent products
+  fq_mul_x3(r0,a0,b0, ..., r2,a2,b2)
+All return canonical (< q) Montgomery products, bit-identical to
+Fq::mul_assign (fq.rs:909-960).
+"""
+import os
+
+PER_BLOCK = 4
+
+
+def block(chains, prods):
+    """prods: list of (chain, x_expr, y_expr, y_is_sgpr) for one asm statement."""
+    text = []
+    used = sorted({c for c, *_ in prods})
+    # outputs: acc_c (+v 64), ov_c (+v), carry_c (=&s 64)
+    out_list = []
+    for c in used:
+        out_list.append(('"+v"', "acc%s" % chains[c]))
+        out_list.append(('"+v"', "ov%s" % chains[c]))
+    for c in used:
+        out_list.append(('"=&s"', "cf%s" % chains[c]))
+    in_list = []
+    in_index = {}
+
+    def inp(cons, expr):
+        k = (cons, expr)
+        if k not in in_index:
+            in_index[k] = len(out_list) + len(in_list)
+            in_list.append(k)
+        return in_index[k]
+
+    oidx = {e: i for i, (_, e) in enumerate(out_list)}
+    by_chain = {c: [p for p in prods if p[0] == c] for c in used}
+    rounds = max(len(v) for v in by_chain.values())
+    for r in range(rounds):
+        live = [c for c in used if r < len(by_chain[c])]
+        for c in live:
+            _, x, y, ys = by_chain[c][r]
+            xi = inp('"v"', x)
+            yi = inp('"s"' if ys else '"v"', y)
+            text.append("v_mad_u64_u32 %%%d, %%%d, %%%d, %%%d, %%%d" % (
+                oidx["acc%s" % chains[c]], oidx["cf%s" % chains[c]], xi, yi, oidx["acc%s" % chains[c]]))
+        if len(live) == 1:
+            text.append("s_nop 0")  # lone chain: pad the carry hazard ourselves
+        for c in live:
+            text.append("v_addc_co_u32 %%%d, %%%d, 0, %%%d, %%%d" % (
+                oidx["ov%s" % chains[c]], oidx["cf%s" % chains[c]], oidx["ov%s" % chains[c]],
+                oidx["cf%s" % chains[c]]))
+    asm = "\\n\\t".join(text)
+    outs_s = ", ".join("%s(%s)" % (k, e) for k, e in out_list)
+    ins_s = ", ".join("%s(%s)" % (k, e) for k, e in in_list)
+    return '    asm("%s"\n        : %s\n        : %s);' % (asm, outs_s, ins_s)
+
+
+def gen(n_chains, name):
+    ids = [str(i) for i in range(n_chains)]
+    split = n_chains == 1  # x1: chain "0" = a*b products, chain "B" = m*q products
+    chains = ids + (["B"] if split else [])
+    args = ", ".join("Fq& r%s, const Fq& a%s, const Fq& b%s" % (i, i, i) for i in ids)
+    L = ["PA_DEV void %s(%s) {" % (name, args)]
+    for i in ids:
+        L.append("    uint32_t m%s[12], t%s[12];" % (i, i))
+    for c in chains:
+        L.append("    uint64_t acc%s = 0, cf%s;" % (c, c))
+        L.append("    uint32_t ov%s = 0;" % c)
+    for k in range(23):
+        prods = []
+        for ci, i in enumerate(ids):
+            ab = [(ci, "a%s.w[%d]" % (i, j), "b%s.w[%d]" % (i, k - j), False)
+                  for j in range(max(0, k - 11), min(k, 11) + 1)]
+            mq = [(ci if not split else 1, "m%s[%d]" % (i, j), "PA_Q%d" % (k - j), True)
+                  for j in range(max(0, k - 11), min(k - 1, 11) + 1)]
+            prods.append(ab + mq)
+        # interleave: emit blocks of PER_BLOCK products per chain
+        if split:
+            flat = prods[0]
+            per = {0: [p for p in flat if p[0] == 0], 1: [p for p in flat if p[0] == 1]}
+        else:
+            per = {ci: prods[ci] for ci in range(n_chains)}
+        nblocks = max((len(v) + PER_BLOCK - 1) // PER_BLOCK for v in per.values())
+        for b in range(nblocks):
+            bp = []
+            for ci, v in per.items():
+                bp += v[b * PER_BLOCK:(b + 1) * PER_BLOCK]
+            if bp:
+                L.append(block(chains, bp))
+        if split:
+            # merge the m*q accumulator into the a*b accumulator (96-bit add)
+            L.append("    { uint64_t s = acc0 + accB; ov0 += ovB + (uint32_t)(s < acc0); acc0 = s; accB = 0; ovB = 0; }")
+        if k < 12:
+            for i in ids:
+                L.append("    m%s[%d] = (uint32_t)acc%s * PA_INV32;" % (i, k, i))
+            L.append(block(chains, [(ci, "m%s[%d]" % (i, k), "PA_Q0", True) for ci, i in enumerate(ids)]))
+        else:
+            for i in ids:
+                L.append("    t%s[%d] = (uint32_t)acc%s;" % (i, k - 12, i))
+        for i in ids:
+            L.append("    acc%s = (acc%s >> 32) | ((uint64_t)ov%s << 32); ov%s = 0;" % (i, i, i, i))
+    for i in ids:
+        L.append("    t%s[11] = (uint32_t)acc%s;" % (i, i))
+        L.append("    fq_reduce_once(r%s, t%s);" % (i, i))
+    L.append("}")
+    return "\n".join(L)
+
+
+def main():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = os.path.join(root, "pairing_amd", "csrc", "fq_mul_gen.h")
+    body = [
+        "// GENERATED by tools/gen_fq_asm.py -- do not edit.",
+        "// Hazard-free FIPS Montgomery multiplication on v_mad_u64_u32 carry-out (see the generator).",
+        "#pragma once",
+        '#include "fq.h"',
+        "namespace pa {",
+        gen(1, "fq_mul_x1"),
+        gen(2, "fq_mul_x2"),
+        gen(3, "fq_mul_x3"),
+        "PA_DEV void fq_mul(Fq& r, const Fq& a, const Fq& b) { fq_mul_x1(r, a, b); }",
+        "PA_DEV void fq_sqr(Fq& r, const Fq& a) { fq_mul_x1(r, a, a); }",
+        "}  // namespace pa",
+        "",
+    ]
+    with open(out, "w") as f:
+        f.write("\n".join(body))
+    print("wrote", out)
+
+
+if __name__ == "__main__":
+    main()
