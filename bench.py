@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 16, help="pairings per GPU per step")
-    ap.add_argument("--workload", choices=["pairing", "fq_mul"], default="pairing")
+    ap.add_argument("--workload", choices=["pairing", "fq_mul", "wnaf"], default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -94,6 +94,24 @@ def cpu_baseline_pairing(p, q, seconds):
     return {"value": n / wall, "unit": "pairings/s", "cores": threads, "kind": "port",
             "sample": "%d pairings of the same synthetic batch, C restatement of the reference "
                       "(oracle/), OpenMP over pairs, %.1f s wall" % (n, wall)}
+
+
+def cpu_baseline_wnaf(base, scalars, seconds):
+    """The reference's Wnaf (window 16 at 2^18 scalars) + batch_normalization, restated in C."""
+    from oracle import binding as oracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))
+    n = min(len(scalars), 131072)
+    t0 = time.perf_counter()
+    out = oracle.g1_wnaf_fixed_base(base, np.ascontiguousarray(scalars[:n]), threads)
+    oracle.g1_batch_normalization(out)
+    wall = time.perf_counter() - t0
+    return {"value": n / wall, "unit": "points/s", "cores": threads, "kind": "port",
+            "sample": "%d scalars, reference wNAF (window for that count) + batch_normalization, C "
+                      "restatement, OpenMP over scalars, %.1f s wall" % (n, wall)}
 
 
 def cpu_baseline_fq_mul(a, b, seconds):
@@ -150,6 +168,30 @@ def main():
             if ws > 1:
                 # the path's one exchange: every shard's Fq12 results to rank 0 (RCCL over xGMI)
                 gather_rows_to_root(out, ws * n)
+    elif args.workload == "wnaf":
+        # config 3: Wnaf::new().base(g, 2^18).scalar(s_i) + G1::batch_normalization
+        n = args.batch if args.batch != (1 << 16) else (1 << 18)
+        d = np.load(os.path.join(ROOT, "tests", "golden", "bench_points.npz"))
+        base_np = np.zeros((1, 18), np.uint64)
+        base_np[0, :12] = d["g1"][0, :12]
+        base_np[0, 12:18] = np.array([0x760900000002fffd, 0xebf4000bc40c0002, 0x5f48985753c758ba,
+                                      0x77ce585370525745, 0x5c071a97a256ec6d, 0x15f65ec3fa80e493], np.uint64)
+        s_np = np.ascontiguousarray(d["s1"][np.arange(n) % 256])
+        s_np[:, 0] ^= np.arange(n, dtype=np.uint64) << np.uint64(8)
+        base = torch.from_numpy(base_np.view(np.int64)).to(dev)
+        scal = torch.from_numpy(s_np.view(np.int64)).to(dev)
+        out = pdev.empty_records(n, 18, dev)
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            table, _ = pdev.g1_fixed_base_table(base, stream)
+            pdev.g1_fixed_base_mul(table, scal, out, stream)
+            if timed:
+                ev[1].record(stream)
+            pdev.g1_batch_normalization(out, stream)
+            if timed:
+                ev[2].record(stream)
     else:
         g = np.random.default_rng(rank)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -177,7 +219,7 @@ def main():
         # per-kernel durations from HIP events on the launch stream
         torch.cuda.synchronize()
         k_ms["a"].append(ev[0].elapsed_time(ev[1]))
-        if args.workload == "pairing":
+        if args.workload in ("pairing", "wnaf"):
             k_ms["b"].append(ev[1].elapsed_time(ev[2]))
     barrier()
     elapsed = time.perf_counter() - t0
@@ -199,6 +241,15 @@ def main():
                       "batch_per_gpu": n, "global_batch": n * ws, "parallelism": "shard%d+rccl_gather" % ws
                       if ws > 1 else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}
+        elif args.workload == "wnaf":
+            mul_ms, norm_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
+            dom_name, dom_ms, dom_bytes = ("g1_fixed_base_mul", mul_ms, 32 + 144) if mul_ms >= norm_ms else \
+                ("g1_batch_normalize", norm_ms, 144 + 144)
+            value = ws * n * args.steps / elapsed
+            metric, unit = "G1 fixed-base scalar mults + batch_normalization per second at batch 2^18", "points/s"
+            config = {"workload": "Wnaf::base(g, 2^18).scalar(s_i) then G1::batch_normalization",
+                      "batch_per_gpu": n, "global_batch": n * ws,
+                      "kernel_ms": {"table+fixed_base_mul": round(mul_ms, 3), "batch_normalize": round(norm_ms, 3)}}
         else:
             dom_name, dom_ms, dom_bytes = "fq_mul_batch", float(np.mean(k_ms["a"])), 144
             value = ws * n * args.steps / elapsed
@@ -218,6 +269,8 @@ def main():
         if not args.no_cpu_baseline and ws == 1:
             if args.workload == "pairing":
                 cpu = cpu_baseline_pairing(p_np, q_np, args.cpu_seconds)
+            elif args.workload == "wnaf":
+                cpu = cpu_baseline_wnaf(base_np, s_np, args.cpu_seconds)
             else:
                 cpu = cpu_baseline_fq_mul(a_np, b_np, args.cpu_seconds)
         line = {"metric": metric, "value": value, "unit": unit, "n_gpus": ws, "steps": args.steps,

@@ -113,7 +113,23 @@ int pa_final_exponentiation_batch(const pa_fq12 *in, pa_fq12 *out, uint8_t *ok, 
 /* Engine::pairing, lib.rs:101-109: out[i] = e(p[i], q[i]) (prepare fused on device) */
 int pa_pairing_batch(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n);
 
+/* ---- G1 (config 3: parameter generation) ---- */
+/* CurveProjective::batch_normalization, ec.rs:246-294, in place.  Zero and
+ * already-normalized points are left untouched; others get z = 1. */
+int pa_g1_batch_normalization(pa_g1 *v, size_t n);
+/* Wnaf::new().base(*base, n).scalar(scalars[i]) for every i (wnaf.rs:93-107,
+ * 169-178): out[i] = scalars[i] * base as a Jacobian point (equal as a point to
+ * the reference's; representation-independent PartialEq, ec.rs:45-85). */
+int pa_g1_wnaf_fixed_base(const pa_g1 *base, const pa_fr_repr *scalars, size_t n, pa_g1 *out);
+
 /* ---- device-resident variants (pointers are device memory) ---- */
+int pa_g1_batch_normalization_device(pa_g1 *v, size_t n, void *stream);
+/* u64 words of the fixed-base table and of the scratch used to build it */
+size_t pa_g1_fixed_base_table_words(void);
+size_t pa_g1_fixed_base_workspace_words(void);
+int pa_g1_fixed_base_table_device(const pa_g1 *base, uint64_t *table, uint64_t *workspace, void *stream);
+int pa_g1_fixed_base_mul_device(const uint64_t *table, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
+                                void *stream);
 int pa_fq_mul_batch_device(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n, void *stream);
 int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
                                       void *stream);

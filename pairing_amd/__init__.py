@@ -24,6 +24,7 @@ __all__ = [
     "fq_mul", "fq_square", "fq_add", "fq_sub", "fq_inverse",
     "fq2_mul", "fq2_square", "fq6_mul", "fq12_mul", "fq12_square", "fq12_inverse",
     "fq12_frobenius_map", "fq12_cyclotomic_square", "fq12_mul_by_014",
+    "g1_batch_normalization", "g1_wnaf_fixed_base",
     "g2_prepare", "miller_loop_batch", "multi_miller_loop", "final_exponentiation", "pairing",
 ]
 
@@ -171,4 +172,22 @@ def pairing(p, q):
         raise ValueError("p and q lengths differ")
     out = np.empty((p.shape[0], W_FQ12), np.uint64)
     call("pa_pairing_batch", ptr(p), ptr(q), ptr(out), p.shape[0])
+    return out
+
+
+# ---- G1 parameter-generation path (config 3) ----
+def g1_batch_normalization(v):
+    """CurveProjective::batch_normalization (ec.rs:246-294); returns the normalized copy."""
+    v = as_rows(v, W_G1, "v").copy()
+    call("pa_g1_batch_normalization", ptr(v), v.shape[0])
+    return v
+
+
+def g1_wnaf_fixed_base(base, scalars):
+    """Wnaf::new().base(base, n).scalar(s) for each FrRepr scalar (wnaf.rs:93-107,
+    169-178): Jacobian points equal to scalars[i] * base."""
+    b = as_rows(base, W_G1, "base")
+    s = as_rows(scalars, 4, "scalars")
+    out = np.empty((s.shape[0], W_G1), np.uint64)
+    call("pa_g1_wnaf_fixed_base", ptr(b), ptr(s), s.shape[0], ptr(out))
     return out

@@ -64,6 +64,11 @@ _SIGS = {
     "pa_multi_miller_loop": [_P, _P, _N, _P],
     "pa_final_exponentiation_batch": [_P, _P, _P, _N],
     "pa_pairing_batch": [_P, _P, _P, _N],
+    "pa_g1_batch_normalization": [_P, _N],
+    "pa_g1_wnaf_fixed_base": [_P, _P, _N, _P],
+    "pa_g1_batch_normalization_device": [_P, _N, _P],
+    "pa_g1_fixed_base_table_device": [_P, _P, _P, _P],
+    "pa_g1_fixed_base_mul_device": [_P, _P, _P, _N, _P],
     "pa_fq_mul_batch_device": [_P, _P, _P, _N, _P],
     "pa_miller_loop_fused_batch_device": [_P, _P, _P, _N, _P],
     "pa_final_exponentiation_batch_device": [_P, _P, _P, _N, _P],
@@ -74,6 +79,8 @@ for _name, _args in _SIGS.items():
     _fn.argtypes = _args
     _fn.restype = ctypes.c_int
 _lib.pa_version.restype = ctypes.c_char_p
+_lib.pa_g1_fixed_base_table_words.restype = ctypes.c_size_t
+_lib.pa_g1_fixed_base_workspace_words.restype = ctypes.c_size_t
 _lib.pa_last_error.restype = ctypes.c_char_p
 
 

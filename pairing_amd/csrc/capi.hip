@@ -252,7 +252,54 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
     return download(out, dout, 576 * n);
 }
 
+int pa_g1_batch_normalization(pa_g1* v, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!v) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf dv;
+    int rc;
+    if ((rc = upload(dv, v, sizeof(pa_g1) * n))) return rc;
+    PA_TRY(pa::launch_g1_batch_normalize(dv.as<uint64_t>(), n, nullptr), "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(v, dv, sizeof(pa_g1) * n);
+}
+
+int pa_g1_wnaf_fixed_base(const pa_g1* base, const pa_fr_repr* scalars, size_t n, pa_g1* out) {
+    if (n == 0) return PA_OK;
+    if (!base || !scalars || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf db, ds, dt, dw, dout;
+    int rc;
+    if ((rc = upload(db, base, sizeof(pa_g1))) || (rc = upload(ds, scalars, sizeof(pa_fr_repr) * n))) return rc;
+    PA_TRY(dt.alloc(8 * pa::g1_comb_table_words()), "hipMalloc");
+    PA_TRY(dw.alloc(8 * pa::g1_comb_workspace_words()), "hipMalloc");
+    PA_TRY(dout.alloc(sizeof(pa_g1) * n), "hipMalloc");
+    PA_TRY(pa::launch_g1_comb_table(db.as<uint64_t>(), dt.as<uint64_t>(), dw.as<uint64_t>(), nullptr),
+           "kernel launch");
+    PA_TRY(pa::launch_g1_comb_mul(dt.as<uint64_t>(), ds.as<uint64_t>(), dout.as<uint64_t>(), n, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, sizeof(pa_g1) * n);
+}
+
 // ---- device-resident variants ----
+int pa_g1_batch_normalization_device(pa_g1* v, size_t n, void* stream) {
+    if (n && !v) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g1_batch_normalize((uint64_t*)v, n, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
+size_t pa_g1_fixed_base_table_words(void) { return pa::g1_comb_table_words(); }
+size_t pa_g1_fixed_base_workspace_words(void) { return pa::g1_comb_workspace_words(); }
+int pa_g1_fixed_base_table_device(const pa_g1* base, uint64_t* table, uint64_t* workspace, void* stream) {
+    if (!base || !table || !workspace) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g1_comb_table((const uint64_t*)base, table, workspace, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
+int pa_g1_fixed_base_mul_device(const uint64_t* table, const pa_fr_repr* scalars, pa_g1* out, size_t n,
+                                void* stream) {
+    if (n && (!table || !scalars || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g1_comb_mul(table, (const uint64_t*)scalars, (uint64_t*)out, n, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
 int pa_fq_mul_batch_device(const pa_fq* a, const pa_fq* b, pa_fq* out, size_t n, void* stream) {
     if (n && (!a || !b || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     PA_TRY(pa::launch_fq_mul_batch((const uint64_t*)a, (const uint64_t*)b, (uint64_t*)out, n, (hipStream_t)stream),

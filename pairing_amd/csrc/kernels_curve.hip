@@ -1,0 +1,190 @@
+// G1 kernels for the parameter-generation path (BASELINE config 3):
+//   Wnaf::new().base(g, n).scalar(s_i) for n scalars   (wnaf.rs:93-107, 169-178)
+//   G1::batch_normalization(&mut out)                    (ec.rs:246-294)
+//
+// Fixed-base multiplication.  The reference recodes each scalar in wNAF with
+// window recommended_wnaf_for_num_scalars(n) (16 at n = 2^18, ec.rs:907-921)
+// against a 2^15-entry Jacobian table built by a serial add chain, then runs
+// ~255 doublings + ~16 additions per scalar.  Only the *point* s*g is
+// observable (CurveProjective's PartialEq is representation-independent,
+// ec.rs:45-85, and batch_normalization makes it canonical), so the GPU uses
+// the fixed-base algorithm that suits a wide machine: a signed base-256 comb.
+//   T[i][d] = d * 2^(8i) * g  (affine), i = 0..32, d = 1..128      (420 KB,
+//   read-only, resident in every XCD's L2)
+//   s*g = sum_i sign(d_i) T[i][|d_i|], digits d_i in [-127, 128]
+// = at most 33 mixed additions (madd-2007-bl) per scalar and no doublings,
+// against ~255 doublings + 16 additions for wNAF.
+//
+// batch_normalization.  Montgomery's trick over chunks of CHUNK points per
+// lane with one Fermat inversion per chunk; zero and already-normalized points
+// are left bit-for-bit untouched, as in the reference (ec.rs:255-257, 271, 285).
+#include "launch.h"
+#include "pairing.h"
+
+namespace pa {
+
+constexpr int kCombWindows = 33;      // 8-bit digits of a 255-bit scalar + final carry
+constexpr int kCombEntries = 128;     // |d| in 1..128
+constexpr int kG1Jac = 18;            // u64 words per Jacobian G1
+constexpr int kAffPair = 12;          // u64 words per table entry (x, y)
+constexpr int kNormChunk = 8;         // points per lane in batch_normalization
+
+// ---------------- batch_normalization ----------------
+__global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict__ v, size_t n) {
+    const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t begin = lane * kNormChunk;
+    if (begin >= n) return;
+    const int cnt = (int)((n - begin) < (size_t)kNormChunk ? (n - begin) : (size_t)kNormChunk);
+    uint64_t* base = v + begin * kG1Jac;
+    // forward pass: prod[k] = z_0 * ... * z_k over non-normalized points
+    Fq prod[kNormChunk];
+    bool skip[kNormChunk];
+    Fq acc;
+    fq_one(acc);
+#pragma unroll
+    for (int k = 0; k < kNormChunk; k++) {
+        if (k < cnt) {
+            Fq z;
+            fq_load(z, base + k * kG1Jac + 12);
+            skip[k] = fq_is_zero(z) || fq_is_one(z);
+            Fq t;
+            fq_mul(t, acc, z);
+            if (!skip[k]) acc = t;
+            prod[k] = acc;
+        } else {
+            skip[k] = true;
+        }
+    }
+    Fq inv;
+    fq_inv(inv, acc);  // acc != 0: product of nonzero z's (or one)
+    // backward pass: z_k^-1 = inv * prod[k-1]; inv *= z_k
+#pragma unroll
+    for (int k = kNormChunk - 1; k >= 0; k--) {
+        if (k < cnt && !skip[k]) {
+            Fq z, zinv, prev;
+            fq_load(z, base + k * kG1Jac + 12);
+            fq_one(prev);
+#pragma unroll
+            for (int j = 0; j < kNormChunk; j++)
+                if (j == k - 1) prev = prod[j];
+            // prod[j] for the last non-skipped j < k equals prod[k-1] (skipped entries carry acc)
+            fq_mul_x2(zinv, inv, prev, inv, inv, z);
+            Fq zz, x, y;
+            fq_sqr(zz, zinv);
+            fq_load(x, base + k * kG1Jac);
+            fq_load(y, base + k * kG1Jac + 6);
+            Fq zzz;
+            fq_mul_x2(x, x, zz, zzz, zz, zinv);
+            fq_mul(y, y, zzz);
+            Fq one;
+            fq_one(one);
+            fq_store(base + k * kG1Jac, x);
+            fq_store(base + k * kG1Jac + 6, y);
+            fq_store(base + k * kG1Jac + 12, one);
+        }
+    }
+}
+
+// ---------------- fixed-base comb ----------------
+// B_i = 2^(8i) g for i = 0..32 (Jacobian), one lane, 256 doublings.
+__global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    Jac<Fq> p;
+    load_jac(p, base);
+#pragma unroll 1
+    for (int i = 0; i < kCombWindows; i++) {
+        store_jac(bases + kG1Jac * i, p);
+#pragma unroll 1
+        for (int k = 0; k < 8; k++) jac_double(p);
+    }
+}
+
+// T[i][d-1] = d * B_i (Jacobian), one lane per entry: double-and-add over d's 8 bits.
+__global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict__ bases, uint64_t* __restrict__ table_jac) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kCombWindows * kCombEntries) return;
+    const int i = e / kCombEntries, d = e % kCombEntries + 1;
+    Jac<Fq> b, acc;
+    load_jac(b, bases + kG1Jac * i);
+    jac_zero(acc);
+#pragma unroll 1
+    for (int bit = 7; bit >= 0; bit--) {
+        jac_double(acc);
+        if ((d >> bit) & 1) jac_add(acc, b);
+    }
+    store_jac(table_jac + (size_t)kG1Jac * e, acc);
+}
+
+// normalized Jacobian table -> packed affine (x, y)
+__global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table_aff) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kCombWindows * kCombEntries) return;
+    for (int w = 0; w < kAffPair; w++) table_aff[(size_t)kAffPair * e + w] = table_jac[(size_t)kG1Jac * e + w];
+}
+
+// s*g for n scalars (FrRepr, 4 x u64 canonical): out Jacobian.
+__global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__ table_aff,
+                                                    const uint64_t* __restrict__ scalars,
+                                                    uint64_t* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t s[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
+    Jac<Fq> acc;
+    jac_zero(acc);
+    int carry = 0;
+#pragma unroll 1
+    for (int win = 0; win < kCombWindows; win++) {
+        int d = carry;
+        if (win < 32) d += (int)((s[win >> 3] >> (8 * (win & 7))) & 0xff);
+        carry = d > 128 ? 1 : 0;
+        if (d > 128) d -= 256;
+        if (d != 0) {
+            const int ad = d < 0 ? -d : d;
+            Aff<Fq> t;
+            const uint64_t* src = table_aff + (size_t)kAffPair * (win * kCombEntries + ad - 1);
+            fq_load(t.x, src);
+            fq_load(t.y, src + 6);
+            t.inf = false;
+            if (d < 0) fq_neg(t.y, t.y);
+            jac_add_mixed(acc, t);
+        }
+    }
+    store_jac(out + (size_t)kG1Jac * i, acc);
+}
+
+static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const size_t lanes = (n + kNormChunk - 1) / kNormChunk;
+    hipLaunchKernelGGL(k_g1_batch_normalize, dim3(blocks_for(lanes, 64)), dim3(64), 0, stream, v, n);
+    return hipGetLastError();
+}
+
+size_t g1_comb_workspace_words() {
+    return (size_t)kG1Jac * kCombWindows + (size_t)kG1Jac * kCombWindows * kCombEntries;
+}
+size_t g1_comb_table_words() { return (size_t)kAffPair * kCombWindows * kCombEntries; }
+
+hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_aff, uint64_t* workspace, hipStream_t stream) {
+    uint64_t* bases = workspace;
+    uint64_t* table_jac = workspace + (size_t)kG1Jac * kCombWindows;
+    const int entries = kCombWindows * kCombEntries;
+    hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, stream, base, bases);
+    hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(entries, 64)), dim3(64), 0, stream, bases, table_jac);
+    hipError_t e = launch_g1_batch_normalize(table_jac, entries, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(entries, 64)), dim3(64), 0, stream, table_jac, table_aff);
+    return hipGetLastError();
+}
+
+hipError_t launch_g1_comb_mul(const uint64_t* table_aff, const uint64_t* scalars, uint64_t* out, size_t n,
+                              hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_aff, scalars, out, n);
+    return hipGetLastError();
+}
+
+}  // namespace pa

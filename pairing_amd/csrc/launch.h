@@ -44,4 +44,14 @@ hipError_t launch_final_exponentiation(const uint64_t* in, uint64_t* out, uint8_
 // out[0] = prod_i in[i] (Fq12), in-place tree reduction over `work` (n entries, clobbered)
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
 
+// G1 batch_normalization in place (n Jacobian records of 18 u64)
+hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream);
+// fixed-base comb: table (g1_comb_table_words() u64) built from `base` using
+// `workspace` (g1_comb_workspace_words() u64); then out[i] = scalars[i] * base
+size_t g1_comb_table_words();
+size_t g1_comb_workspace_words();
+hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_aff, uint64_t* workspace, hipStream_t stream);
+hipError_t launch_g1_comb_mul(const uint64_t* table_aff, const uint64_t* scalars, uint64_t* out, size_t n,
+                              hipStream_t stream);
+
 }  // namespace pa

@@ -9,7 +9,7 @@ import ctypes
 
 import torch
 
-from ._native import W_FQ, W_FQ12, W_G1A, W_G2A, call
+from ._native import W_FQ, W_FQ12, W_G1, W_G1A, W_G2A, _lib, call
 
 
 def _stream_ptr(stream):
@@ -52,3 +52,23 @@ def pairing(p, q, out, scratch, stream=None):
     """out[i] = e(p[i], q[i]) for a batch resident in HBM (BASELINE config 4)."""
     call("pa_pairing_batch_device", _dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"), _dptr(out, W_FQ12, "out"),
          _dptr(scratch, W_FQ12, "scratch"), p.shape[0], _stream_ptr(stream))
+
+
+def g1_fixed_base_table(base, stream=None):
+    """Build the fixed-base table for `base` (a (1,18) Jacobian record) in HBM."""
+    dev = base.device
+    table = torch.empty(int(_lib.pa_g1_fixed_base_table_words()), dtype=torch.int64, device=dev)
+    ws = torch.empty(int(_lib.pa_g1_fixed_base_workspace_words()), dtype=torch.int64, device=dev)
+    call("pa_g1_fixed_base_table_device", _dptr(base, W_G1, "base"), ctypes.c_void_p(table.data_ptr()),
+         ctypes.c_void_p(ws.data_ptr()), _stream_ptr(stream))
+    return table, ws
+
+
+def g1_fixed_base_mul(table, scalars, out, stream=None):
+    """out[i] = scalars[i] * base (config 3), scalars (n,4) int64 FrRepr."""
+    call("pa_g1_fixed_base_mul_device", ctypes.c_void_p(table.data_ptr()), _dptr(scalars, 4, "scalars"),
+         _dptr(out, W_G1, "out"), scalars.shape[0], _stream_ptr(stream))
+
+
+def g1_batch_normalization(v, stream=None):
+    call("pa_g1_batch_normalization_device", _dptr(v, W_G1, "v"), v.shape[0], _stream_ptr(stream))

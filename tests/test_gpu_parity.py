@@ -183,3 +183,58 @@ def test_pairing_bilinearity(gpu, oracle):
     e3 = gpu.pairing(oracle.g1_mul_generator(one, NT), oracle.g2_mul_generator(ab, NT))
     np.testing.assert_array_equal(e1, e2)
     np.testing.assert_array_equal(e1, e3)
+
+
+# ---------------- config 3: G1 batch_normalization + fixed-base (wNAF path) ----------------
+
+def _jacobian_points(oracle, seed, n):
+    g = rng(seed)
+    v = oracle.g1_mul_generator_jacobian(random_scalars(g, n), NT)
+    # zeros keep garbage x, y with z = 0 (ec.rs:398, 477); normalized points have z = 1
+    zero_idx = [1, n // 3, n - 1]
+    v[zero_idx, 12:18] = 0
+    norm_idx = [2, n // 2]
+    v[norm_idx] = oracle.g1_from_affine(oracle.g1_into_affine(v[norm_idx]))
+    return v
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 4099])
+def test_g1_batch_normalization_bit_exact(gpu, oracle, n):
+    v = _jacobian_points(oracle, 40 + n, max(n, 8))[:n]
+    np.testing.assert_array_equal(gpu.g1_batch_normalization(v), oracle.g1_batch_normalization(v))
+
+
+def test_g1_fixed_base_equals_reference_wnaf(gpu, oracle):
+    g = rng(50)
+    base = oracle.g1_mul_generator_jacobian(random_scalars(g, 1))  # non-normalized base
+    s = random_scalars(g, 512)
+    s[0] = 0
+    s[1] = limbs(1, 4)
+    s[2] = limbs(R_ORDER - 1, 4)
+    s[3] = limbs((1 << 255) - 1, 4)   # > r: any 256-bit FrRepr is accepted
+    s[4] = limbs(128 + 256 * 128, 4)  # digit edge cases of the signed recoding
+    got = gpu.g1_wnaf_fixed_base(base, s)
+    exp = oracle.g1_wnaf_fixed_base(base, s, NT)
+    assert oracle.g1_eq(got, exp).all()  # PartialEq (ec.rs:45-85)
+    np.testing.assert_array_equal(gpu.g1_batch_normalization(got), oracle.g1_batch_normalization(exp))
+
+
+def test_g1_config3_full_size_properties(gpu, oracle):
+    """2^18 scalars (BASELINE config 3): sampled equality with the oracle and
+    linearity out[i] + out[j] == (s_i + s_j) * g on sampled pairs."""
+    n = 1 << 18
+    g = rng(51)
+    base = oracle.g1_mul_generator_jacobian(random_scalars(g, 1))
+    s = np.ascontiguousarray(random_scalars(g, 4096)[np.arange(n) % 4096])
+    s[:, 0] ^= np.arange(n, dtype=np.uint64)  # distinct scalars, still < 2^256
+    got = gpu.g1_batch_normalization(gpu.g1_wnaf_fixed_base(base, s))
+    idx = rng(52).choice(n, 256, replace=False)
+    exp = oracle.g1_batch_normalization(oracle.g1_wnaf_fixed_base(base, np.ascontiguousarray(s[idx]), NT))
+    np.testing.assert_array_equal(got[idx], exp)
+    i, j = idx[:64], idx[64:128]
+    ssum = np.array([limbs((sum(int(x) << (64 * k) for k, x in enumerate(s[a])) +
+                            sum(int(x) << (64 * k) for k, x in enumerate(s[b]))) % R_ORDER, 4)
+                     for a, b in zip(i, j)], np.uint64)
+    lhs = oracle.g1_add(np.ascontiguousarray(got[i]), np.ascontiguousarray(got[j]))
+    rhs = oracle.g1_wnaf_fixed_base(base, ssum, NT)
+    assert oracle.g1_eq(lhs, rhs).all()
