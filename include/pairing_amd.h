@@ -76,6 +76,10 @@ const char *pa_last_error(void);
 int pa_device_count(int *count);
 int pa_set_device(int device);
 int pa_synchronize(void);
+/* Tuning knob: lanes per pairing in the Miller-loop / final-exponentiation
+ * kernels (2 = default, two lanes share each pairing; 1 = one lane per
+ * pairing).  Results are identical; only speed differs. */
+int pa_set_pairing_lanes(int lanes);
 
 /* ---- Fq (src/bls12_381/fq.rs, Field trait src/lib.rs:267-325) ---- */
 /* Field::mul_assign, fq.rs:909-960 + mont_reduce fq.rs:1036-1122 */

@@ -45,6 +45,7 @@ _SIGS = {
     "pa_device_count": [ctypes.POINTER(ctypes.c_int)],
     "pa_set_device": [ctypes.c_int],
     "pa_synchronize": [],
+    "pa_set_pairing_lanes": [ctypes.c_int],
     "pa_fq_mul_batch": [_P, _P, _P, _N],
     "pa_fq_square_batch": [_P, _P, _N],
     "pa_fq_add_batch": [_P, _P, _P, _N],
@@ -101,6 +102,11 @@ def device_count():
     c = ctypes.c_int(0)
     rc = _lib.pa_device_count(ctypes.byref(c))
     return c.value if rc == PA_OK else 0
+
+
+def set_pairing_lanes(lanes):
+    """1 or 2 lanes per pairing in the pairing kernels (identical results)."""
+    call("pa_set_pairing_lanes", int(lanes))
 
 
 def set_device(dev):

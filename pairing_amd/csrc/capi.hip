@@ -14,6 +14,17 @@
 namespace {
 
 thread_local std::string g_last_error;
+// lanes per pairing for the Miller-loop / final-exponentiation kernels (1 or 2)
+int g_pairing_lanes = 1;
+
+hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
+    return g_pairing_lanes == 2 ? pa::launch_miller_loop_fused2(p, q, out, n, s)
+                                : pa::launch_miller_loop_fused(p, q, out, n, s);
+}
+hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
+    return g_pairing_lanes == 2 ? pa::launch_final_exponentiation2(in, out, ok, n, s)
+                                : pa::launch_final_exponentiation(in, out, ok, n, s);
+}
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
     char buf[256];
@@ -102,6 +113,11 @@ int pa_device_count(int* count) {
 }
 int pa_set_device(int device) {
     PA_TRY(hipSetDevice(device), "hipSetDevice");
+    return PA_OK;
+}
+int pa_set_pairing_lanes(int lanes) {
+    if (lanes != 1 && lanes != 2) return fail(PA_ERR_INVALID_ARGUMENT, "lanes must be 1 or 2");
+    g_pairing_lanes = lanes;
     return PA_OK;
 }
 int pa_synchronize(void) {
@@ -227,7 +243,7 @@ int pa_final_exponentiation_batch(const pa_fq12* in, pa_fq12* out, uint8_t* ok, 
     if ((rc = upload(din, in, 576 * n))) return rc;
     PA_TRY(dout.alloc(576 * n), "hipMalloc");
     PA_TRY(dok.alloc(n), "hipMalloc");
-    PA_TRY(pa::launch_final_exponentiation(din.as<uint64_t>(), dout.as<uint64_t>(), dok.as<uint8_t>(), n, nullptr),
+    PA_TRY(fe_launch(din.as<uint64_t>(), dout.as<uint64_t>(), dok.as<uint8_t>(), n, nullptr),
            "kernel launch");
     PA_TRY(hipDeviceSynchronize(), "kernel execution");
     if ((rc = download(out, dout, 576 * n))) return rc;
@@ -243,10 +259,9 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
         return rc;
     PA_TRY(dml.alloc(576 * n), "hipMalloc");
     PA_TRY(dout.alloc(576 * n), "hipMalloc");
-    PA_TRY(pa::launch_miller_loop_fused(dp.as<uint64_t>(), dq.as<uint64_t>(), dml.as<uint64_t>(), n, nullptr),
-           "kernel launch");
+    PA_TRY(ml_launch(dp.as<uint64_t>(), dq.as<uint64_t>(), dml.as<uint64_t>(), n, nullptr), "kernel launch");
     // Engine::pairing unwraps: a Miller-loop value is never zero, ok is not reported
-    PA_TRY(pa::launch_final_exponentiation(dml.as<uint64_t>(), dout.as<uint64_t>(), nullptr, n, nullptr),
+    PA_TRY(fe_launch(dml.as<uint64_t>(), dout.as<uint64_t>(), nullptr, n, nullptr),
            "kernel launch");
     PA_TRY(hipDeviceSynchronize(), "kernel execution");
     return download(out, dout, 576 * n);
@@ -309,26 +324,21 @@ int pa_fq_mul_batch_device(const pa_fq* a, const pa_fq* b, pa_fq* out, size_t n,
 int pa_miller_loop_fused_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n,
                                       void* stream) {
     if (n && (!p || !q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
-    PA_TRY(pa::launch_miller_loop_fused((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n,
-                                        (hipStream_t)stream),
+    PA_TRY(ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n, (hipStream_t)stream),
            "kernel launch");
     return PA_OK;
 }
 int pa_final_exponentiation_batch_device(const pa_fq12* in, pa_fq12* out, uint8_t* ok, size_t n, void* stream) {
     if (n && (!in || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
-    PA_TRY(pa::launch_final_exponentiation((const uint64_t*)in, (uint64_t*)out, ok, n, (hipStream_t)stream),
-           "kernel launch");
+    PA_TRY(fe_launch((const uint64_t*)in, (uint64_t*)out, ok, n, (hipStream_t)stream), "kernel launch");
     return PA_OK;
 }
 int pa_pairing_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, pa_fq12* scratch,
                             size_t n, void* stream) {
     if (n && (!p || !q || !out || !scratch)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
-    PA_TRY(pa::launch_miller_loop_fused((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)scratch, n,
-                                        (hipStream_t)stream),
+    PA_TRY(ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)scratch, n, (hipStream_t)stream),
            "kernel launch");
-    PA_TRY(pa::launch_final_exponentiation((const uint64_t*)scratch, (uint64_t*)out, nullptr, n,
-                                           (hipStream_t)stream),
-           "kernel launch");
+    PA_TRY(fe_launch((const uint64_t*)scratch, (uint64_t*)out, nullptr, n, (hipStream_t)stream), "kernel launch");
     return PA_OK;
 }
 

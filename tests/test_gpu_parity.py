@@ -114,6 +114,13 @@ def _points(seed, n, inf_every=0):
     return s1, s2
 
 
+@pytest.fixture(params=[2, 1], ids=["2lanes", "1lane"])
+def lanes(request, gpu):
+    gpu.set_pairing_lanes(request.param)
+    yield request.param
+    gpu.set_pairing_lanes(2)
+
+
 @pytest.fixture(scope="module")
 def pairs(oracle):
     s1, s2 = _points(21, 96)
@@ -145,7 +152,7 @@ def test_multi_miller_loop_is_product(gpu, oracle, pairs):
     np.testing.assert_array_equal(gpu.multi_miller_loop(p[:0], prep[:0]), fq12_one()[0])
 
 
-def test_final_exponentiation_matches_oracle(gpu, oracle, pairs):
+def test_final_exponentiation_matches_oracle(gpu, oracle, pairs, lanes):
     p, q = pairs
     f = oracle.miller_loop_batch(p[:32], oracle.g2_prepare(q[:32], NT), NT)
     f[7] = 0  # final_exponentiation(0) is None (mod.rs:108, 157-158)
@@ -156,19 +163,19 @@ def test_final_exponentiation_matches_oracle(gpu, oracle, pairs):
     np.testing.assert_array_equal(got[ok], exp[ok])
 
 
-def test_pairing_matches_oracle(gpu, oracle, pairs):
+def test_pairing_matches_oracle(gpu, oracle, pairs, lanes):
     p, q = pairs
     np.testing.assert_array_equal(gpu.pairing(p, q), oracle.pairing(p, q, NT))
 
 
-def test_pairing_relic_kat(gpu, oracle):
+def test_pairing_relic_kat(gpu, oracle, lanes):
     one = small_scalars([1])
     p = oracle.g1_mul_generator(one)
     q = oracle.g2_mul_generator(one)
     np.testing.assert_array_equal(gpu.pairing(p, q), relic_fq12())
 
 
-def test_pairing_bilinearity(gpu, oracle):
+def test_pairing_bilinearity(gpu, oracle, lanes):
     # e(aP, bQ) == e(abP, Q) == e(P, abQ) (engine.rs:93-126), all on the GPU
     g = rng(33)
     a = random_scalars(g, 16)

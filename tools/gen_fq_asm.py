@@ -121,6 +121,71 @@ def gen(n_chains, name):
     return "\n".join(L)
 
 
+Q_WORDS = ["0xffffaaab", "0xb9feffff", "0xb153ffff", "0x1eabfffe", "0xf6b0f624", "0x6730d2a0",
+           "0xf38512bf", "0x64774b84", "0x434bacd7", "0x4b1ba7b6", "0x397fe69a", "0x1a0111ea"]
+
+
+def gen_addsub():
+    """fq_add / fq_sub: two interleaved 12-word carry chains (one VOP3b with an
+    SGPR-pair carry, one VOP2 with the literal q word and VCC), so every carry
+    is read two instructions after it is written, then one `s_nop 1` and 12
+    v_cndmask.  37 VALU slots against ~150 for hipcc's lowering."""
+    # operands: 0..11 = x (=&v), 12..23 = y (=&v), 24 = c (=&s), 25..36 = a, 37..48 = b,
+    # 49..60 = q words in VGPRs (a VOP2 carry op reads VCC, so a literal or SGPR
+    # second operand would exceed gfx9's one-read constant bus)
+    QV = lambda i: "%%%d" % (49 + i)
+    A = lambda i: "%%%d" % (25 + i)
+    B = lambda i: "%%%d" % (37 + i)
+    X = lambda i: "%%%d" % i
+    Y = lambda i: "%%%d" % (12 + i)
+    C = "%24"
+    outs = ", ".join('"=&v"(x[%d])' % i for i in range(12)) + ", " + \
+        ", ".join('"=&v"(y[%d])' % i for i in range(12)) + ', "=&s"(c)'
+    ins = ", ".join('"v"(a.w[%d])' % i for i in range(12)) + ", " + ", ".join('"v"(b.w[%d])' % i for i in range(12)) \
+        + ", " + ", ".join('"v"(PA_Q%d)' % i for i in range(12))
+
+    def body(first_a, next_a, first_b, next_b, select):
+        t = []
+        for i in range(12):
+            t.append((first_a if i == 0 else next_a)(i))
+            t.append((first_b if i == 0 else next_b)(i))
+        t.append("s_nop 1")
+        t += [select(i) for i in range(12)]
+        return "\\n\\t".join(t)
+
+    # add: x = a + b (SGPR carry), y = x - q (VCC borrow); keep x iff y borrowed
+    add_text = body(lambda i: "v_add_co_u32 %s, %s, %s, %s" % (X(i), C, A(i), B(i)),
+                    lambda i: "v_addc_co_u32 %s, %s, %s, %s, %s" % (X(i), C, A(i), B(i), C),
+                    lambda i: "v_sub_co_u32 %s, vcc, %s, %s" % (Y(i), X(i), QV(i)),
+                    lambda i: "v_subb_co_u32 %s, vcc, %s, %s, vcc" % (Y(i), X(i), QV(i)),
+                    lambda i: "v_cndmask_b32 %s, %s, %s, vcc" % (X(i), Y(i), X(i)))
+    # sub: x = a - b (SGPR borrow), y = x + q (VCC carry); keep y iff x borrowed
+    sub_text = body(lambda i: "v_sub_co_u32 %s, %s, %s, %s" % (X(i), C, A(i), B(i)),
+                    lambda i: "v_subb_co_u32 %s, %s, %s, %s, %s" % (X(i), C, A(i), B(i), C),
+                    lambda i: "v_add_co_u32 %s, vcc, %s, %s" % (Y(i), X(i), QV(i)),
+                    lambda i: "v_addc_co_u32 %s, vcc, %s, %s, vcc" % (Y(i), X(i), QV(i)),
+                    lambda i: "v_cndmask_b32_e64 %s, %s, %s, %s" % (X(i), X(i), Y(i), C))
+    out = []
+    for name, text, ref in (("fq_add", add_text, "fq.rs:812-819: a + b, minus q if >= q"),
+                            ("fq_sub", sub_text, "fq.rs:830-838: a - b, plus q on borrow")):
+        out.append("// %s" % ref)
+        out.append("PA_DEV void %s(Fq& r, const Fq& a, const Fq& b) {" % name)
+        out.append("    uint32_t x[12], y[12];")
+        out.append("    uint64_t c;")
+        out.append('    asm("%s"\n        : %s\n        : %s\n        : "vcc");' % (text, outs, ins))
+        out.append("#pragma unroll")
+        out.append("    for (int i = 0; i < 12; i++) r.w[i] = x[i];")
+        out.append("}")
+    out.append("PA_DEV void fq_dbl(Fq& r, const Fq& a) { fq_add(r, a, a); }  // fq.rs:821-828")
+    out.append("// fq.rs:840-847: q - a unless a == 0 (0 - a reduces to exactly that)")
+    out.append("PA_DEV void fq_neg(Fq& r, const Fq& a) {")
+    out.append("    Fq z;")
+    out.append("    fq_zero(z);")
+    out.append("    fq_sub(r, z, a);")
+    out.append("}")
+    return "\n".join(out)
+
+
 def main():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.path.join(root, "pairing_amd", "csrc", "fq_mul_gen.h")
@@ -130,6 +195,7 @@ def main():
         "#pragma once",
         '#include "fq.h"',
         "namespace pa {",
+        gen_addsub(),
         gen(1, "fq_mul_x1"),
         gen(2, "fq_mul_x2"),
         gen(3, "fq_mul_x3"),
