@@ -134,8 +134,8 @@ def main():
 
     torch.cuda.set_device(local)
     pairing_amd.set_device(local)
-    if os.environ.get("PA_PAIRING_LANES"):
-        pairing_amd.set_pairing_lanes(int(os.environ["PA_PAIRING_LANES"]))
+    if os.environ.get("PA_PAIRING_KERNEL"):
+        pairing_amd.set_pairing_kernel(int(os.environ["PA_PAIRING_KERNEL"]))
     dev = torch.device("cuda", local)
     if ws > 1:
         dist.init_process_group("nccl", device_id=dev)
@@ -240,7 +240,7 @@ def main():
             value = ws * n * args.steps / elapsed
             metric, unit = "BLS12-381 pairings/sec at batch 2^16", "pairings/s"
             config = {"workload": "bls12_381 e(P_i,Q_i) batch (fused G2 prepare + Miller loop + final exp)",
-                      "lanes_per_pairing": int(os.environ.get("PA_PAIRING_LANES", "1")),
+                      "kernel_variant": ["lazy28", "word32", "word32x2"][int(os.environ.get("PA_PAIRING_KERNEL", "0"))],
                       "batch_per_gpu": n, "global_batch": n * ws, "parallelism": "shard%d+rccl_gather" % ws
                       if ws > 1 else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}

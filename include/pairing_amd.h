@@ -76,10 +76,13 @@ const char *pa_last_error(void);
 int pa_device_count(int *count);
 int pa_set_device(int device);
 int pa_synchronize(void);
-/* Tuning knob: lanes per pairing in the Miller-loop / final-exponentiation
- * kernels (2 = default, two lanes share each pairing; 1 = one lane per
- * pairing).  Results are identical; only speed differs. */
-int pa_set_pairing_lanes(int lanes);
+/* Tuning knob: which kernel family runs the Miller loop / final
+ * exponentiation (identical results):
+ *   0 = lazy 28-bit-limb core, one pairing per lane (default)
+ *   1 = 32-bit-word core, one pairing per lane
+ *   2 = 32-bit-word core, two lanes per pairing
+ * Not part of the reference interface; for A/B measurement. */
+int pa_set_pairing_kernel(int variant);
 
 /* ---- Fq (src/bls12_381/fq.rs, Field trait src/lib.rs:267-325) ---- */
 /* Field::mul_assign, fq.rs:909-960 + mont_reduce fq.rs:1036-1122 */

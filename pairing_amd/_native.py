@@ -45,7 +45,7 @@ _SIGS = {
     "pa_device_count": [ctypes.POINTER(ctypes.c_int)],
     "pa_set_device": [ctypes.c_int],
     "pa_synchronize": [],
-    "pa_set_pairing_lanes": [ctypes.c_int],
+    "pa_set_pairing_kernel": [ctypes.c_int],
     "pa_fq_mul_batch": [_P, _P, _P, _N],
     "pa_fq_square_batch": [_P, _P, _N],
     "pa_fq_add_batch": [_P, _P, _P, _N],
@@ -104,9 +104,10 @@ def device_count():
     return c.value if rc == PA_OK else 0
 
 
-def set_pairing_lanes(lanes):
-    """1 or 2 lanes per pairing in the pairing kernels (identical results)."""
-    call("pa_set_pairing_lanes", int(lanes))
+def set_pairing_kernel(variant):
+    """Pairing kernel family: 0 lazy 28-bit core (default), 1 32-bit one lane,
+    2 32-bit two lanes per pairing.  Identical results."""
+    call("pa_set_pairing_kernel", int(variant))
 
 
 def set_device(dev):

@@ -14,16 +14,22 @@
 namespace {
 
 thread_local std::string g_last_error;
-// lanes per pairing for the Miller-loop / final-exponentiation kernels (1 or 2)
-int g_pairing_lanes = 1;
+// kernel family for the Miller loop / final exponentiation (pa_set_pairing_kernel)
+int g_pairing_kernel = 0;
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
-    return g_pairing_lanes == 2 ? pa::launch_miller_loop_fused2(p, q, out, n, s)
-                                : pa::launch_miller_loop_fused(p, q, out, n, s);
+    switch (g_pairing_kernel) {
+        case 1: return pa::launch_miller_loop_fused(p, q, out, n, s);
+        case 2: return pa::launch_miller_loop_fused2(p, q, out, n, s);
+        default: return pa::launch_miller_loop_fl(p, q, out, n, s);
+    }
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
-    return g_pairing_lanes == 2 ? pa::launch_final_exponentiation2(in, out, ok, n, s)
-                                : pa::launch_final_exponentiation(in, out, ok, n, s);
+    switch (g_pairing_kernel) {
+        case 1: return pa::launch_final_exponentiation(in, out, ok, n, s);
+        case 2: return pa::launch_final_exponentiation2(in, out, ok, n, s);
+        default: return pa::launch_final_exp_fl(in, out, ok, n, s);
+    }
 }
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
@@ -115,9 +121,9 @@ int pa_set_device(int device) {
     PA_TRY(hipSetDevice(device), "hipSetDevice");
     return PA_OK;
 }
-int pa_set_pairing_lanes(int lanes) {
-    if (lanes != 1 && lanes != 2) return fail(PA_ERR_INVALID_ARGUMENT, "lanes must be 1 or 2");
-    g_pairing_lanes = lanes;
+int pa_set_pairing_kernel(int variant) {
+    if (variant < 0 || variant > 2) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0, 1 or 2");
+    g_pairing_kernel = variant;
     return PA_OK;
 }
 int pa_synchronize(void) {
