@@ -81,6 +81,8 @@ int pa_synchronize(void);
  *   0 = lazy 28-bit-limb core, one pairing per lane (default)
  *   1 = 32-bit-word core, one pairing per lane
  *   2 = 32-bit-word core, two lanes per pairing
+ *   3 = generated kernels (tools/pgen: own register allocation, code objects
+ *       lib/pa_gen_*.hsaco loaded at first use)
  * Not part of the reference interface; for A/B measurement. */
 int pa_set_pairing_kernel(int variant);
 

@@ -106,7 +106,7 @@ def device_count():
 
 def set_pairing_kernel(variant):
     """Pairing kernel family: 0 lazy 28-bit core (default), 1 32-bit one lane,
-    2 32-bit two lanes per pairing.  Identical results."""
+    2 32-bit two lanes per pairing, 3 generated (tools/pgen).  Identical results."""
     call("pa_set_pairing_kernel", int(variant))
 
 

@@ -21,6 +21,7 @@ hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t
     switch (g_pairing_kernel) {
         case 1: return pa::launch_miller_loop_fused(p, q, out, n, s);
         case 2: return pa::launch_miller_loop_fused2(p, q, out, n, s);
+        case 3: return pa::launch_miller_loop_gen(p, q, out, n, s);
         default: return pa::launch_miller_loop_fl(p, q, out, n, s);
     }
 }
@@ -28,6 +29,7 @@ hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, h
     switch (g_pairing_kernel) {
         case 1: return pa::launch_final_exponentiation(in, out, ok, n, s);
         case 2: return pa::launch_final_exponentiation2(in, out, ok, n, s);
+        case 3: return pa::launch_final_exp_gen(in, out, ok, n, s);
         default: return pa::launch_final_exp_fl(in, out, ok, n, s);
     }
 }
@@ -122,7 +124,7 @@ int pa_set_device(int device) {
     return PA_OK;
 }
 int pa_set_pairing_kernel(int variant) {
-    if (variant < 0 || variant > 2) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0, 1 or 2");
+    if (variant < 0 || variant > 3) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..3");
     g_pairing_kernel = variant;
     return PA_OK;
 }

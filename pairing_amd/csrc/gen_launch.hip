@@ -1,0 +1,98 @@
+// Host side of the generated pairing kernels (tools/pgen): the code objects
+// pairing_amd/lib/pa_gen_*.hsaco sit next to libpairing_amd.so and are
+// loaded once per device through the HIP module API; each launch passes the
+// five kernel arguments of tools/pgen/kcfg.py and a per-wave spill
+// workspace (pa_gen_meta.h gives its size).  A missing code object is an
+// error, never a fallback.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
+
+#include "launch.h"
+#include "pa_gen_meta.h"
+
+namespace pa {
+namespace {
+
+struct GenDevice {
+    bool loaded = false;
+    hipError_t err = hipSuccess;
+    hipModule_t mod[2] = {nullptr, nullptr};
+    hipFunction_t fn[2] = {nullptr, nullptr};
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+};
+
+std::mutex g_mu;
+GenDevice g_dev[64];
+
+const char* const kFile[2] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco"};
+const char* const kName[2] = {"pa_gen_miller_loop", "pa_gen_final_exp"};
+const size_t kWaveBytes[2] = {PA_GEN_MILLER_LOOP_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_MEM_SLOTS * 3584ull};
+
+std::string lib_dir() {
+    Dl_info info;
+    if (dladdr(reinterpret_cast<void*>(&lib_dir), &info) && info.dli_fname) {
+        std::string p(info.dli_fname);
+        const size_t k = p.rfind('/');
+        if (k != std::string::npos) return p.substr(0, k);
+    }
+    return ".";
+}
+
+hipError_t load(GenDevice& d) {
+    if (d.loaded) return d.err;
+    d.loaded = true;
+    const std::string dir = lib_dir();
+    for (int k = 0; k < 2; k++) {
+        const std::string path = dir + "/" + kFile[k];
+        if ((d.err = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess) return d.err;
+        if ((d.err = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) return d.err;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch(int which, const void* a0, const void* a1, const void* a2, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lock(g_mu);
+    GenDevice& d = g_dev[dev];
+    if ((e = load(d)) != hipSuccess) return e;
+    const size_t blocks = (n + 63) / 64;
+    const size_t need = blocks * (kWaveBytes[0] > kWaveBytes[1] ? kWaveBytes[0] : kWaveBytes[1]);
+    if (need > d.ws_bytes) {
+        if (d.ws) (void)hipFree(d.ws);
+        d.ws = nullptr;
+        d.ws_bytes = 0;
+        if ((e = hipMalloc(&d.ws, need)) != hipSuccess) return e;
+        d.ws_bytes = need;
+    }
+    struct {
+        const void* a0;
+        const void* a1;
+        const void* a2;
+        uint64_t n;
+        void* ws;
+    } args{a0, a1, a2, (uint64_t)n, d.ws};
+    size_t size = sizeof(args);
+    void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                      HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(d.fn[which], (unsigned)blocks, 1, 1, 64, 1, 1, 0, stream, nullptr, config);
+}
+
+}  // namespace
+
+hipError_t launch_miller_loop_gen(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+                                  hipStream_t stream) {
+    return launch(0, p_aff, q_aff, out, n, stream);
+}
+hipError_t launch_final_exp_gen(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream) {
+    return launch(1, in, out, ok, n, stream);
+}
+
+}  // namespace pa

@@ -33,11 +33,16 @@ __global__ void __launch_bounds__(64) k_miller_loop_fl(const uint64_t* __restric
     if (i >= n) return;
     const uint64_t* p = p_aff + 13 * i;
     const uint64_t* q = q_aff + 25 * i;
-    const F<1> px = load_aff_fq(p), py = load_aff_fq(p + 6);
-    const F2<1> qx{load_aff_fq(q), load_aff_fq(q + 6)};
-    const F2<1> qy{load_aff_fq(q + 12), load_aff_fq(q + 18)};
+    __shared__ uint32_t lds[84 * 64];
+    const fl::PQ pq{lds + threadIdx.x};
+    pq.put(0, load_aff_fq(p));
+    pq.put(1, load_aff_fq(p + 6));
+    pq.put(2, load_aff_fq(q));
+    pq.put(3, load_aff_fq(q + 6));
+    pq.put(4, load_aff_fq(q + 12));
+    pq.put(5, load_aff_fq(q + 18));
     const bool inf = ((p[12] | q[24]) & 0xff) != 0;
-    F12<1> f = fl::miller_loop(px, py, qx, qy);
+    F12<1> f = fl::miller_loop(pq);
     if (inf) f = f12_one();  // mod.rs:50-54: pairs with an infinity are skipped
     store12(out + 72 * i, f);
 }

@@ -80,34 +80,59 @@ PA_DEV F12<1> ell(const F12<1>& f, const Line& c, const F<1>& px, const F<1>& py
     return mul_by_014(f, c.c2, mul_by_fq(c.c1, px), mul_by_fq(c.c0, py));
 }
 
-// One doubling (and, on the set bits of |x|, one addition) step with its
-// line folded into f.  The step kind is wave-uniform.
-PA_DEV void line_step(F12<1>& f, G2J& r, bool add_step, const F2<1>& qx, const F2<1>& qy, const F<1>& px,
-                      const F<1>& py) {
-    const Line c = add_step ? addition_step(r, qx, qy) : doubling_step(r);
-    f = ell(f, c, px, py);
+// P and Q are loop-invariant but used only once per step: they live in LDS
+// (word-major, one column per lane: conflict-free) and are re-read where
+// needed, which keeps ~84 VGPRs free for the Fq12 temporaries.
+struct PQ {
+    uint32_t* base;  // LDS, [84 words][64 lanes]
+    PA_DEV F<1> get(int k) const {
+        uint32_t* b = base;
+        asm volatile("" : "+v"(b));  // opaque: no hoisting of the reads out of the loop
+        F<1> r;
+#pragma unroll
+        for (int i = 0; i < 14; i++) r.w[i] = b[(14 * k + i) * 64];
+        return r;
+    }
+    PA_DEV void put(int k, const F<1>& x) const {
+#pragma unroll
+        for (int i = 0; i < 14; i++) base[(14 * k + i) * 64] = x.w[i];
+    }
+};
+// slots: 0 px, 1 py, 2 qx.c0, 3 qx.c1, 4 qy.c0, 5 qy.c1
+
+// One doubling or addition step (wave-uniform choice) with its line folded
+// into f.
+PA_DEV void line_step(F12<1>& f, G2J& r, bool add_step, const PQ& pq) {
+    Line c;
+    if (add_step) {
+        c = addition_step(r, {pq.get(2), pq.get(3)}, {pq.get(4), pq.get(5)});
+    } else {
+        c = doubling_step(r);
+    }
+    f = ell(f, c, pq.get(0), pq.get(1));
 }
 
 // Single-pair Miller loop, mod.rs:40-102, with G2 preparation fused in.
 // Infinity pairs give one (mod.rs:50-54): those lanes run the same stream
-// on their data and are selected out at the end.
-PA_DEV F12<1> miller_loop(const F<1>& px, const F<1>& py, const F2<1>& qx, const F2<1>& qy) {
-    G2J r{qx, qy, f2_one()};
+// on their data and are selected out by the caller.
+PA_DEV F12<1> miller_loop(const PQ& pq) {
+    G2J r{{pq.get(2), pq.get(3)}, {pq.get(4), pq.get(5)}, f2_one()};
     F12<1> f = f12_one();
 #pragma unroll 1
     for (int bit = 61; bit >= 0; bit--) {
         const bool set = ((kX >> 1) >> bit) & 1;  // wave-uniform
 #pragma unroll 1
-        for (int k = 0; k <= (int)set; k++) line_step(f, r, k == 1, qx, qy, px, py);
+        for (int k = 0; k <= (int)set; k++) line_step(f, r, k == 1, pq);
         f = sqr(f);
     }
-    line_step(f, r, false, qx, qy, px, py);
+    line_step(f, r, false, pq);
     return red(conj(f));
 }
 
 // exp_by_x (mod.rs:116-121): f^|x| by square-and-multiply (lib.rs:306-324)
 // with cyclotomic squarings, then conjugation (x < 0)
-PA_DEV F12<1> exp_by_x(const F12<1>& f, uint64_t x) {
+__device__ __noinline__ void exp_by_x_into(F12<1>* out, const F12<1>* fp, uint64_t x) {
+    const F12<1> f = *fp;
     F12<1> res = f;
     const int top = 63 - __builtin_clzll(x);
 #pragma unroll 1
@@ -115,7 +140,12 @@ PA_DEV F12<1> exp_by_x(const F12<1>& f, uint64_t x) {
         res = cyclotomic_sqr(res);
         if ((x >> bit) & 1) res = mul(res, f);  // wave-uniform
     }
-    return red(conj(res));
+    *out = red(conj(res));
+}
+PA_DEV F12<1> exp_by_x(const F12<1>& f, uint64_t x) {
+    F12<1> r;
+    exp_by_x_into(&r, &f, x);
+    return r;
 }
 
 PA_DEV F12<1> cj(const F12<1>& a) { return red(conj(a)); }

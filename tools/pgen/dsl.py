@@ -1,0 +1,336 @@
+"""Tracing DSL for the pairing kernels over the lazy 28-bit-limb field.
+
+A kernel is built by running Python code that calls Prog methods; every
+call appends an Op to the current Block and returns an SSA value `Val`
+carrying its static bound u (every limb <= u (2^28-1), value < u 2q; see
+pairing_amd/csrc/fl.h).  Long-lived state crosses loop / branch
+boundaries through named variables (getvar / setvar), which the register
+allocator pins to fixed homes.
+
+`evaluate()` interprets a Prog on concrete inputs with the exact limb
+semantics of the emitted instructions (column-accumulator Montgomery
+products, the one-pass red(), limb-wise add/sub), asserting every bound as
+it goes -- the golden model the instruction-level simulator and the GPU are
+compared against, and itself compared against the C oracle.
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+from gen_consts import Q  # noqa: E402
+import gen_fl  # noqa: E402
+
+NL, LB, MASK = gen_fl.NL, gen_fl.LB, gen_fl.MASK
+R = 1 << (NL * LB)
+QL = gen_fl.limbs(Q)
+QINV28 = gen_fl.QINV
+KQ = gen_fl.KQ
+SUBC = {}
+SUBCU = {}
+for _ub in range(1, gen_fl.U_MAX_SUB + 1):
+    SUBC[_ub], SUBCU[_ub] = gen_fl.sub_constant(_ub)
+U_MAX = 16
+COL_BOUND = 17
+
+
+def to_mont_limbs(x):
+    """field value -> canonical Fl limbs (x R mod q)"""
+    return tuple(gen_fl.limbs(x * R % Q))
+
+
+def val_of(limbs):
+    return sum(int(x) << (LB * i) for i, x in enumerate(limbs))
+
+
+class Val:
+    __slots__ = ("id", "u")
+
+    def __init__(self, id_, u):
+        self.id, self.u = id_, u
+
+    def __repr__(self):
+        return "v%d/u%d" % (self.id, self.u)
+
+
+class Op:
+    __slots__ = ("kind", "dst", "srcs", "imm")
+
+    def __init__(self, kind, dst, srcs, imm=None):
+        self.kind, self.dst, self.srcs, self.imm = kind, dst, srcs, imm
+
+    def __repr__(self):
+        return "%s %s <- %s %s" % (self.kind, self.dst, self.srcs, "" if self.imm is None else self.imm)
+
+
+class Block:
+    def __init__(self):
+        self.items = []
+
+
+class Loop:
+    """body runs `trips` times; counter i = trips-1 .. 0 (bit index for If)"""
+
+    def __init__(self, trips):
+        self.trips = trips
+        self.body = Block()
+
+
+class If:
+    """body runs when (mask >> loop.i) & 1"""
+
+    def __init__(self, mask, loop):
+        self.mask, self.loop = mask, loop
+        self.body = Block()
+
+
+class Var:
+    def __init__(self, name, u, home):
+        self.name, self.u, self.home = name, u, home
+
+
+class Prog:
+    def __init__(self, name):
+        self.name = name
+        self.root = Block()
+        self.cur = self.root
+        self.nval = 0
+        self.vars = {}
+        self.inputs = []   # (name, kind): kernel inputs, see kernels.py
+        self.stack = []
+
+    # ---- plumbing ----
+    def _val(self, u):
+        assert 1 <= u <= U_MAX, "bound %d out of range" % u
+        v = Val(self.nval, u)
+        self.nval += 1
+        return v
+
+    def _op(self, kind, srcs, u, imm=None):
+        v = self._val(u) if u else None
+        self.cur.items.append(Op(kind, v, list(srcs), imm))
+        return v
+
+    # ---- field ops ----
+    def mul(self, a, b):
+        assert a.u * b.u <= COL_BOUND, "mul bound %d*%d" % (a.u, b.u)
+        return self._op("sop", [a, b], 1)
+
+    def sop(self, a, b, c, d):
+        assert a.u * b.u + c.u * d.u <= COL_BOUND, "sop bound %d*%d+%d*%d" % (a.u, b.u, c.u, d.u)
+        return self._op("sop", [a, b, c, d], 1)
+
+    def sqr(self, a):
+        assert a.u <= 3, "sqr bound %d" % a.u
+        return self._op("sqr", [a], 1)
+
+    def add(self, a, b):
+        return self._op("add", [a, b], a.u + b.u)
+
+    def dbl(self, a):
+        return self.add(a, a)
+
+    def sub(self, a, b):
+        assert b.u in SUBCU, "sub subtrahend bound %d" % b.u
+        return self._op("sub", [a, b], a.u + SUBCU[b.u], imm=b.u)
+
+    def neg(self, b):
+        assert b.u in SUBCU, "neg bound %d" % b.u
+        return self._op("neg", [b], SUBCU[b.u], imm=b.u)
+
+    def red(self, a):
+        if a.u == 1:
+            return a
+        return self._op("red", [a], 1)
+
+    def const(self, x):
+        """field element x (plain integer) as a canonical Fl constant"""
+        return self._op("const", [], 1, imm=to_mont_limbs(x % Q))
+
+    def const_limbs(self, limbs):
+        return self._op("const", [], 1, imm=tuple(limbs))
+
+    # ---- state ----
+    def var(self, name, u=1, home=None):
+        self.vars[name] = Var(name, u, home)
+
+    def get(self, name):
+        return self._op("getvar", [], self.vars[name].u, imm=name)
+
+    def set(self, name, v):
+        assert v.u <= self.vars[name].u, "setvar %s: bound %d > %d" % (name, v.u, self.vars[name].u)
+        self.cur.items.append(Op("setvar", None, [v], imm=name))
+
+    # ---- kernel I/O (see kernels.py for the record layouts) ----
+    def load(self, slot):
+        """input Fq number `slot` of this lane's record (canonical, R = 2^384)
+        -> Fl with R = 2^392 (u = 1): raw limbs times 2^400 mod q"""
+        raw = self._op("load_raw", [], 1, imm=slot)
+        return self.mul(raw, self.const_limbs(gen_fl.limbs(pow(2, 400, Q))))
+
+    def store(self, slot, v):
+        """canonical output Fq `slot` (R = 2^384) of this lane"""
+        w = self.mul(self.red(v), self.const_limbs(gen_fl.limbs(pow(2, 384, Q))))
+        self.cur.items.append(Op("store_raw", None, [w], imm=slot))
+
+    # ---- control ----
+    def loop(self, trips):
+        return _Ctx(self, Loop(trips))
+
+    def if_bit(self, mask, loop):
+        return _Ctx(self, If(mask, loop))
+
+
+def check_scopes(prog):
+    """Only named variables cross into loop / branch bodies: every Val used in
+    a body is defined in that same body (the allocator relies on it)."""
+    # simpler exact rule: track the defining block of each value
+    owner = {}
+
+    def mark(block):
+        for it in block.items:
+            if isinstance(it, (Loop, If)):
+                mark(it.body)
+            elif it.dst is not None:
+                owner[it.dst.id] = id(block)
+
+    def check(block):
+        for it in block.items:
+            if isinstance(it, (Loop, If)):
+                check(it.body)
+            else:
+                for v in it.srcs:
+                    assert owner[v.id] == id(block), "%r uses v%d defined in another block" % (it, v.id)
+    mark(prog.root)
+    check(prog.root)
+
+
+class _Ctx:
+    def __init__(self, prog, node):
+        self.prog, self.node = prog, node
+
+    def __enter__(self):
+        self.prog.cur.items.append(self.node)
+        self.prog.stack.append(self.prog.cur)
+        self.prog.cur = self.node.body
+        return self.node
+
+    def __exit__(self, *exc):
+        self.prog.cur = self.prog.stack.pop()
+        return False
+
+
+# ======================= exact evaluation =======================
+class Stats:
+    def __init__(self):
+        self.counts = {}
+
+    def bump(self, k, n=1):
+        self.counts[k] = self.counts.get(k, 0) + n
+
+
+def _check(limbs, u, what):
+    assert all(0 <= x <= u * MASK for x in limbs), "%s: limb bound u=%d violated" % (what, u)
+    assert val_of(limbs) < u * 2 * Q, "%s: value bound u=%d violated" % (what, u)
+
+
+def mont_sop(pairs):
+    """exact result of the column-accumulator Montgomery product of sum a*b"""
+    # column sums must fit the 64-bit accumulator (the static bound proves it;
+    # check the concrete columns too)
+    cols = [0] * (2 * NL)
+    for a, b in pairs:
+        for i in range(NL):
+            for j in range(NL):
+                cols[i + j] += a[i] * b[j]
+    s = sum(int(a_) * int(b_) for a, b in pairs for a_, b_ in [(val_of(a), val_of(b))])
+    m = (-s * pow(Q, -1, R)) % R
+    t = s + m * Q
+    assert t % R == 0
+    ml = gen_fl.limbs(m)
+    for k in range(2 * NL - 1):
+        mq = sum(ml[i] * QL[k - i] for i in range(max(0, k - NL + 1), min(k, NL - 1) + 1))
+        assert cols[k] + mq < (1 << 64) - (1 << 36), "column %d overflows" % k
+    out = t // R
+    assert out < R
+    return tuple(gen_fl.limbs(out))
+
+
+def red_limbs(x):
+    p1 = x[12] * KQ
+    p2 = x[13] * KQ
+    k = (p2 + (p1 >> 28)) >> 36
+    r = []
+    acc = 0
+    for i in range(NL - 1):
+        acc += x[i] - k * QL[i]
+        r.append(acc & MASK)
+        acc >>= 28
+    acc += x[13] - k * QL[13]
+    assert 0 <= acc < (1 << 32)
+    r.append(acc)
+    return tuple(r)
+
+
+def evaluate(prog, inputs, stats=None, trace=None):
+    """inputs: dict slot -> canonical ABI integer (R = 2^384 Montgomery value,
+    i.e. the integer held in the record).  Returns dict slot -> output integer."""
+    env = {}
+    vars_ = {}
+    outs = {}
+    counters = {}
+    st = stats or Stats()
+
+    def run(block):
+        for it in block.items:
+            if isinstance(it, Loop):
+                for i in range(it.trips - 1, -1, -1):
+                    counters[id(it)] = i
+                    run(it.body)
+            elif isinstance(it, If):
+                if (it.mask >> counters[id(it.loop)]) & 1:
+                    run(it.body)
+            else:
+                step(it)
+
+    def step(op):
+        k = op.kind
+        s = [env[v.id] for v in op.srcs]
+        st.bump(k)
+        if k == "sop":
+            r = mont_sop(list(zip(s[0::2], s[1::2])))
+        elif k == "sqr":
+            r = mont_sop([(s[0], s[0])])
+        elif k == "add":
+            r = tuple(a + b for a, b in zip(*s))
+        elif k == "sub":
+            c = SUBC[op.imm]
+            r = tuple(a + ci - b for a, ci, b in zip(s[0], c, s[1]))
+        elif k == "neg":
+            c = SUBC[op.imm]
+            r = tuple(ci - b for ci, b in zip(c, s[0]))
+        elif k == "red":
+            r = red_limbs(s[0])
+        elif k == "const":
+            r = op.imm
+        elif k == "getvar":
+            r = vars_[op.imm]
+        elif k == "setvar":
+            vars_[op.imm] = s[0]
+            return
+        elif k == "load_raw":
+            r = tuple(gen_fl.limbs(inputs[op.imm]))
+        elif k == "store_raw":
+            v = val_of(s[0])
+            assert v < 2 * Q
+            outs[op.imm] = v % Q
+            return
+        else:
+            raise ValueError(k)
+        _check(r, op.dst.u, repr(op))
+        env[op.dst.id] = r
+        if trace is not None:
+            trace.append((op.dst.id, r, op))
+
+    run(prog.root)
+    return outs

@@ -1,0 +1,621 @@
+"""Register allocation and gfx950 instruction emission for DSL programs.
+
+Storage model (one pairing per lane, one wave per SIMD, 512 registers):
+  VGPR  v0..v15   work area of the product / reduction / record I/O code:
+                  acc = v[0:1], Montgomery digits m_0..m_13 = v2..v15
+        v16       tid * 8 (LDS / spill lane offset)      v17  spare
+        v18..v255 17 "V slots" of 14 VGPRs, where every operand must be
+  AGPR  a0..a251  18 "A slots" (VALU cannot read AGPRs: 14 accvgpr moves)
+  LDS   11 "L slots" per wave, layout [slot][pair][lane] x 8 B (ds_*_b64)
+  HBM   "M slots" in a per-wave workspace, same layout (global_*_dwordx2)
+  SGPR  s[80:93] q limbs, s94 -q^-1 mod 2^28, s95 floor(2^400/q)
+
+A value lives in one or more locations; operations need their sources in
+V slots and define their destination in a V slot.  Within a straight-line
+block the allocator evicts the V-resident value whose next use is furthest
+(Belady), dropping it if a copy exists elsewhere (a variable's home, an
+earlier spill) and otherwise spilling to an A, then L, then M slot.
+Variables (DSL getvar/setvar) have fixed homes for their lifetime; values
+that live across a loop / branch are parked in A/L/M slots the body does
+not touch.  Control flow is SALU only (wave-uniform), with long branches
+(s_setpc) because bodies exceed s_cbranch's +-128 KiB reach.
+
+Output: a list of instruction tuples (mnemonic, operands...) where
+operands are ints (VGPR n: n, AGPR n: 256+n, SGPR n: 512+n), ("k", value)
+for constants, or label strings; see render.py / sim.py.
+"""
+from dsl import Loop, If, Op, SUBC, NL, MASK, QL, QINV28, KQ
+
+A_BASE, S_BASE = 256, 512
+VCC = S_BASE + 106
+
+
+def V(n): return n
+def A(n): return A_BASE + n
+def S(n): return S_BASE + n
+def K(x): return ("k", x)
+
+
+ACC = 0
+M0 = 2
+LOFF, ORACC = 16, 17               # tid * 8 (LDS / spill lane offset); spare
+GID, ADDR = 14, 12                 # work-area temporaries of the record I/O code
+VSLOT0, NV = 18, 17
+NA = 18
+NL_SLOTS = 11
+SLOT_BYTES = NL * 4 * 64          # 3584: one Fq for 64 lanes
+SQ, SQINV, SKQ = 80, 94, 95
+# SGPR map
+S_KARG = 0          # s[0:1] kernarg pointer
+S_WG = 2            # workgroup id
+S_ARG = 4           # s[4:13] five 8-byte kernel args
+S_WS = 14           # s[14:15] this wave's workspace base
+S_TMP = 16          # s[16:17] address temporary
+S_EXEC = 18         # s[18:19] saved exec
+S_CNT = 20          # s20.. loop counters by depth
+S_MASK = 24         # s[24+2d : 25+2d] branch masks by depth
+S_JMP = 30          # s[30:31] long-branch temporary
+S_VALID = 36        # s[36:37] lane mask: output valid (not infinity / f != 0)
+
+
+class AllocError(Exception):
+    pass
+
+
+class ValState:
+    __slots__ = ("val", "locs", "uses", "var")
+
+    def __init__(self, val):
+        self.val = val
+        self.locs = set()   # ("V"|"A"|"L"|"M", k)
+        self.uses = []      # item positions (in the defining block) that read it
+        self.var = None     # name of the variable whose home holds it (getvar values)
+
+
+class Emitter:
+    def __init__(self, prog, cfg):
+        self.prog = prog
+        self.cfg = cfg          # kernel config (kernels.py): loads / stores / flags
+        self.code = []
+        self.nlabel = 0
+        self.vslot = [None] * NV            # ValState or None
+        self.aslot = [None] * NA            # owner: ("val", vs) | ("var", name) | None
+        self.lslot = [None] * NL_SLOTS
+        self.mslot = []
+        self.home = {}                      # var name -> loc
+        self.states = {}                    # val id -> ValState
+        self.depth = 0
+        self.pinned = set()                 # V slots that must not be evicted now
+        self.stats = {}
+        self.recent_vwrite = {}             # VGPR -> instruction index of last VALU write
+        self.recent_awrite = {}
+        self.mem_stores_pending = False
+        self.debug = False
+        self.weight = 1
+        self.ensuring = None
+        self.defer_vm_wait = False   # batch the waits of one operation's HBM reloads
+        self.vm_wait_owed = False
+
+    # ---------------- emission helpers ----------------
+    def i(self, *t):
+        self.code.append(t)
+
+    def label(self):
+        self.nlabel += 1
+        return ".L%s_%d" % (self.prog.name, self.nlabel)
+
+    def bump(self, k, n=1):
+        self.stats[k] = self.stats.get(k, 0) + n
+        # dynamic estimate: weighted by the trip counts of the enclosing loops
+        self.stats["dyn_" + k] = self.stats.get("dyn_" + k, 0) + n * self.weight
+
+    @staticmethod
+    def vbase(k):
+        return VSLOT0 + 14 * k
+
+    # ---------------- slot bookkeeping ----------------
+    def free_vslot(self):
+        for k in range(NV):
+            if self.vslot[k] is None:
+                return k
+        return None
+
+    def next_use(self, vs, pos):
+        for u in vs.uses:
+            if u > pos:
+                return u
+        return 1 << 30
+
+    def get_vslot(self, pos, avoid=()):
+        k = self.free_vslot()
+        if k is not None:
+            return k
+        # Belady, cost-weighted: a value with a copy elsewhere is dropped for
+        # free, so it is preferred unless it is needed much sooner
+        best, bk = -1, None
+        for k in range(NV):
+            if k in avoid or k in self.pinned:
+                continue
+            vs = self.vslot[k]
+            nu = self.next_use(vs, pos) - pos
+            clean = len(vs.locs) > 1
+            score = nu * (3 if clean else 1)
+            if score > best:
+                best, bk = score, k
+        if bk is None:
+            raise AllocError("no evictable V slot")
+        self.evict(bk, pos)
+        return bk
+
+    def evict(self, k, pos):
+        vs = self.vslot[k]
+        vs.locs.discard(("V", k))
+        if not vs.locs:
+            loc = self.tier_slot(vs, pos)
+            self.copy(("V", k), loc)
+            self.own(loc, vs)
+            vs.locs.add(loc)
+            self.bump("spill_" + loc[0])
+        self.vslot[k] = None
+
+    def tier_slot(self, vs, pos):
+        """spill destination: a free A or L slot; else demote the A/L-resident
+        spill with the furthest next use to M if it is needed later than vs"""
+        for kind, tab in (("A", self.aslot), ("L", self.lslot)):
+            for k, o in enumerate(tab):
+                if o is None:
+                    return (kind, k)
+        mine = self.next_use(vs, pos)
+        best, bl = mine, None
+        for kind, tab in (("A", self.aslot), ("L", self.lslot)):
+            for k, o in enumerate(tab):
+                if (o is not None and o[0] == "val" and o[1].val.id in self.local_ids
+                        and o[1] is not self.ensuring and not any(l[0] == "V" and l[1] in self.pinned
+                                                                  for l in o[1].locs)):
+                    nu = self.next_use(o[1], pos)
+                    if nu > best:
+                        best, bl = nu, (kind, k)
+        if bl is None:
+            return self.spill_slot(prefer="M")
+        other = (self.aslot if bl[0] == "A" else self.lslot)[bl[1]][1]
+        m = self.spill_slot(prefer="M")
+        self.copy_via_work(bl, m)
+        other.locs.discard(bl)
+        other.locs.add(m)
+        self.own(m, other)
+        self.bump("demote_" + bl[0])
+        return bl
+
+    def copy_via_work(self, src, dst):
+        """A/L -> M through the work area v0..v13 (free between operations)"""
+        sk, s = src
+        if sk == "A":
+            for j in range(14):
+                self.i("v_accvgpr_read_b32", j, A(14 * s + j))
+        else:
+            for j in range(7):
+                self.i("ds_read_b64", 2 * j, LOFF, s * SLOT_BYTES + 512 * j)
+            self.i("s_waitcnt_lgkm0")
+        d = dst[1]
+        self.i("s_add_u32", S(S_TMP), S(S_WS), K(d * SLOT_BYTES))
+        self.i("s_addc_u32", S(S_TMP + 1), S(S_WS + 1), K(0))
+        for j in range(7):
+            self.i("global_store_dwordx2_s", LOFF, 2 * j, S(S_TMP), 512 * j)
+        self.mem_stores_pending = True
+
+    def own(self, loc, vs):
+        kind, k = loc
+        if kind == "A":
+            self.aslot[k] = ("val", vs)
+        elif kind == "L":
+            self.lslot[k] = ("val", vs)
+        elif kind == "M":
+            self.mslot[k] = ("val", vs)
+        elif kind == "V":
+            self.vslot[k] = vs
+
+    def spill_slot(self, prefer="A"):
+        order = {"A": "ALM", "L": "LAM", "M": "MLA"}[prefer]
+        for kind in order:
+            tab = {"A": self.aslot, "L": self.lslot, "M": self.mslot}[kind]
+            for k, o in enumerate(tab):
+                if o is None:
+                    return (kind, k)
+            if kind == "M":
+                self.mslot.append(None)
+                return ("M", len(self.mslot) - 1)
+        raise AllocError("no spill slot")
+
+    def release_loc(self, loc, vs):
+        kind, k = loc
+        tab = {"A": self.aslot, "L": self.lslot, "M": self.mslot}.get(kind)
+        if kind == "V":
+            if self.vslot[k] is vs:
+                self.vslot[k] = None
+        elif tab[k] == ("val", vs):
+            tab[k] = None
+
+    def kill(self, vs):
+        for loc in list(vs.locs):
+            self.release_loc(loc, vs)
+        vs.locs.clear()
+
+    # ---------------- data movement ----------------
+    def copy(self, src, dst):
+        """move one Fq between locations (src and dst kinds may differ)"""
+        sk, s = src
+        dk, d = dst
+        self.bump("move_%s%s" % (sk, dk))
+        if sk == "V" and dk == "V":
+            for j in range(7):
+                self.i("v_mov_b64", self.vbase(d) + 2 * j, self.vbase(s) + 2 * j)
+        elif sk == "V" and dk == "A":
+            for j in range(14):
+                self.i("v_accvgpr_write_b32", A(14 * d + j), self.vbase(s) + j)
+        elif sk == "A" and dk == "V":
+            for j in range(14):
+                self.i("v_accvgpr_read_b32", self.vbase(d) + j, A(14 * s + j))
+        elif sk == "V" and dk == "L":
+            for j in range(7):
+                self.i("ds_write_b64", LOFF, self.vbase(s) + 2 * j, d * SLOT_BYTES + 512 * j)
+        elif sk == "L" and dk == "V":
+            for j in range(7):
+                self.i("ds_read_b64", self.vbase(d) + 2 * j, LOFF, s * SLOT_BYTES + 512 * j)
+            self.i("s_waitcnt_lgkm0")
+        elif sk == "V" and dk == "M":
+            self.i("s_add_u32", S(S_TMP), S(S_WS), K(d * SLOT_BYTES))
+            self.i("s_addc_u32", S(S_TMP + 1), S(S_WS + 1), K(0))
+            for j in range(7):
+                self.i("global_store_dwordx2_s", LOFF, self.vbase(s) + 2 * j, S(S_TMP), 512 * j)
+            self.mem_stores_pending = True
+        elif sk == "M" and dk == "V":
+            if self.mem_stores_pending:
+                self.i("s_waitcnt_vm0")
+                self.mem_stores_pending = False
+            self.i("s_add_u32", S(S_TMP), S(S_WS), K(s * SLOT_BYTES))
+            self.i("s_addc_u32", S(S_TMP + 1), S(S_WS + 1), K(0))
+            for j in range(7):
+                self.i("global_load_dwordx2_s", self.vbase(d) + 2 * j, LOFF, S(S_TMP), 512 * j)
+            if self.defer_vm_wait:
+                self.vm_wait_owed = True
+            else:
+                self.i("s_waitcnt_vm0")
+        else:
+            # via a V slot is the caller's job
+            raise AllocError("copy %s -> %s" % (src, dst))
+
+    def best_src(self, vs):
+        for kind in "VALM":
+            for loc in vs.locs:
+                if loc[0] == kind:
+                    return loc
+        raise AllocError("value %r has no location" % vs.val)
+
+    def ensure_v(self, vs, pos, avoid):
+        for loc in vs.locs:
+            if loc[0] == "V":
+                return loc[1]
+        self.ensuring = vs
+        k = self.get_vslot(pos, avoid)   # may demote other spills (not vs)
+        self.ensuring = None
+        src = self.best_src(vs)
+        self.copy(src, ("V", k))
+        self.vslot[k] = vs
+        vs.locs.add(("V", k))
+        self.bump("reload_" + src[0])
+        return k
+
+    # ---------------- ops ----------------
+    def emit_sop(self, pairs, d):
+        first = True
+        acc = (ACC, ACC + 1)
+        for k in range(2 * NL - 1):
+            for a, b in pairs:
+                for i in range(max(0, k - NL + 1), min(k, NL - 1) + 1):
+                    self.i("v_mad_u64_u32", ACC, a + i, b + k - i, K(0) if first else ACC)
+                    first = False
+            for i in range(max(0, k - NL + 1), min(k - 1, NL - 1) + 1):
+                self.i("v_mad_u64_u32", ACC, M0 + i, S(SQ + k - i), ACC)
+            if k < NL:
+                self.i("v_mul_lo_u32", M0 + k, ACC, S(SQINV))
+                self.i("v_and_b32", M0 + k, K(MASK), M0 + k)
+                self.i("v_mad_u64_u32", ACC, M0 + k, S(SQ), ACC)
+            else:
+                self.i("v_and_b32", d + k - NL, K(MASK), ACC)
+            self.i("v_lshrrev_b64", ACC, K(28), ACC)
+        self.i("v_mov_b32", d + NL - 1, ACC)
+        del acc
+
+    def emit_red(self, x, d):
+        self.i("v_mad_u64_u32", ACC, x + 12, S(SKQ), K(0))
+        self.i("v_mad_u64_u32", 4, x + 13, S(SKQ), K(0))
+        self.i("v_lshrrev_b64", ACC, K(28), ACC)
+        self.i("v_lshl_add_u64", ACC, 4, K(0), ACC)
+        self.i("v_lshrrev_b32", 2, K(4), ACC + 1)          # k
+        self.i("v_sub_u32", 3, K(0), 2)                     # -k
+        for i in range(NL):
+            self.i("v_mad_u64_u32", ACC, x + i, K(1), K(0) if i == 0 else ACC)
+            self.i("v_mad_i64_i32", ACC, 3, S(SQ + i), ACC)
+            if i < NL - 1:
+                self.i("v_and_b32", d + i, K(MASK), ACC)
+                self.i("v_ashrrev_i64", ACC, K(28), ACC)
+            else:
+                self.i("v_mov_b32", d + i, ACC)
+
+    def emit_add(self, a, b, d):
+        for i in range(NL):
+            self.i("v_add_u32", d + i, a + i, b + i)
+
+    def emit_sub(self, a, b, d, ub):
+        c = SUBC[ub]
+        if d == b:
+            assert a != b
+            for i in range(NL):
+                self.i("v_sub_u32", d + i, K(c[i]), b + i)
+                self.i("v_add_u32", d + i, a + i, d + i)
+        else:
+            for i in range(NL):
+                self.i("v_add_u32", d + i, K(c[i]), a + i)
+                self.i("v_sub_u32", d + i, d + i, b + i)
+
+    def emit_neg(self, b, d, ub):
+        c = SUBC[ub]
+        for i in range(NL):
+            self.i("v_sub_u32", d + i, K(c[i]), b + i)
+
+    def emit_const(self, limbs, d):
+        for i in range(NL):
+            self.i("v_mov_b32", d + i, K(limbs[i]))
+
+    # ---------------- blocks ----------------
+    def analyse(self, block):
+        """ValStates + use positions for the values defined in `block`"""
+        for pos, it in enumerate(block.items):
+            if isinstance(it, Op):
+                for v in it.srcs:
+                    self.states[v.id].uses.append(pos)
+                if it.dst is not None:
+                    self.states[it.dst.id] = ValState(it.dst)
+
+    def var_ranges(self, block):
+        """for each var touched in `block` (at any depth): (first, last) item position"""
+        rng = {}
+
+        def touch(name, pos):
+            f, l = rng.get(name, (pos, pos))
+            rng[name] = (min(f, pos), max(l, pos))
+
+        def walk(b, pos):
+            for it in b.items:
+                if isinstance(it, (Loop, If)):
+                    walk(it.body, pos)
+                elif it.kind in ("getvar", "setvar"):
+                    touch(it.imm, pos)
+
+        for pos, it in enumerate(block.items):
+            if isinstance(it, (Loop, If)):
+                walk(it.body, pos)
+            elif it.kind in ("getvar", "setvar"):
+                touch(it.imm, pos)
+        return rng
+
+    def alloc_home(self, name, pos):
+        var = self.prog.vars[name]
+        pref = (var.home or "A")[0] if isinstance(var.home, str) else "A"
+        loc = self.spill_slot(prefer=pref)
+        if pref != "M" and loc[0] != pref:
+            # the preferred tier is full of spills: push the coldest one to M
+            tab = self.aslot if pref == "A" else self.lslot
+            best, bk = -1, None
+            for k, o in enumerate(tab):
+                if o is not None and o[0] == "val":
+                    nu = self.next_use(o[1], pos)
+                    if nu > best:
+                        best, bk = nu, k
+            if bk is not None:
+                other = tab[bk][1]
+                m = self.spill_slot(prefer="M")
+                self.copy_via_work((pref, bk), m)
+                other.locs.discard((pref, bk))
+                other.locs.add(m)
+                self.own(m, other)
+                self.bump("demote_home_" + pref)
+                tab[bk] = None
+                loc = (pref, bk)
+        tab = {"A": self.aslot, "L": self.lslot, "M": self.mslot}[loc[0]]
+        tab[loc[1]] = ("var", name)
+        self.home[name] = loc
+
+    def free_home(self, name, pos):
+        """the variable is dead; values read from it may still be live and keep
+        the slot as their own storage"""
+        loc = self.home.pop(name)
+        tab = {"A": self.aslot, "L": self.lslot, "M": self.mslot}[loc[0]]
+        tab[loc[1]] = None
+        for vs in self.states.values():
+            if loc in vs.locs:
+                if self.next_use(vs, pos) == 1 << 30:
+                    vs.locs.discard(loc)
+                elif tab[loc[1]] is None:
+                    tab[loc[1]] = ("val", vs)
+                else:
+                    vs.locs.discard(loc)
+                    if not vs.locs:
+                        raise AllocError("two live readers of dead variable %s" % name)
+
+    def run_block(self, block, top=False):
+        self.analyse(block)
+        saved_ids = getattr(self, "local_ids", set())
+        self.local_ids = self.block_vals(block)
+        vr = self.var_ranges(block) if top else {}
+        for pos, it in enumerate(block.items):
+            if top:
+                for name, (f, _) in vr.items():
+                    if f == pos and name not in self.home:
+                        self.alloc_home(name, pos)
+            if isinstance(it, (Loop, If)):
+                self.park(block, pos)
+                self.run_construct(it)
+            else:
+                self.run_op(it, pos)
+            if top:
+                for name, (_, l) in vr.items():
+                    if l == pos and name in self.home:
+                        self.free_home(name, pos)
+        # everything defined here is dead now
+        for k in range(NV):
+            vs = self.vslot[k]
+            if vs is not None and vs.val.id in self.local_ids:
+                self.kill(vs)
+        self.local_ids = saved_ids
+
+    def block_vals(self, block):
+        return {it.dst.id for it in block.items if isinstance(it, Op) and it.dst is not None}
+
+    def park(self, block, pos):
+        """before a construct: values of this block live after it leave the V
+        slots (the body needs them all)"""
+        ids = self.block_vals(block)
+        for k in range(NV):
+            vs = self.vslot[k]
+            if vs is None or vs.val.id not in ids:
+                continue
+            if self.next_use(vs, pos) == 1 << 30:
+                self.kill(vs)
+                continue
+            vs.locs.discard(("V", k))
+            self.vslot[k] = None
+            for loc in list(vs.locs):
+                if loc in self.home.values():
+                    vs.locs.discard(loc)
+            if not vs.locs:
+                loc = self.spill_slot(prefer="M")
+                self.copy(("V", k), loc)
+                self.own(loc, vs)
+                vs.locs.add(loc)
+                self.bump("park_" + loc[0])
+
+    def run_construct(self, it):
+        d = self.depth
+        self.depth += 1
+        w0 = self.weight
+        if isinstance(it, Loop):
+            self.weight = w0 * it.trips
+            it.sreg = S_CNT + d
+            top, done = self.label(), None
+            self.i("s_mov_b32", S(it.sreg), K(it.trips - 1))
+            self.i("label", top)
+            self.run_block(it.body)
+            self.i("s_sub_u32", S(it.sreg), S(it.sreg), K(1))
+            self.i("s_cmp_ge_i32", S(it.sreg), K(0))
+            self.i("long_cbranch_scc1", top)
+            del done
+        else:
+            skip = self.label()
+            m = S_MASK + 2 * d
+            self.i("s_mov_b32", S(m), K(it.mask & 0xffffffff))
+            self.i("s_mov_b32", S(m + 1), K(it.mask >> 32))
+            self.i("s_bitcmp1_b64", S(m), S(it.loop.sreg))
+            self.weight = w0 * bin(it.mask).count("1") / max(1, it.loop.trips)
+            self.i("long_cbranch_scc0", skip)
+            self.run_block(it.body)
+            self.i("label", skip)
+        self.weight = w0
+        self.depth -= 1
+
+    def run_op(self, op, pos):
+        k = op.kind
+        self.bump("op_" + k)
+        if k == "getvar":
+            vs = self.states[op.dst.id]
+            loc = self.home[op.imm]
+            vs.locs.add(loc)
+            vs.var = op.imm
+            if not vs.uses:
+                self.kill(vs)
+            return
+        if k == "setvar":
+            self.do_setvar(op, pos)
+            return
+        srcs = [self.states[v.id] for v in op.srcs]
+        self.pinned = set()
+        sk = []
+        self.defer_vm_wait = True
+        for vs in srcs:
+            kk = self.ensure_v(vs, pos, avoid=self.pinned)
+            self.pinned.add(kk)
+            sk.append(kk)
+        self.defer_vm_wait = False
+        if self.vm_wait_owed:
+            self.i("s_waitcnt_vm0")
+            self.vm_wait_owed = False
+        dying = [vs for vs in srcs if self.next_use(vs, pos) == 1 << 30]
+        if op.dst is not None:
+            dvs = self.states[op.dst.id]
+            # in place over a dying source (safe for every op kind below)
+            dk = None
+            for vs, kk in zip(srcs, sk):
+                if vs in dying and self.vslot[kk] is vs and not (k == "sub" and op.srcs[0].id == op.srcs[1].id):
+                    dk = kk
+                    break
+            if dk is None:
+                dk = self.get_vslot(pos, avoid=self.pinned)
+        else:
+            dk = None
+        base = [self.vbase(x) for x in sk]
+        d = self.vbase(dk) if dk is not None else None
+        if k == "sop":
+            self.emit_sop(list(zip(base[0::2], base[1::2])), d)
+        elif k == "sqr":
+            self.emit_sop([(base[0], base[0])], d)
+        elif k == "red":
+            self.emit_red(base[0], d)
+        elif k == "add":
+            self.emit_add(base[0], base[1], d)
+        elif k == "sub":
+            self.emit_sub(base[0], base[1], d, op.imm)
+        elif k == "neg":
+            self.emit_neg(base[0], d, op.imm)
+        elif k == "const":
+            self.emit_const(op.imm, d)
+        elif k == "load_raw":
+            self.cfg.emit_load(self, op.imm, d)
+        elif k == "store_raw":
+            self.cfg.emit_store(self, op.imm, base[0])
+        else:
+            raise AllocError(k)
+        self.pinned = set()
+        for vs in dying:
+            # the destination may have taken its V slot
+            for loc in list(vs.locs):
+                if loc[0] == "V" and loc[1] == dk:
+                    vs.locs.discard(loc)
+                    continue
+                self.release_loc(loc, vs)
+            vs.locs.clear()
+        if op.dst is not None:
+            dvs = self.states[op.dst.id]
+            self.vslot[dk] = dvs
+            dvs.locs = {("V", dk)}
+            if self.debug:
+                self.i("mark", op.dst.id, d)
+            if not dvs.uses:
+                self.kill(dvs)
+
+    def do_setvar(self, op, pos):
+        name = op.imm
+        vs = self.states[op.srcs[0].id]
+        home = self.home[name]
+        if home[0] == "V":
+            raise AllocError("V homes unsupported")
+        # values still holding the old contents of this home keep a copy
+        for other in list(self.states.values()):
+            if other is not vs and home in other.locs:
+                if len(other.locs) == 1 and self.next_use(other, pos) != 1 << 30:
+                    self.ensure_v(other, pos, avoid=())
+                other.locs.discard(home)
+        if home not in vs.locs:
+            k = self.ensure_v(vs, pos, avoid=())
+            self.copy(("V", k), home)
+        if self.next_use(vs, pos) == 1 << 30:
+            self.kill(vs)

@@ -1,0 +1,190 @@
+"""Kernel-level glue for the generated kernels: argument layout, prologue,
+record loads / canonical stores, the lane masks for infinity (Miller loop)
+and f == 0 (final exponentiation), epilogue.
+
+Kernel arguments (5 x 8 bytes, all kernels):
+  miller_loop: p_aff (G1Affine, 13 u64), q_aff (G2Affine, 25 u64), out (Fq12, 72 u64), n, workspace
+  final_exp:   in (Fq12), out (Fq12), ok (u8 per lane, may be null), n, workspace
+"""
+import gen_fl
+from dsl import Q
+from emit import (A, ACC, ADDR, GID, K, LOFF, ORACC, S, S_ARG, S_EXEC, S_KARG, S_TMP, S_VALID, S_WG, S_WS,
+                  SKQ, SQ, SQINV, NL, MASK, QL, QINV28, KQ)
+
+ONE_ABI = (1 << 384) % Q          # Montgomery one in the ABI (R = 2^384)
+S_STRIDE = 32
+
+
+def words32(x, n=12):
+    return [(x >> (32 * j)) & 0xffffffff for j in range(n)]
+
+
+class KernelCfg:
+    name = None
+    args = ()
+    records = {}          # input slot -> (arg index, record bytes, byte offset)
+    out_arg, out_bytes = 2, 576
+
+    def emit_prologue(self, em, code, nmem, end_label):
+        i = code.append
+        for a in range(5):
+            i(("s_load_dwordx2", S(S_ARG + 2 * a), S(S_KARG), 8 * a))
+        i(("s_waitcnt_lgkm0",))
+        i(("v_lshlrev_b32", LOFF, K(3), 0))
+        i(("v_lshl_add_u32", GID, S(S_WG), K(6), 0))   # global lane index
+        i(("v_cmp_gt_u32", S(S_ARG + 6), GID))
+        i(("s_and_saveexec_b64", S(S_EXEC)))
+        i(("long_cbranch_execz", end_label))
+        for k, w in enumerate(QL):
+            i(("s_mov_b32", S(SQ + k), K(w)))
+        i(("s_mov_b32", S(SQINV), K(QINV28)))
+        i(("s_mov_b32", S(SKQ), K(KQ)))
+        wave_bytes = max(nmem, 1) * gen_fl.NL * 4 * 64
+        i(("s_mul_i32", S(S_TMP), S(S_WG), K(wave_bytes)))
+        i(("s_mul_hi_u32", S(S_TMP + 1), S(S_WG), K(wave_bytes)))
+        i(("s_add_u32", S(S_WS), S(S_ARG + 8), S(S_TMP)))
+        i(("s_addc_u32", S(S_WS + 1), S(S_ARG + 9), S(S_TMP + 1)))
+        self.prologue_masks(em, code)
+
+    def prologue_masks(self, em, code):
+        pass
+
+    def lane_addr(self, code, arg, stride):
+        # global lane index from tid * 8; one SGPR per VALU instruction
+        # (constant bus): the base goes through VGPRs
+        code.append(("v_lshrrev_b32", GID, K(3), LOFF))
+        code.append(("v_lshl_add_u32", GID, S(S_WG), K(6), GID))
+        code.append(("v_mov_b64", ADDR, S(S_ARG + 2 * arg)))
+        code.append(("s_mov_b32", S(S_STRIDE), K(stride)))
+        code.append(("v_mad_u64_u32", ADDR, GID, S(S_STRIDE), ADDR))
+
+    def emit_load(self, em, slot, d):
+        arg, stride, off = self.records[slot]
+        self.lane_addr(em.code, arg, stride)
+        for j in range(6):
+            em.i("global_load_dwordx2", 2 * j, ADDR, off + 8 * j)
+        em.i("s_waitcnt_vm0")
+        self.after_load(em, slot)
+        for li in range(NL):
+            bit = 28 * li
+            wi, sh = bit // 32, bit % 32
+            if wi + 1 < 12:
+                em.i("v_alignbit_b32", d + li, wi + 1, wi, K(sh))
+                em.i("v_and_b32", d + li, K(MASK), d + li)
+            else:
+                em.i("v_lshrrev_b32", d + li, K(sh), wi)
+
+    def after_load(self, em, slot):
+        pass
+
+    def emit_store(self, em, slot, t):
+        # canonical: t (limbs < 2^28, value < 2q) -> t mod q, in place
+        bor = 14
+        for li in range(NL):
+            em.i("v_subrev_u32", li, K(QL[li]), t + li)
+            if li:
+                em.i("v_add_u32", li, li, bor)
+            em.i("v_ashrrev_i32", bor, K(28), li)
+            em.i("v_and_b32", li, K(MASK), li)
+        for li in range(NL):
+            em.i("v_bfi_b32", t + li, bor, t + li, li)   # t < q ? t : t - q
+        # pack 14 x 28 -> 12 x 32 into v0..v11
+        for j in range(12):
+            bit = 32 * j
+            li, sh = bit // 28, bit % 28
+            em.i("v_lshrrev_b32", j, K(sh), t + li)
+            em.i("v_lshl_or_b32", j, t + li + 1, K(28 - sh), j)
+            if 56 - sh < 32 and li + 2 < NL:
+                em.i("v_lshl_or_b32", j, t + li + 2, K(56 - sh), j)
+        # lanes that are not valid get the fixed value
+        em.i("s_mov_b64", S(106), S(S_VALID))
+        em.i("s_nop", 1)
+        for j, w in enumerate(self.invalid_words(slot)):
+            if -16 <= w <= 64:      # inline constant: no constant-bus slot
+                em.i("v_cndmask_b32", j, K(w), j)
+            else:                   # literal + VCC would need two
+                em.i("v_mov_b32", 15, K(w))
+                em.i("v_cndmask_b32", j, 15, j)
+        self.lane_addr(em.code, self.out_arg, self.out_bytes)
+        for j in range(6):
+            em.i("global_store_dwordx2", ADDR, 2 * j, 48 * slot + 8 * j)
+
+    def invalid_words(self, slot):
+        raise NotImplementedError
+
+    def emit_epilogue(self, em, code):
+        pass
+
+
+class MillerLoopCfg(KernelCfg):
+    name = "pa_gen_miller_loop"
+    records = {0: (0, 104, 0), 1: (0, 104, 48),
+               2: (1, 200, 0), 3: (1, 200, 48), 4: (1, 200, 96), 5: (1, 200, 144)}
+
+    def prologue_masks(self, em, code):
+        # valid = neither P nor Q is the point at infinity (mod.rs:50-54)
+        self.lane_addr(code, 0, 104)
+        code.append(("global_load_dword", 0, ADDR, 96))
+        self.lane_addr(code, 1, 200)
+        code.append(("global_load_dword", 1, ADDR, 192))
+        code.append(("s_waitcnt_vm0",))
+        code.append(("v_or_b32", 0, 0, 1))
+        code.append(("v_and_b32", 0, K(0xff), 0))
+        code.append(("v_cmp_eq_u32", K(0), 0))
+        code.append(("s_nop", 1))
+        code.append(("s_mov_b64", S(S_VALID), S(106)))
+
+    def invalid_words(self, slot):
+        # one (fq12.rs): only coordinate 0 is one
+        return words32(ONE_ABI) if slot == 0 else [0] * 12
+
+
+class FinalExpCfg(KernelCfg):
+    name = "pa_gen_final_exp"
+    records = {k: (0, 576, 48 * k) for k in range(12)}
+    out_arg = 1
+
+    def prologue_masks(self, em, code):
+        code.append(("v_mov_b32", ORACC, K(0)))
+
+    def after_load(self, em, slot):
+        for j in range(12):
+            em.i("v_or_b32", ORACC, ORACC, j)
+        if slot == 11:
+            em.i("v_cmp_ne_u32", K(0), ORACC)
+            em.i("s_nop", 1)
+            em.i("s_mov_b64", S(S_VALID), S(106))
+
+    def invalid_words(self, slot):
+        return [0] * 12      # reference: None; the C ABI writes zero and ok = 0
+
+    def emit_epilogue(self, em, code):
+        skip = em.label()
+        code.append(("s_cmp_eq_u64", S(S_ARG + 4), K(0)))
+        code.append(("long_cbranch_scc1", skip))
+        code.append(("v_mov_b32", 1, K(1)))
+        code.append(("s_mov_b64", S(106), S(S_VALID)))
+        code.append(("s_nop", 1))
+        code.append(("v_cndmask_b32", 0, K(0), 1))
+        self.lane_addr(code, 2, 1)
+        code.append(("global_store_byte", ADDR, 0, 0))
+        code.append(("label", skip))
+
+
+def build(prog, cfg, debug=False):
+    """allocate + emit: returns (code list, emitter)"""
+    from emit import Emitter
+    em = Emitter(prog, cfg)
+    em.debug = debug
+    em.run_block(prog.root, top=True)
+    body = em.code
+    code = []
+    end = em.label()
+    cfg.emit_prologue(em, code, len(em.mslot), end)
+    code.extend(body)
+    cfg.emit_epilogue(em, code)
+    code.append(("label", end))
+    code.append(("s_endpgm",))
+    em.code = code
+    em.lds_bytes = max(1, sum(1 for _ in range(len(em.lslot)))) * gen_fl.NL * 4 * 64
+    return code, em

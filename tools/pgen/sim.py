@@ -1,0 +1,259 @@
+"""Single-lane simulator of the instruction subset emit.py / kcfg.py produce.
+
+Executes the abstract instruction list (before text rendering) for one lane
+with a 256 VGPR / 256 AGPR / 108 SGPR register file, byte-addressed global
+memory and per-lane LDS, so register-allocation or emission bugs show up on
+the CPU as a difference against dsl.evaluate.
+"""
+M32 = 0xffffffff
+M64 = (1 << 64) - 1
+
+
+def sx32(x):
+    x &= M32
+    return x - (1 << 32) if x >> 31 else x
+
+
+def sx64(x):
+    x &= M64
+    return x - (1 << 64) if x >> 63 else x
+
+
+class Sim:
+    def __init__(self, code, lane=0):
+        self.code = code
+        self.v = [0] * 256
+        self.a = [0] * 256
+        self.s = [0] * 108
+        self.scc = 0
+        self.mem = {}       # dword address -> u32
+        self.lds = {}
+        self.lane = lane
+        self.labels = {t[1]: i for i, t in enumerate(code) if t[0] == "label"}
+        self.count = 0
+        self.trace = None
+
+    # ---------- operand access ----------
+    def rd(self, x):
+        if isinstance(x, tuple):
+            return x[1] & M32
+        if x >= 512:
+            return self.s[x - 512]
+        if x >= 256:
+            return self.a[x - 256]
+        return self.v[x]
+
+    def rd64(self, x):
+        if isinstance(x, tuple):
+            return x[1] & M64
+        if x >= 512:
+            return self.s[x - 512] | (self.s[x - 511] << 32)
+        return self.v[x] | (self.v[x + 1] << 32)
+
+    def wr(self, x, val):
+        val &= M32
+        if x >= 512:
+            self.s[x - 512] = val
+        elif x >= 256:
+            self.a[x - 256] = val
+        else:
+            self.v[x] = val
+
+    def wr64(self, x, val):
+        self.wr(x, val & M32)
+        self.wr(x + 1, (val >> 32) & M32)
+
+    def set_vcc(self, bit):
+        m = self.s[106] | (self.s[107] << 32)
+        b = self.lane % 64
+        m = (m & ~(1 << b)) | (int(bool(bit)) << b)
+        self.s[106], self.s[107] = m & M32, m >> 32
+
+    def vcc(self):
+        m = self.s[106] | (self.s[107] << 32)
+        return (m >> (self.lane % 64)) & 1
+
+    def ld32(self, addr):
+        return self.mem.get(addr, 0)
+
+    def st32(self, addr, val):
+        self.mem[addr] = val & M32
+
+    # ---------- execution ----------
+    def run(self, max_steps=10 ** 9):
+        code = self.code
+        pc = 0
+        n = len(code)
+        while pc < n:
+            t = code[pc]
+            self.count += 1
+            if self.count > max_steps:
+                raise RuntimeError("step limit")
+            nxt = self.step(t)
+            if nxt == "end":
+                return
+            pc = self.labels[nxt] if nxt is not None else pc + 1
+
+    def step(self, t):
+        m = t[0]
+        a = t[1:]
+        rd, rd64, wr, wr64 = self.rd, self.rd64, self.wr, self.wr64
+        if m == "v_mad_u64_u32":
+            r = rd(a[1]) * rd(a[2]) + rd64(a[3])
+            wr64(a[0], r)
+            self.set_vcc(r >> 64)
+        elif m == "v_mad_i64_i32":
+            r = sx32(rd(a[1])) * sx32(rd(a[2])) + sx64(rd64(a[3]))
+            wr64(a[0], r)
+        elif m == "v_mul_lo_u32":
+            wr(a[0], rd(a[1]) * rd(a[2]))
+        elif m == "v_and_b32":
+            wr(a[0], rd(a[1]) & rd(a[2]))
+        elif m == "v_or_b32":
+            wr(a[0], rd(a[1]) | rd(a[2]))
+        elif m == "v_add_u32":
+            wr(a[0], rd(a[1]) + rd(a[2]))
+        elif m == "v_sub_u32":
+            wr(a[0], rd(a[1]) - rd(a[2]))
+        elif m == "v_subrev_u32":
+            wr(a[0], rd(a[2]) - rd(a[1]))
+        elif m == "v_lshrrev_b32":
+            wr(a[0], rd(a[2]) >> (rd(a[1]) & 31))
+        elif m == "v_lshlrev_b32":
+            wr(a[0], rd(a[2]) << (rd(a[1]) & 31))
+        elif m == "v_ashrrev_i32":
+            wr(a[0], sx32(rd(a[2])) >> (rd(a[1]) & 31))
+        elif m == "v_lshrrev_b64":
+            wr64(a[0], rd64(a[2]) >> (rd(a[1]) & 63))
+        elif m == "v_ashrrev_i64":
+            wr64(a[0], sx64(rd64(a[2])) >> (rd(a[1]) & 63))
+        elif m == "v_lshl_add_u64":
+            wr64(a[0], (rd64(a[1]) << (rd(a[2]) & 63)) + rd64(a[3]))
+        elif m == "v_lshl_add_u32":
+            wr(a[0], (rd(a[1]) << (rd(a[2]) & 31)) + rd(a[3]))
+        elif m == "v_lshl_or_b32":
+            wr(a[0], (rd(a[1]) << (rd(a[2]) & 31)) | rd(a[3]))
+        elif m == "v_alignbit_b32":
+            wr(a[0], ((rd(a[1]) << 32) | rd(a[2])) >> (rd(a[3]) & 31))
+        elif m == "v_bfi_b32":
+            msk = rd(a[1])
+            wr(a[0], (msk & rd(a[2])) | (~msk & rd(a[3])))
+        elif m == "v_cndmask_b32":
+            wr(a[0], rd(a[2]) if self.vcc() else rd(a[1]))
+        elif m == "v_mov_b32" or m == "v_accvgpr_write_b32" or m == "v_accvgpr_read_b32":
+            wr(a[0], rd(a[1]))
+        elif m == "v_mov_b64":
+            wr64(a[0], rd64(a[1]))
+        elif m == "v_cmp_gt_u32":
+            self.set_vcc(rd(a[0]) > rd(a[1]))
+        elif m == "v_cmp_eq_u32":
+            self.set_vcc(rd(a[0]) == rd(a[1]))
+        elif m == "v_cmp_ne_u32":
+            self.set_vcc(rd(a[0]) != rd(a[1]))
+        elif m == "ds_write_b64":
+            addr = rd(a[0]) + a[2]
+            self.lds[addr] = rd(a[1])
+            self.lds[addr + 4] = rd(a[1] + 1)
+        elif m == "ds_read_b64":
+            addr = rd(a[1]) + a[2]
+            wr(a[0], self.lds.get(addr, 0))
+            wr(a[0] + 1, self.lds.get(addr + 4, 0))
+        elif m == "global_load_dwordx2":
+            addr = rd64(a[1]) + a[2]
+            wr(a[0], self.ld32(addr))
+            wr(a[0] + 1, self.ld32(addr + 4))
+        elif m == "global_load_dword":
+            wr(a[0], self.ld32(rd64(a[1]) + a[2]))
+        elif m == "global_store_dwordx2":
+            addr = rd64(a[0]) + a[2]
+            self.st32(addr, rd(a[1]))
+            self.st32(addr + 4, rd(a[1] + 1))
+        elif m == "global_store_byte":
+            addr = rd64(a[0]) + a[2]
+            base = addr & ~3
+            sh = 8 * (addr & 3)
+            w = self.ld32(base)
+            self.st32(base, (w & ~(0xff << sh)) | ((rd(a[1]) & 0xff) << sh))
+        elif m == "global_store_dwordx2_s":
+            addr = rd64(a[2]) + rd(a[0]) + a[3]
+            self.st32(addr, rd(a[1]))
+            self.st32(addr + 4, rd(a[1] + 1))
+        elif m == "global_load_dwordx2_s":
+            addr = rd64(a[2]) + rd(a[1]) + a[3]
+            wr(a[0], self.ld32(addr))
+            wr(a[0] + 1, self.ld32(addr + 4))
+        elif m == "s_load_dwordx2":
+            addr = rd64(a[1]) + a[2]
+            wr(a[0], self.ld32(addr))
+            wr(a[0] + 1, self.ld32(addr + 4))
+        elif m == "s_mov_b32":
+            wr(a[0], rd(a[1]))
+        elif m == "s_mov_b64":
+            wr64(a[0], rd64(a[1]))
+        elif m == "s_add_u32":
+            r = rd(a[1]) + rd(a[2])
+            wr(a[0], r)
+            self.scc = r >> 32
+        elif m == "s_addc_u32":
+            r = rd(a[1]) + rd(a[2]) + self.scc
+            wr(a[0], r)
+            self.scc = r >> 32
+        elif m == "s_sub_u32":
+            r = rd(a[1]) - rd(a[2])
+            wr(a[0], r)
+            self.scc = int(r < 0)
+        elif m == "s_cmp_ge_i32":
+            self.scc = int(sx32(rd(a[0])) >= sx32(rd(a[1])))
+        elif m == "s_cmp_eq_u64":
+            self.scc = int(rd64(a[0]) == rd64(a[1]))
+        elif m == "s_bitcmp1_b64":
+            self.scc = (rd64(a[0]) >> (rd(a[1]) & 63)) & 1
+        elif m == "s_mul_i32":
+            wr(a[0], rd(a[1]) * rd(a[2]))
+        elif m == "s_mul_hi_u32":
+            wr(a[0], (rd(a[1]) * rd(a[2])) >> 32)
+        elif m == "s_and_saveexec_b64":
+            if not self.vcc():
+                return "end"
+        elif m == "mark":
+            if self.trace is not None:
+                while True:
+                    vid, limbs, op = next(self.trace)
+                    if vid == a[0]:
+                        break
+                got = tuple(self.v[a[1] + i] for i in range(14))
+                if got != tuple(limbs):
+                    raise AssertionError("first divergence at %r (instr %d): got %s want %s" % (
+                        op, self.count, got, tuple(limbs)))
+        elif m in ("s_nop", "s_waitcnt_lgkm0", "s_waitcnt_vm0", "label"):
+            pass
+        elif m == "long_cbranch_scc1":
+            return a[0] if self.scc else None
+        elif m == "long_cbranch_scc0":
+            return None if self.scc else a[0]
+        elif m == "long_cbranch_execz":
+            return None
+        elif m == "s_endpgm":
+            return "end"
+        else:
+            raise NotImplementedError(m)
+        return None
+
+
+def run_lane(code, args, buffers, lane=0, max_steps=10 ** 9, trace=None):
+    """args: 5 u64 kernel arguments; buffers: {base_address: list of u64}"""
+    sm = Sim(code, lane)
+    sm.trace = iter(trace) if trace is not None else None
+    for base, words in buffers.items():
+        for i, w in enumerate(words):
+            sm.mem[base + 8 * i] = w & M32
+            sm.mem[base + 8 * i + 4] = (w >> 32) & M32
+    karg = 0x1000
+    for i, x in enumerate(args):
+        sm.mem[karg + 8 * i] = x & M32
+        sm.mem[karg + 8 * i + 4] = x >> 32
+    sm.s[0], sm.s[1] = karg, 0
+    sm.s[2] = lane // 64
+    sm.v[0] = lane % 64
+    sm.run(max_steps)
+    return sm

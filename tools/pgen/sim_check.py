@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Simulate one lane of a generated kernel (sim.py) and compare with the DSL
+golden model.  python tools/pgen/sim_check.py small|ml|fe"""
+import os
+import random
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [HERE, os.path.dirname(HERE)]
+import build_gen  # noqa: E402
+import dsl  # noqa: E402
+import sim  # noqa: E402
+
+
+def words(xs):
+    out = []
+    for x in xs:
+        out += [(x >> (64 * i)) & (2 ** 64 - 1) for i in range(6)]
+    return out
+
+
+def check(which, seed=5, lane=3, debug=True):
+    import kcfg
+    f = build_gen.PROGRAMS[which]
+    prog, cfg, kname, nmem = f()
+    code = f.cache["r"][4]
+    if debug:
+        code, _ = kcfg.build(prog, type(cfg)(), debug=True)
+    trace = []
+    rng = random.Random(seed)
+    IN, OUT, AUX, WS = 0x100000, 0x200000, 0x300000, 0x400000
+    if which in ("small", "fe"):
+        ins = [rng.randrange(dsl.Q) for _ in range(12)]
+        rec = [0] * (72 * lane) + words(ins)
+        want = dsl.evaluate(prog, {k: ins[k] for k in range(12)}, trace=trace)
+        args = [IN, OUT, AUX, lane + 1, WS]
+        bufs = {IN: rec}
+    else:
+        # any field values (the loop does not care whether they are on the curve)
+        ins = [rng.randrange(dsl.Q) for _ in range(6)]
+        prec = [0] * (13 * lane) + words(ins[:2]) + [0]
+        qrec = [0] * (25 * lane) + words(ins[2:]) + [0]
+        want = dsl.evaluate(prog, {k: ins[k] for k in range(6)}, trace=trace)
+        args = [IN, AUX, OUT, lane + 1, WS]
+        bufs = {IN: prec, AUX: qrec}
+    t = time.time()
+    sm = sim.run_lane(code, args, bufs, lane=lane, trace=trace if debug else None)
+    got = []
+    for k in range(12):
+        base = OUT + 576 * lane + 48 * k
+        got.append(sum(sm.mem.get(base + 4 * j, 0) << (32 * j) for j in range(12)))
+    ok = got == [want[k] for k in range(12)]
+    print("%s lane %d: %s (%d instructions simulated, %.1fs)" % (which, lane, "OK" if ok else "MISMATCH",
+                                                              sm.count, time.time() - t))
+    return ok
+
+
+if __name__ == "__main__":
+    sys.exit(0 if all(check(w) for w in sys.argv[1:] or ["small"]) else 1)

@@ -1,0 +1,252 @@
+"""BLS12-381 tower, line functions, Miller loop and final exponentiation
+written against the tracing DSL (dsl.py).  The formulas are those of
+pairing_amd/csrc/tower_fl.h / pairing_fl.h (themselves the reference's:
+fq2.rs, fq6.rs, fq12.rs, mod.rs -- cited per function below); the bound of
+every value is tracked by the DSL, and red() is placed exactly where the
+next operation's bound check needs it.
+
+Element encodings: Fq2 = (c0, c1) of Val; Fq6 = 3-tuple of Fq2;
+Fq12 = (Fq6, Fq6).
+"""
+from dsl import SUBCU, Q
+
+X_ABS = 0xD201000000010000  # |x|, x < 0 (mod.rs:23-25)
+
+
+def _frob_consts():
+    """Frobenius coefficients (fq.rs:139-498) as field values, derived as in
+    tools/gen_consts.py."""
+    import gen_consts as g
+    return g.FROB_FQ6_C1, g.FROB_FQ6_C2, g.FROB_FQ12_C1
+
+
+class Tower:
+    def __init__(self, p):
+        self.p = p
+
+    # ---------------- Fq2 ----------------
+    def add2(self, a, b): return (self.p.add(a[0], b[0]), self.p.add(a[1], b[1]))
+    def sub2(self, a, b): return (self.p.sub(a[0], b[0]), self.p.sub(a[1], b[1]))
+    def neg2(self, a): return (self.p.neg(a[0]), self.p.neg(a[1]))
+    def dbl2(self, a): return self.add2(a, a)
+    def red2(self, a): return (self.p.red(a[0]), self.p.red(a[1]))
+    def u2(self, a): return max(a[0].u, a[1].u)
+
+    def xi(self, a):  # fq2.rs:41-45, * (u + 1)
+        return (self.p.sub(a[0], a[1]), self.p.add(a[0], a[1]))
+
+    def conj2(self, a):
+        return (a[0], self.p.neg(a[1]))
+
+    def mul2(self, a, b):  # fq2.rs:123-136, schoolbook, one reduction per coordinate
+        p = self.p
+        A, B = self.u2(a), self.u2(b)
+        if SUBCU[A] * B <= A * SUBCU[B]:
+            c0 = p.sop(a[0], b[0], p.neg(a[1]), b[1])
+        else:
+            c0 = p.sop(a[0], b[0], a[1], p.neg(b[1]))
+        c1 = p.sop(a[0], b[1], a[1], b[0])
+        return (c0, c1)
+
+    def sqr2(self, a):  # fq2.rs:87-101
+        p = self.p
+        A = self.u2(a)
+        if 2 * A * (A + SUBCU[A]) <= 17:
+            c0 = p.mul(p.add(a[0], a[1]), p.sub(a[0], a[1]))
+        else:
+            c0 = p.sop(a[0], a[0], p.neg(a[1]), a[1])
+        c1 = p.mul(p.dbl(a[0]), a[1])
+        return (c0, c1)
+
+    def mul_fq(self, a, b):
+        return (self.p.mul(a[0], b), self.p.mul(a[1], b))
+
+    def lim2(self, a):
+        return a if self.u2(a) <= 2 else self.red2(a)
+
+    def const2(self, c):
+        return (self.p.const(c[0]), self.p.const(c[1]))
+
+    def one2(self):
+        return (self.p.const(1), self.p.const(0))
+
+    # ---------------- Fq6 ----------------
+    def add6(self, a, b): return tuple(self.add2(x, y) for x, y in zip(a, b))
+    def sub6(self, a, b): return tuple(self.sub2(x, y) for x, y in zip(a, b))
+    def neg6(self, a): return tuple(self.neg2(x) for x in a)
+    def red6(self, a): return tuple(self.red2(x) for x in a)
+    def u6(self, a): return max(self.u2(x) for x in a)
+    def mul_v(self, a): return (self.xi(a[2]), a[0], a[1])  # fq6.rs:32-38
+
+    def mul6(self, a, b):  # fq6.rs:199-248, Karatsuba
+        assert self.u6(a) <= 2 and self.u6(b) <= 2
+        t = self
+        v0 = t.mul2(a[0], b[0])
+        v1 = t.mul2(a[1], b[1])
+        v2 = t.mul2(a[2], b[2])
+        t0 = t.mul2(t.lim2(t.add2(a[1], a[2])), t.lim2(t.add2(b[1], b[2])))
+        t1 = t.mul2(t.lim2(t.add2(a[0], a[1])), t.lim2(t.add2(b[0], b[1])))
+        t2 = t.mul2(t.lim2(t.add2(a[0], a[2])), t.lim2(t.add2(b[0], b[2])))
+        c0 = t.red2(t.add2(t.xi(t.sub2(t0, t.add2(v1, v2))), v0))
+        c1 = t.red2(t.add2(t.sub2(t1, t.add2(v0, v1)), t.xi(v2)))
+        c2 = t.red2(t.add2(t.sub2(t2, t.add2(v0, v2)), v1))
+        return (c0, c1, c2)
+
+    def mul_by_1(self, a, c1):  # fq6.rs:40-66
+        xc = self.xi(c1)
+        return (self.mul2(a[2], xc), self.mul2(a[0], c1), self.mul2(a[1], c1))
+
+    def mul_by_01(self, a, c0, c1):  # fq6.rs:68-109
+        t = self
+        a_a = t.mul2(a[0], c0)
+        b_b = t.mul2(a[1], c1)
+        t1 = t.mul2(c1, t.lim2(t.add2(a[1], a[2])))
+        t3 = t.mul2(c0, t.lim2(t.add2(a[0], a[2])))
+        t2 = t.mul2(t.lim2(t.add2(c0, c1)), t.lim2(t.add2(a[0], a[1])))
+        r0 = t.red2(t.add2(t.xi(t.sub2(t1, b_b)), a_a))
+        r1 = t.red2(t.sub2(t2, t.add2(a_a, b_b)))
+        r2 = t.red2(t.add2(t.sub2(t3, a_a), b_b))
+        return (r0, r1, r2)
+
+    def frob6(self, a, power):  # fq6.rs:157-164
+        c6_1, c6_2, _ = _frob_consts()
+        if power & 1:
+            a = tuple(self.red2(self.conj2(x)) for x in a)
+        return (a[0], self.mul2(a[1], self.const2(c6_1[power % 6])),
+                self.mul2(a[2], self.const2(c6_2[power % 6])))
+
+    # ---------------- Fq12 ----------------
+    def conj12(self, a):  # fq12.rs:30-32
+        return (a[0], self.red6(self.neg6(a[1])))
+
+    # Operation order matters for register pressure (the allocator follows
+    # it): the product with freshly computed operands goes first, while the
+    # plain operands (often variable-backed, free to drop and re-read) wait.
+    def mul12(self, a, b):  # fq12.rs:116-130
+        t = self
+        cross = t.mul6(t.add6(a[0], a[1]), t.add6(b[0], b[1]))
+        aa = t.mul6(a[0], b[0])
+        bb = t.mul6(a[1], b[1])
+        c1 = t.red6(t.sub6(cross, t.add6(aa, bb)))
+        c0 = t.red6(t.add6(t.mul_v(bb), aa))
+        return (c0, c1)
+
+    def sqr12(self, a):  # fq12.rs:99-114
+        t = self
+        s = t.mul6(t.red6(t.add6(t.mul_v(a[1]), a[0])), t.add6(a[0], a[1]))
+        ab = t.mul6(a[0], a[1])
+        c0 = t.red6(t.sub6(s, t.add6(ab, t.mul_v(ab))))
+        c1 = t.red6(t.add6(ab, ab))
+        return (c0, c1)
+
+    def mul_by_014(self, a, c0, c1, c4):  # fq12.rs:34-48
+        t = self
+        s = t.mul_by_01(t.red6(t.add6(a[1], a[0])), c0, t.lim2(t.add2(c1, c4)))
+        aa = t.mul_by_01(a[0], c0, c1)
+        bb = t.mul_by_1(a[1], c4)
+        r1 = t.red6(t.sub6(s, t.add6(aa, bb)))
+        r0 = t.red6(t.add6(t.mul_v(bb), aa))
+        return (r0, r1)
+
+    def frob12(self, a, power):  # fq12.rs:90-97
+        _, _, c12 = _frob_consts()
+        c0 = self.frob6(a[0], power)
+        c1 = self.frob6(a[1], power)
+        k = self.const2(c12[power % 12])
+        return (c0, tuple(self.mul2(x, k) for x in c1))
+
+    def fq4_sqr(self, a, b):
+        t = self
+        t0 = t.sqr2(a)
+        t1 = t.sqr2(b)
+        t2 = t.sqr2(t.add2(a, b))
+        r1 = t.red2(t.sub2(t2, t.add2(t0, t1)))
+        r0 = t.red2(t.add2(t.xi(t1), t0))
+        return r0, r1
+
+    def cyc_sqr(self, f):
+        """Granger-Scott squaring (value of Fq12::square on the cyclotomic subgroup)"""
+        t = self
+        (a0, a1, a2), (b0, b1, b2) = f
+        t0, t1 = t.fq4_sqr(a0, b1)
+        t2, t3 = t.fq4_sqr(b0, a2)
+        t4, t5 = t.fq4_sqr(a1, b2)
+        c00 = t.red2(t.add2(t.dbl2(t.sub2(t0, a0)), t0))
+        c01 = t.red2(t.add2(t.dbl2(t.sub2(t2, a1)), t2))
+        c02 = t.red2(t.add2(t.dbl2(t.sub2(t4, a2)), t4))
+        t5x = t.xi(t5)
+        c10 = t.red2(t.add2(t.dbl2(t.add2(t5x, b0)), t5x))
+        c11 = t.red2(t.add2(t.dbl2(t.add2(t1, b1)), t1))
+        c12 = t.red2(t.add2(t.dbl2(t.add2(t3, b2)), t3))
+        return ((c00, c01, c02), (c10, c11, c12))
+
+    # ---------------- inversion ----------------
+    def inv_fq(self, a, tag):
+        """a^(q-2) (Fermat; the same value as fq.rs:849-902's Euclid for a != 0)"""
+        p = self.p
+        e = Q - 2
+        assert e.bit_length() == 381
+        va, vr = "inv_a_" + tag, "inv_r_" + tag
+        p.var(va)
+        p.var(vr)
+        p.set(va, a)
+        p.set(vr, a)  # top bit (380)
+        # bits 379..0 in words: [379..320] then five 64-bit words
+        spans = [(320, 60)] + [(64 * w, 64) for w in range(4, -1, -1)]
+        for lo, nbits in spans:
+            mask = (e >> lo) & ((1 << nbits) - 1)
+            with p.loop(nbits) as L:
+                p.set(vr, p.sqr(p.get(vr)))
+                with p.if_bit(mask, L):
+                    p.set(vr, p.mul(p.get(vr), p.get(va)))
+        return p.get(vr)
+
+    def inv2(self, a, tag):  # fq2.rs:138-155
+        p = self.p
+        t = self.inv_fq(p.sop(a[0], a[0], a[1], a[1]), tag)
+        return (p.mul(a[0], t), p.mul(p.neg(a[1]), t))
+
+    def inv6(self, a, tag):  # fq6.rs:250-301
+        t = self
+        c0 = t.red2(t.sub2(t.sqr2(a[0]), t.mul2(t.xi(a[2]), a[1])))
+        c1 = t.red2(t.sub2(t.red2(t.xi(t.sqr2(a[2]))), t.mul2(a[0], a[1])))
+        c2 = t.red2(t.sub2(t.sqr2(a[1]), t.mul2(a[0], a[2])))
+        s = t.red2(t.add2(t.xi(t.add2(t.mul2(a[2], c1), t.mul2(a[1], c2))), t.mul2(a[0], c0)))
+        i = t.inv2(s, tag)
+        return (t.mul2(i, c0), t.mul2(i, c1), t.mul2(i, c2))
+
+    def inv12(self, a, tag="f"):  # fq12.rs:132-148
+        t = self
+        s = t.red6(t.sub6(t.mul6(a[0], a[0]), t.mul_v(t.mul6(a[1], a[1]))))
+        i = t.inv6(s, tag)
+        return (t.mul6(a[0], i), t.red6(t.neg6(t.mul6(a[1], i))))
+
+
+# ======================= variables of tower values =======================
+def names12(prefix):
+    return ["%s%d" % (prefix, i) for i in range(12)]
+
+
+def flat12(f):
+    return [x for c6 in f for c2 in c6 for x in c2]
+
+
+def unflat12(xs):
+    xs = list(xs)
+    return (((xs[0], xs[1]), (xs[2], xs[3]), (xs[4], xs[5])),
+            ((xs[6], xs[7]), (xs[8], xs[9]), (xs[10], xs[11])))
+
+
+def declare12(p, prefix, home=None):
+    """home: preferred storage tier of the 12 variables ("A", "L" or "M")"""
+    for n in names12(prefix):
+        p.var(n, 1, home)
+
+
+def set12(p, prefix, f):
+    for n, v in zip(names12(prefix), flat12(f)):
+        p.set(n, v)
+
+
+def get12(p, prefix):
+    return unflat12(p.get(n) for n in names12(prefix))

@@ -25,7 +25,7 @@ def kernels(paths):
     for name, v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
         m = meta[name]
         out.append("| %s | %d | %.1f | %.1f | %.1f | %.1f%% | %s | %s | %s | %s | %s | %s |" % (
-            name.split("(")[0], len(v), sum(v) / len(v) / 1e3, min(v) / 1e3, max(v) / 1e3,
+            name.replace("(anonymous namespace)::", "").split("(")[0], len(v), sum(v) / len(v) / 1e3, min(v) / 1e3, max(v) / 1e3,
             100.0 * sum(v) / total if total else 0, m[0], m[1], m[2], m[3], m[4], m[5]))
     return "\n".join(out)
 
@@ -51,7 +51,7 @@ def pmc(path, counter):
         acc.setdefault(name, []).append(float(val))
     out = ["| kernel | dispatches | %s mean/dispatch |" % counter, "|---|---|---|"]
     for name, v in sorted(acc.items()):
-        out.append("| %s | %d | %.1f |" % (str(name).split("(")[0], len(v), sum(v) / len(v)))
+        out.append("| %s | %d | %.1f |" % (str(name).replace("(anonymous namespace)::", "").split("(")[0], len(v), sum(v) / len(v)))
     return "\n".join(out)
 
 
