@@ -31,6 +31,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# v_mad_u64_u32 issue ceiling, measured (profiles/r01_clock_probe.txt): 5.13
+# shader clocks per wave-instruction per SIMD at a sustained 2.39 GHz,
+# 1024 SIMDs x 64 lanes -> limb multiply-accumulates per second
+VALU_MAC_PEAK_T = 1024 * 64 / 5.13 * 2.39e9 / 1e12
 FQ12_BYTES = 576
 G1A_BYTES, G2A_BYTES = 104, 200  # ABI records (coordinates + infinity flag + pad)
 # algorithmic HBM bytes per pairing, per kernel (DESIGN.md "Roofline")
@@ -240,7 +244,7 @@ def main():
             value = ws * n * args.steps / elapsed
             metric, unit = "BLS12-381 pairings/sec at batch 2^16", "pairings/s"
             config = {"workload": "bls12_381 e(P_i,Q_i) batch (fused G2 prepare + Miller loop + final exp)",
-                      "kernel_variant": ["lazy28", "word32", "word32x2", "gen"][int(os.environ.get("PA_PAIRING_KERNEL", "0"))],
+                      "kernel_variant": ["lazy28", "word32", "word32x2", "gen", "gen2"][int(os.environ.get("PA_PAIRING_KERNEL", "3"))],
                       "batch_per_gpu": n, "global_batch": n * ws, "parallelism": "shard%d+rccl_gather" % ws
                       if ws > 1 else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}
@@ -268,6 +272,21 @@ def main():
         roof = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "bytes_per_unit": dom_bytes, "avg_launch_ms": round(dom_ms, 4)}
+        work_path = os.path.join(ROOT, "pairing_amd", "lib", "pa_gen_work.json")
+        if args.workload == "pairing" and os.path.exists(work_path):
+            # the pairing kernels are VALU-issue bound (multiply-accumulate
+            # chains), not HBM bound: report that roofline, with the HBM view
+            # kept alongside
+            with open(work_path) as f:
+                work = json.load(f)
+            macs = work["final_exp" if dom_name == "final_exponentiation" else "miller_loop"]["limb_macs"]
+            mac_rate = macs * n / (dom_ms * 1e-3) / 1e12
+            roof = {"kernel": dom_name, "bound": "valu", "achieved": round(mac_rate, 3),
+                    "peak": round(VALU_MAC_PEAK_T, 3), "unit": "T limb-MAC/s (28x28-bit v_mad_u64_u32)",
+                    "frac": mac_rate / VALU_MAC_PEAK_T, "traffic": traffic, "macs_per_unit": macs,
+                    "avg_launch_ms": round(dom_ms, 4),
+                    "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS,
+                            "bytes_per_unit": dom_bytes}}
         cpu = None
         if not args.no_cpu_baseline and ws == 1:
             if args.workload == "pairing":

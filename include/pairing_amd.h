@@ -78,11 +78,12 @@ int pa_set_device(int device);
 int pa_synchronize(void);
 /* Tuning knob: which kernel family runs the Miller loop / final
  * exponentiation (identical results):
- *   0 = lazy 28-bit-limb core, one pairing per lane (default)
+ *   0 = lazy 28-bit-limb core, one pairing per lane
  *   1 = 32-bit-word core, one pairing per lane
  *   2 = 32-bit-word core, two lanes per pairing
  *   3 = generated kernels (tools/pgen: own register allocation, code objects
- *       lib/pa_gen_*.hsaco loaded at first use)
+ *       lib/pa_gen_*.hsaco loaded at first use), one lane per pairing (default)
+ *   4 = generated kernels, a lane pair per pairing (two waves per SIMD)
  * Not part of the reference interface; for A/B measurement. */
 int pa_set_pairing_kernel(int variant);
 

@@ -105,8 +105,9 @@ def device_count():
 
 
 def set_pairing_kernel(variant):
-    """Pairing kernel family: 0 lazy 28-bit core (default), 1 32-bit one lane,
-    2 32-bit two lanes per pairing, 3 generated (tools/pgen).  Identical results."""
+    """Pairing kernel family: 0 lazy 28-bit core, 1 32-bit one lane, 2 32-bit
+    two lanes per pairing, 3 generated (tools/pgen, default), 4 generated on
+    lane pairs.  Identical results."""
     call("pa_set_pairing_kernel", int(variant))
 
 

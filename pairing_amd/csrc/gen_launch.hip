@@ -19,8 +19,8 @@ namespace {
 struct GenDevice {
     bool loaded = false;
     hipError_t err = hipSuccess;
-    hipModule_t mod[2] = {nullptr, nullptr};
-    hipFunction_t fn[2] = {nullptr, nullptr};
+    hipModule_t mod[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipFunction_t fn[4] = {nullptr, nullptr, nullptr, nullptr};
     void* ws = nullptr;
     size_t ws_bytes = 0;
 };
@@ -28,9 +28,13 @@ struct GenDevice {
 std::mutex g_mu;
 GenDevice g_dev[64];
 
-const char* const kFile[2] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco"};
-const char* const kName[2] = {"pa_gen_miller_loop", "pa_gen_final_exp"};
-const size_t kWaveBytes[2] = {PA_GEN_MILLER_LOOP_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_MEM_SLOTS * 3584ull};
+// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing
+const char* const kFile[4] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco", "pa_gen_miller_loop2.hsaco",
+                              "pa_gen_final_exp2.hsaco"};
+const char* const kName[4] = {"pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2", "pa_gen_final_exp2"};
+const size_t kWaveBytes[4] = {PA_GEN_MILLER_LOOP_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_MEM_SLOTS * 3584ull,
+                              PA_GEN_MILLER_LOOP2_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP2_MEM_SLOTS * 3584ull};
+const int kLanes[4] = {1, 1, 2, 2};
 
 std::string lib_dir() {
     Dl_info info;
@@ -46,7 +50,7 @@ hipError_t load(GenDevice& d) {
     if (d.loaded) return d.err;
     d.loaded = true;
     const std::string dir = lib_dir();
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < 4; k++) {
         const std::string path = dir + "/" + kFile[k];
         if ((d.err = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess) return d.err;
         if ((d.err = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) return d.err;
@@ -63,8 +67,10 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
     std::lock_guard<std::mutex> lock(g_mu);
     GenDevice& d = g_dev[dev];
     if ((e = load(d)) != hipSuccess) return e;
-    const size_t blocks = (n + 63) / 64;
-    const size_t need = blocks * (kWaveBytes[0] > kWaveBytes[1] ? kWaveBytes[0] : kWaveBytes[1]);
+    const size_t blocks = (n * kLanes[which] + 63) / 64;
+    size_t wave_bytes = 0;
+    for (int k = 0; k < 4; k++) wave_bytes = kWaveBytes[k] > wave_bytes ? kWaveBytes[k] : wave_bytes;
+    const size_t need = blocks * wave_bytes;
     if (need > d.ws_bytes) {
         if (d.ws) (void)hipFree(d.ws);
         d.ws = nullptr;
@@ -93,6 +99,13 @@ hipError_t launch_miller_loop_gen(const uint64_t* p_aff, const uint64_t* q_aff, 
 }
 hipError_t launch_final_exp_gen(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream) {
     return launch(1, in, out, ok, n, stream);
+}
+hipError_t launch_miller_loop_gen2(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+                                   hipStream_t stream) {
+    return launch(2, p_aff, q_aff, out, n, stream);
+}
+hipError_t launch_final_exp_gen2(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream) {
+    return launch(3, in, out, ok, n, stream);
 }
 
 }  // namespace pa

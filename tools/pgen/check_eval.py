@@ -21,13 +21,13 @@ def words_to_int(ws):
     return sum(int(w) << (64 * i) for i, w in enumerate(ws))
 
 
-def run(n=2, seed=3):
+def run(n=2, seed=3, lanes=1):
     g = rng(seed)
     p = O.g1_mul_generator(random_scalars(g, n))
     q = O.g2_mul_generator(random_scalars(g, n))
     ml_ref = O.miller_loop_batch(p, O.g2_prepare(q))
     fe_ref, _ = O.final_exponentiation(ml_ref)
-    ml, fe = kernels.miller_loop_prog(), kernels.final_exp_prog()
+    ml, fe = kernels.miller_loop_prog(lanes=lanes), kernels.final_exp_prog(lanes=lanes)
     for i in range(n):
         ins = {k: words_to_int(p[i, 6 * k:6 * k + 6]) for k in range(2)}
         ins.update({2 + k: words_to_int(q[i, 6 * k:6 * k + 6]) for k in range(4)})
@@ -48,4 +48,6 @@ def run(n=2, seed=3):
 
 
 if __name__ == "__main__":
-    run()
+    for lanes in (int(a) for a in (sys.argv[1:] or ["1", "2"])):
+        print("lanes =", lanes)
+        run(lanes=lanes)

@@ -90,8 +90,9 @@ class Var:
 
 
 class Prog:
-    def __init__(self, name):
+    def __init__(self, name, lanes=1):
         self.name = name
+        self.lanes = lanes      # 2: a lane pair shares each pairing (tower2.py)
         self.root = Block()
         self.cur = self.root
         self.nval = 0
@@ -136,12 +137,31 @@ class Prog:
 
     def neg(self, b):
         assert b.u in SUBCU, "neg bound %d" % b.u
-        return self._op("neg", [b], SUBCU[b.u], imm=b.u)
+        return self._cse("neg", [b], SUBCU[b.u], imm=b.u)
 
     def red(self, a):
         if a.u == 1:
             return a
-        return self._op("red", [a], 1)
+        return self._cse("red", [a], 1)
+
+    def _cse(self, kind, srcs, u, imm=None):
+        """pure ops on the same operands in the same block are computed once"""
+        memo = self.cur.__dict__.setdefault("memo", {})
+        key = (kind, tuple(v.id for v in srcs), imm)
+        if key not in memo:
+            memo[key] = self._op(kind, srcs, u, imm)
+        return memo[key]
+
+    # ---- lane-pair ops (two-lane programs) ----
+    def swap(self, a):
+        """the partner lane's value (v_mov_b32_dpp quad_perm:[1,0,3,2])"""
+        assert self.lanes == 2
+        return self._cse("swap", [a], a.u)
+
+    def sel(self, a, b):
+        """lane 0 takes a, lane 1 takes b"""
+        assert self.lanes == 2
+        return self._cse("sel", [a, b], max(a.u, b.u))
 
     def const(self, x):
         """field element x (plain integer) as a canonical Fl constant"""
@@ -162,14 +182,19 @@ class Prog:
         self.cur.items.append(Op("setvar", None, [v], imm=name))
 
     # ---- kernel I/O (see kernels.py for the record layouts) ----
-    def load(self, slot):
+    def load(self, slot, slot1=None):
         """input Fq number `slot` of this lane's record (canonical, R = 2^384)
-        -> Fl with R = 2^392 (u = 1): raw limbs times 2^400 mod q"""
-        raw = self._op("load_raw", [], 1, imm=slot)
+        -> Fl with R = 2^392 (u = 1): raw limbs times 2^400 mod q.  Two-lane
+        programs: lane 1 reads `slot1` (default: the same slot)."""
+        imm = slot if slot1 is None else (slot, slot1)
+        raw = self._op("load_raw", [], 1, imm=imm)
         return self.mul(raw, self.const_limbs(gen_fl.limbs(pow(2, 400, Q))))
 
-    def store(self, slot, v):
-        """canonical output Fq `slot` (R = 2^384) of this lane"""
+    def store(self, slot, v, slot1=None):
+        """canonical output Fq `slot` (R = 2^384) of this lane (two-lane
+        programs: lane 1 writes `slot1`)"""
+        if slot1 is not None:
+            slot = (slot, slot1)
         w = self.mul(self.red(v), self.const_limbs(gen_fl.limbs(pow(2, 384, Q))))
         self.cur.items.append(Op("store_raw", None, [w], imm=slot))
 
@@ -274,7 +299,10 @@ def red_limbs(x):
 
 def evaluate(prog, inputs, stats=None, trace=None):
     """inputs: dict slot -> canonical ABI integer (R = 2^384 Montgomery value,
-    i.e. the integer held in the record).  Returns dict slot -> output integer."""
+    i.e. the integer held in the record).  Returns dict slot -> output integer.
+    Two-lane programs (prog.lanes == 2) run both lanes of a pair in lockstep;
+    their load/store slots are (lane 0 slot, lane 1 slot) pairs."""
+    L = prog.lanes
     env = {}
     vars_ = {}
     outs = {}
@@ -293,44 +321,57 @@ def evaluate(prog, inputs, stats=None, trace=None):
             else:
                 step(it)
 
+    def lane_op(k, op, s):
+        if k == "sop":
+            return mont_sop(list(zip(s[0::2], s[1::2])))
+        if k == "sqr":
+            return mont_sop([(s[0], s[0])])
+        if k == "add":
+            return tuple(a + b for a, b in zip(*s))
+        if k == "sub":
+            c = SUBC[op.imm]
+            return tuple(a + ci - b for a, ci, b in zip(s[0], c, s[1]))
+        if k == "neg":
+            c = SUBC[op.imm]
+            return tuple(ci - b for ci, b in zip(c, s[0]))
+        if k == "red":
+            return red_limbs(s[0])
+        raise ValueError(k)
+
     def step(op):
         k = op.kind
-        s = [env[v.id] for v in op.srcs]
+        s = [env[v.id] for v in op.srcs]      # per source: list over lanes
         st.bump(k)
         if k == "sop":
-            r = mont_sop(list(zip(s[0::2], s[1::2])))
-        elif k == "sqr":
-            r = mont_sop([(s[0], s[0])])
-        elif k == "add":
-            r = tuple(a + b for a, b in zip(*s))
-        elif k == "sub":
-            c = SUBC[op.imm]
-            r = tuple(a + ci - b for a, ci, b in zip(s[0], c, s[1]))
-        elif k == "neg":
-            c = SUBC[op.imm]
-            r = tuple(ci - b for ci, b in zip(c, s[0]))
-        elif k == "red":
-            r = red_limbs(s[0])
-        elif k == "const":
-            r = op.imm
+            st.bump("sop%d" % (len(op.srcs) // 2))
+        if k == "const":
+            r = [op.imm] * L
         elif k == "getvar":
             r = vars_[op.imm]
         elif k == "setvar":
             vars_[op.imm] = s[0]
             return
         elif k == "load_raw":
-            r = tuple(gen_fl.limbs(inputs[op.imm]))
+            slots = op.imm if isinstance(op.imm, tuple) else (op.imm,) * L
+            r = [tuple(gen_fl.limbs(inputs[slots[ln]])) for ln in range(L)]
         elif k == "store_raw":
-            v = val_of(s[0])
-            assert v < 2 * Q
-            outs[op.imm] = v % Q
+            slots = op.imm if isinstance(op.imm, tuple) else (op.imm,) * L
+            for ln in range(L):
+                v = val_of(s[0][ln])
+                assert v < 2 * Q
+                outs[slots[ln]] = v % Q
             return
+        elif k == "swap":
+            r = [s[0][1 - ln] for ln in range(L)]
+        elif k == "sel":
+            r = [s[ln][ln] for ln in range(L)]
         else:
-            raise ValueError(k)
-        _check(r, op.dst.u, repr(op))
+            r = [lane_op(k, op, [x[ln] for x in s]) for ln in range(L)]
+        for ln in range(L):
+            _check(r[ln], op.dst.u, repr(op))
         env[op.dst.id] = r
         if trace is not None:
-            trace.append((op.dst.id, r, op))
+            trace.append((op.dst.id, r[0] if L == 1 else tuple(r), op))
 
     run(prog.root)
     return outs

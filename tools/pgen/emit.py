@@ -72,15 +72,23 @@ class ValState:
         self.var = None     # name of the variable whose home holds it (getvar values)
 
 
+S_ODD = 40          # s[40:41] lane mask of the odd lanes (lane pairs: role 1)
+
+# storage configurations: (V slots, A slots, L slots)
+STORAGE = {1: (17, 18, 11),     # one wave per SIMD: 256 VGPR + 256 AGPR, 40 KB LDS
+           2: (11, 6, 5)}       # two waves per SIMD: 172 VGPR + 84 AGPR, 20 KB LDS
+
+
 class Emitter:
     def __init__(self, prog, cfg):
         self.prog = prog
         self.cfg = cfg          # kernel config (kernels.py): loads / stores / flags
         self.code = []
         self.nlabel = 0
-        self.vslot = [None] * NV            # ValState or None
-        self.aslot = [None] * NA            # owner: ("val", vs) | ("var", name) | None
-        self.lslot = [None] * NL_SLOTS
+        self.NV, self.NA, self.NL = STORAGE[prog.lanes]
+        self.vslot = [None] * self.NV       # ValState or None
+        self.aslot = [None] * self.NA       # owner: ("val", vs) | ("var", name) | None
+        self.lslot = [None] * self.NL
         self.mslot = []
         self.home = {}                      # var name -> loc
         self.states = {}                    # val id -> ValState
@@ -115,7 +123,7 @@ class Emitter:
 
     # ---------------- slot bookkeeping ----------------
     def free_vslot(self):
-        for k in range(NV):
+        for k in range(self.NV):
             if self.vslot[k] is None:
                 return k
         return None
@@ -133,7 +141,7 @@ class Emitter:
         # Belady, cost-weighted: a value with a copy elsewhere is dropped for
         # free, so it is preferred unless it is needed much sooner
         best, bk = -1, None
-        for k in range(NV):
+        for k in range(self.NV):
             if k in avoid or k in self.pinned:
                 continue
             vs = self.vslot[k]
@@ -363,6 +371,15 @@ class Emitter:
         for i in range(NL):
             self.i("v_sub_u32", d + i, K(c[i]), b + i)
 
+    def emit_swap(self, a, d):
+        self.i("s_nop", 1)   # VALU write -> DPP read of the same VGPR: 2 wait states
+        for i in range(NL):
+            self.i("v_mov_b32_dpp_swap", d + i, a + i)
+
+    def emit_sel(self, a, b, d):
+        for i in range(NL):
+            self.i("v_cndmask_b32_e64", d + i, a + i, b + i, S(S_ODD))
+
     def emit_const(self, limbs, d):
         for i in range(NL):
             self.i("v_mov_b32", d + i, K(limbs[i]))
@@ -463,7 +480,7 @@ class Emitter:
                     if l == pos and name in self.home:
                         self.free_home(name, pos)
         # everything defined here is dead now
-        for k in range(NV):
+        for k in range(self.NV):
             vs = self.vslot[k]
             if vs is not None and vs.val.id in self.local_ids:
                 self.kill(vs)
@@ -476,7 +493,7 @@ class Emitter:
         """before a construct: values of this block live after it leave the V
         slots (the body needs them all)"""
         ids = self.block_vals(block)
-        for k in range(NV):
+        for k in range(self.NV):
             vs = self.vslot[k]
             if vs is None or vs.val.id not in ids:
                 continue
@@ -555,7 +572,8 @@ class Emitter:
             # in place over a dying source (safe for every op kind below)
             dk = None
             for vs, kk in zip(srcs, sk):
-                if vs in dying and self.vslot[kk] is vs and not (k == "sub" and op.srcs[0].id == op.srcs[1].id):
+                if (vs in dying and self.vslot[kk] is vs and k != "swap"
+                        and not (k == "sub" and op.srcs[0].id == op.srcs[1].id)):
                     dk = kk
                     break
             if dk is None:
@@ -578,6 +596,10 @@ class Emitter:
             self.emit_neg(base[0], d, op.imm)
         elif k == "const":
             self.emit_const(op.imm, d)
+        elif k == "swap":
+            self.emit_swap(base[0], d)
+        elif k == "sel":
+            self.emit_sel(base[0], base[1], d)
         elif k == "load_raw":
             self.cfg.emit_load(self, op.imm, d)
         elif k == "store_raw":

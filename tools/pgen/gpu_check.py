@@ -17,6 +17,7 @@ import numpy as np  # noqa: E402
 import dsl  # noqa: E402
 
 hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+LANES = 1
 P = ctypes.c_void_p
 
 
@@ -43,7 +44,7 @@ def launch(hsaco, kname, args, n, ws_bytes_per_wave, lds_unused=0, reps=3):
     mod, fn = P(), P()
     ck(hip.hipModuleLoad(ctypes.byref(mod), hsaco.encode()), "hipModuleLoad")
     ck(hip.hipModuleGetFunction(ctypes.byref(fn), mod, kname.encode()), "hipModuleGetFunction")
-    nblk = (n + 63) // 64
+    nblk = (n * LANES + 63) // 64
     ws = dev(ws_bytes_per_wave * nblk)
     buf = (ctypes.c_uint64 * 5)(*(list(args[:3]) + [n, ws.value or 0]))
     size = ctypes.c_size_t(ctypes.sizeof(buf))
@@ -73,8 +74,10 @@ def main():
     import importlib
     meta = importlib.import_module("build_gen").PROGRAMS[which]
     prog, cfg, kname, nmem = meta()
+    global LANES
+    LANES = prog.lanes
     rng = random.Random(5)
-    if which in ("small", "fe"):
+    if which in ("small", "fe", "fe2"):
         ins = [[rand_fq(rng) for _ in range(12)] for _ in range(n)]
         ins[1] = [0] * 12  # f == 0 lane
         rec_in = np.array([to_words(r) for r in ins], dtype=np.uint64)
@@ -97,7 +100,7 @@ def main():
             print("lane %d: %s" % (lane, "OK" if good else "MISMATCH"))
         print("time %.3f ms for n=%d" % (dt * 1e3, n))
         sys.exit(1 if bad else 0)
-    if which == "ml":
+    if which in ("ml", "ml2"):
         ins = [[rand_fq(rng) for _ in range(6)] for _ in range(n)]
         prec = np.array([to_words(r[:2]) + [0] for r in ins], dtype=np.uint64)
         qrec = np.array([to_words(r[2:]) + [0] for r in ins], dtype=np.uint64)

@@ -8,8 +8,8 @@ Kernel arguments (5 x 8 bytes, all kernels):
 """
 import gen_fl
 from dsl import Q
-from emit import (A, ACC, ADDR, GID, K, LOFF, ORACC, S, S_ARG, S_EXEC, S_KARG, S_TMP, S_VALID, S_WG, S_WS,
-                  SKQ, SQ, SQINV, NL, MASK, QL, QINV28, KQ)
+from emit import (A, ACC, ADDR, GID, K, LOFF, ORACC, S, S_ARG, S_EXEC, S_KARG, S_ODD, S_TMP, S_VALID, S_WG,
+                  S_WS, SKQ, SQ, SQINV, NL, MASK, QL, QINV28, KQ)
 
 ONE_ABI = (1 << 384) % Q          # Montgomery one in the ABI (R = 2^384)
 S_STRIDE = 32
@@ -20,7 +20,11 @@ def words32(x, n=12):
 
 
 class KernelCfg:
+    """lanes = 1: lane i handles pairing i.  lanes = 2: lanes 2j and 2j+1
+    handle pairing j (role r = lane & 1); a load / store slot pair (s0, s1)
+    means lane r uses slot s_r of pairing j's record."""
     name = None
+    lanes = 1
     args = ()
     records = {}          # input slot -> (arg index, record bytes, byte offset)
     out_arg, out_bytes = 2, 576
@@ -32,6 +36,10 @@ class KernelCfg:
         i(("s_waitcnt_lgkm0",))
         i(("v_lshlrev_b32", LOFF, K(3), 0))
         i(("v_lshl_add_u32", GID, S(S_WG), K(6), 0))   # global lane index
+        if self.lanes == 2:
+            i(("s_lshl_b32", S(S_ARG + 6), S(S_ARG + 6), K(1)))   # 2n active lanes
+            i(("s_mov_b32", S(S_ODD), K(0xAAAAAAAA)))
+            i(("s_mov_b32", S(S_ODD + 1), K(0xAAAAAAAA)))
         i(("v_cmp_gt_u32", S(S_ARG + 6), GID))
         i(("s_and_saveexec_b64", S(S_EXEC)))
         i(("long_cbranch_execz", end_label))
@@ -49,18 +57,31 @@ class KernelCfg:
     def prologue_masks(self, em, code):
         pass
 
-    def lane_addr(self, code, arg, stride):
+    def lane_addr(self, code, arg, stride, delta=0):
+        """v[12:13] = arg + (pairing index) * stride + (lane role) * delta"""
         # global lane index from tid * 8; one SGPR per VALU instruction
         # (constant bus): the base goes through VGPRs
         code.append(("v_lshrrev_b32", GID, K(3), LOFF))
         code.append(("v_lshl_add_u32", GID, S(S_WG), K(6), GID))
+        if self.lanes == 2:
+            code.append(("v_and_b32", 15, K(1), GID))
+            code.append(("v_lshrrev_b32", GID, K(1), GID))
         code.append(("v_mov_b64", ADDR, S(S_ARG + 2 * arg)))
         code.append(("s_mov_b32", S(S_STRIDE), K(stride)))
         code.append(("v_mad_u64_u32", ADDR, GID, S(S_STRIDE), ADDR))
+        if self.lanes == 2 and delta:
+            code.append(("v_mul_u32_u24", 15, K(delta), 15))
+            code.append(("v_mad_u64_u32", ADDR, 15, K(1), ADDR))
+
+    def slot_pair(self, imm):
+        return imm if isinstance(imm, tuple) else (imm, imm)
 
     def emit_load(self, em, slot, d):
-        arg, stride, off = self.records[slot]
-        self.lane_addr(em.code, arg, stride)
+        s0, s1 = self.slot_pair(slot)
+        arg, stride, off = self.records[s0]
+        arg1, stride1, off1 = self.records[s1]
+        assert (arg, stride) == (arg1, stride1)
+        self.lane_addr(em.code, arg, stride, off1 - off)
         for j in range(6):
             em.i("global_load_dwordx2", 2 * j, ADDR, off + 8 * j)
         em.i("s_waitcnt_vm0")
@@ -97,17 +118,21 @@ class KernelCfg:
             if 56 - sh < 32 and li + 2 < NL:
                 em.i("v_lshl_or_b32", j, t + li + 2, K(56 - sh), j)
         # lanes that are not valid get the fixed value
+        s0, s1 = self.slot_pair(slot)
         em.i("s_mov_b64", S(106), S(S_VALID))
         em.i("s_nop", 1)
-        for j, w in enumerate(self.invalid_words(slot)):
-            if -16 <= w <= 64:      # inline constant: no constant-bus slot
-                em.i("v_cndmask_b32", j, K(w), j)
-            else:                   # literal + VCC would need two
-                em.i("v_mov_b32", 15, K(w))
-                em.i("v_cndmask_b32", j, 15, j)
-        self.lane_addr(em.code, self.out_arg, self.out_bytes)
+        for j, (w0, w1) in enumerate(zip(self.invalid_words(s0), self.invalid_words(s1))):
+            if w0 == w1 and -16 <= w0 <= 64:    # inline constant: no constant-bus slot
+                em.i("v_cndmask_b32", j, K(w0), j)
+                continue
+            em.i("v_mov_b32", 15, K(w0))            # literal + VCC would need two
+            if w1 != w0:
+                em.i("v_mov_b32", 14, K(w1))
+                em.i("v_cndmask_b32_e64", 15, 15, 14, S(S_ODD))
+            em.i("v_cndmask_b32", j, 15, j)
+        self.lane_addr(em.code, self.out_arg, self.out_bytes, 48 * (s1 - s0))
         for j in range(6):
-            em.i("global_store_dwordx2", ADDR, 2 * j, 48 * slot + 8 * j)
+            em.i("global_store_dwordx2", ADDR, 2 * j, 48 * s0 + 8 * j)
 
     def invalid_words(self, slot):
         raise NotImplementedError
@@ -150,7 +175,11 @@ class FinalExpCfg(KernelCfg):
     def after_load(self, em, slot):
         for j in range(12):
             em.i("v_or_b32", ORACC, ORACC, j)
-        if slot == 11:
+        if self.slot_pair(slot)[1] == 11:
+            if self.lanes == 2:   # the pair's two halves of the record
+                em.i("s_nop", 1)
+                em.i("v_mov_b32_dpp_swap", 14, ORACC)
+                em.i("v_or_b32", ORACC, ORACC, 14)
             em.i("v_cmp_ne_u32", K(0), ORACC)
             em.i("s_nop", 1)
             em.i("s_mov_b64", S(S_VALID), S(106))
@@ -171,6 +200,16 @@ class FinalExpCfg(KernelCfg):
         code.append(("label", skip))
 
 
+class MillerLoopCfg2(MillerLoopCfg):
+    name = "pa_gen_miller_loop2"
+    lanes = 2
+
+
+class FinalExpCfg2(FinalExpCfg):
+    name = "pa_gen_final_exp2"
+    lanes = 2
+
+
 def build(prog, cfg, debug=False):
     """allocate + emit: returns (code list, emitter)"""
     from emit import Emitter
@@ -186,5 +225,5 @@ def build(prog, cfg, debug=False):
     code.append(("label", end))
     code.append(("s_endpgm",))
     em.code = code
-    em.lds_bytes = max(1, sum(1 for _ in range(len(em.lslot)))) * gen_fl.NL * 4 * 64
+    em.lds_bytes = len(em.lslot) * gen_fl.NL * 4 * 64
     return code, em

@@ -11,18 +11,9 @@ lane selects done by the emitted prologue/epilogue, outside the DSL.
 """
 from dsl import Prog
 from tower import Tower, X_ABS, declare12, get12, set12
+from tower2 import Tower2
 
 ML_MASK = (X_ABS >> 1) & ((1 << 62) - 1)  # bits 61..0 below the leading one of |x| >> 1
-
-
-def _getR(p):
-    return tuple((p.get(n + "0"), p.get(n + "1")) for n in ("rx", "ry", "rz"))
-
-
-def _setR(p, r):
-    for n, v in zip(("rx", "ry", "rz"), r):
-        p.set(n + "0", v[0])
-        p.set(n + "1", v[1])
 
 
 def doubling_step(T, r):
@@ -77,67 +68,120 @@ def ell(T, f, c, px, py):
 
 ML_HOMES = {"px": "L", "py": "L", "qx0": "M", "qx1": "M", "qy0": "M", "qy1": "M",
             "rx0": "A", "rx1": "A", "ry0": "A", "ry1": "A", "rz0": "A", "rz1": "A", "f": "A"}
+# the Fq12 variable names f<i>_<c> carry the home of "f"
 
 
-def miller_loop_prog(homes=None):
+def miller_loop_prog(homes=None, lanes=1):
     homes = dict(ML_HOMES, **(homes or {}))
-    p = Prog("miller_loop")
-    T = Tower(p)
-    pq = ("px", "py", "qx0", "qx1", "qy0", "qy1")
-    for i, n in enumerate(pq):
+    p = Prog("miller_loop" if lanes == 1 else "miller_loop2", lanes)
+    T = Tower(p) if lanes == 1 else Tower2(p)
+    V = _Vars(p, lanes)
+    for n in ("px", "py"):
         p.var(n, 1, homes.get(n))
-        p.set(n, p.load(i))
-    for n in ("rx0", "rx1", "ry0", "ry1", "rz0", "rz1"):
+    p.set("px", p.load(0))
+    p.set("py", p.load(1))
+    for n in ("qx0", "qx1", "qy0", "qy1", "rx0", "rx1", "ry0", "ry1", "rz0", "rz1"):
         p.var(n, 1, homes.get(n))
-    declare12(p, "f", homes.get("f"))
-    one, zero = p.const(1), p.const(0)
-    _setR(p, ((p.get("qx0"), p.get("qx1")), (p.get("qy0"), p.get("qy1")), (one, zero)))
-    set12(p, "f", ((T.one2(), (zero, zero), (zero, zero)), ((zero, zero),) * 3))
+    V.set2("qx", (p.load(2), p.load(3)) if lanes == 1 else p.load(2, 3))
+    V.set2("qy", (p.load(4), p.load(5)) if lanes == 1 else p.load(4, 5))
+    V.declare12("f", homes.get("f"))
+    zero = T.const2((0, 0))
+    V.set2("rx", V.get2("qx"))
+    V.set2("ry", V.get2("qy"))
+    V.set2("rz", T.one2())
+    V.set12("f", ((T.one2(), zero, zero), (zero, zero, zero)))
 
     def line(step):
-        f = get12(p, "f")
-        r = _getR(p)
+        r = tuple(V.get2(n) for n in ("rx", "ry", "rz"))
         if step == "dbl":
             c, r = doubling_step(T, r)
         else:
-            c, r = addition_step(T, r, (p.get("qx0"), p.get("qx1")), (p.get("qy0"), p.get("qy1")))
-        f = ell(T, f, c, p.get("px"), p.get("py"))
-        set12(p, "f", f)
-        _setR(p, r)
+            c, r = addition_step(T, r, V.get2("qx"), V.get2("qy"))
+        for n, v in zip(("rx", "ry", "rz"), r):
+            V.set2(n, v)
+        V.set12("f", ell(T, V.get12("f"), c, p.get("px"), p.get("py")))
 
     with p.loop(62) as L:
         line("dbl")
         with p.if_bit(ML_MASK, L):
             line("add")
-        set12(p, "f", T.sqr12(get12(p, "f")))
+        V.set12("f", T.sqr12(V.get12("f")))
     line("dbl")
-    f = T.conj12(get12(p, "f"))
-    for i, x in enumerate(v for c6 in f for c2 in c6 for v in c2):
-        p.store(i, x)
+    V.store12(T.conj12(V.get12("f")))
     return p
 
 
-def exp_by_x(p, T, f, x, tag):
+class _Vars:
+    """Fq2 / Fq12 state variables: a one-lane Fq2 is two variables (c0, c1),
+    a distributed Fq2 one variable per lane (named <n>0; <n>1 unused)."""
+
+    def __init__(self, p, lanes):
+        self.p, self.lanes = p, lanes
+
+    def get2(self, n):
+        p = self.p
+        return (p.get(n + "0"), p.get(n + "1")) if self.lanes == 1 else p.get(n + "0")
+
+    def set2(self, n, v):
+        p = self.p
+        if self.lanes == 1:
+            p.set(n + "0", v[0])
+            p.set(n + "1", v[1])
+        else:
+            p.set(n + "0", v)
+
+    def declare12(self, prefix, home=None):
+        for i in range(6):
+            for c in (0, 1):
+                self.p.var("%s%d_%d" % (prefix, i, c), 1, home)
+
+    def get12(self, prefix):
+        xs = [self.get2("%s%d_" % (prefix, i)) for i in range(6)]
+        return ((xs[0], xs[1], xs[2]), (xs[3], xs[4], xs[5]))
+
+    def set12(self, prefix, f):
+        for i, v in enumerate([x for c6 in f for x in c6]):
+            self.set2("%s%d_" % (prefix, i), v)
+
+    def store12(self, f):
+        """ABI order: coordinate (2i + c) of Fq2 number i"""
+        for i, v in enumerate([x for c6 in f for x in c6]):
+            if self.lanes == 1:
+                self.p.store(2 * i, v[0])
+                self.p.store(2 * i + 1, v[1])
+            else:
+                self.p.store(2 * i, v, 2 * i + 1)
+
+    def load12(self):
+        p = self.p
+        if self.lanes == 1:
+            xs = [(p.load(2 * i), p.load(2 * i + 1)) for i in range(6)]
+        else:
+            xs = [p.load(2 * i, 2 * i + 1) for i in range(6)]
+        return ((xs[0], xs[1], xs[2]), (xs[3], xs[4], xs[5]))
+
+
+def exp_by_x(p, T, V, f, x, tag):
     """exp_by_x (mod.rs:116-121): f^|x| by square-and-multiply (lib.rs:306-324)
     with cyclotomic squarings, then conjugation (x < 0)"""
     base, res = "eb%s_" % tag, "er%s_" % tag
-    declare12(p, base, "M")
-    declare12(p, res, "A")
-    set12(p, base, f)
-    set12(p, res, f)
+    V.declare12(base, "M")
+    V.declare12(res, "A")
+    V.set12(base, f)
+    V.set12(res, f)
     top = x.bit_length() - 1
     with p.loop(top) as L:
-        set12(p, res, T.cyc_sqr(get12(p, res)))
+        V.set12(res, T.cyc_sqr(V.get12(res)))
         with p.if_bit(x & ((1 << top) - 1), L):
-            set12(p, res, T.mul12(get12(p, res), get12(p, base)))
-    return T.conj12(get12(p, res))
+            V.set12(res, T.mul12(V.get12(res), V.get12(base)))
+    return T.conj12(V.get12(res))
 
 
-def final_exp_prog():
-    p = Prog("final_exp")
-    T = Tower(p)
-    f = (((p.load(0), p.load(1)), (p.load(2), p.load(3)), (p.load(4), p.load(5))),
-         ((p.load(6), p.load(7)), (p.load(8), p.load(9)), (p.load(10), p.load(11))))
+def final_exp_prog(lanes=1):
+    p = Prog("final_exp" if lanes == 1 else "final_exp2", lanes)
+    T = Tower(p) if lanes == 1 else Tower2(p)
+    V = _Vars(p, lanes)
+    f = V.load12()
     # mod.rs:104-160
     f1 = T.conj12(f)
     f2 = T.inv12(f)
@@ -146,26 +190,25 @@ def final_exp_prog():
     r = T.mul12(T.frob12(r, 2), f2)
     x = X_ABS
     y0 = T.cyc_sqr(r)
-    y1 = exp_by_x(p, T, y0, x, "a")
-    y2 = exp_by_x(p, T, y1, x >> 1, "b")
+    y1 = exp_by_x(p, T, V, y0, x, "a")
+    y2 = exp_by_x(p, T, V, y1, x >> 1, "b")
     y3 = T.conj12(r)
     y1 = T.mul12(y1, y3)
     y1 = T.conj12(y1)
     y1 = T.mul12(y1, y2)
-    y2 = exp_by_x(p, T, y1, x, "c")
-    y3 = exp_by_x(p, T, y2, x, "d")
+    y2 = exp_by_x(p, T, V, y1, x, "c")
+    y3 = exp_by_x(p, T, V, y2, x, "d")
     y1 = T.conj12(y1)
     y3 = T.mul12(y3, y1)
     y1 = T.conj12(y1)
     y1 = T.frob12(y1, 3)
     y2 = T.frob12(y2, 2)
     y1 = T.mul12(y1, y2)
-    y2 = exp_by_x(p, T, y3, x, "e")
+    y2 = exp_by_x(p, T, V, y3, x, "e")
     y2 = T.mul12(y2, y0)
     y2 = T.mul12(y2, r)
     y1 = T.mul12(y1, y2)
     y2 = T.frob12(y3, 1)
     y1 = T.mul12(y1, y2)
-    for i, v in enumerate(v for c6 in y1 for c2 in c6 for v in c2):
-        p.store(i, v)
+    V.store12(y1)
     return p

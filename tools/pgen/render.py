@@ -84,6 +84,10 @@ class Renderer:
             return ["%s vcc, %s, %s" % (m, o[0], o[1])]
         if m == "v_cndmask_b32":
             return ["v_cndmask_b32 %s, %s, %s, vcc" % (o[0], o[1], o[2])]
+        if m == "v_cndmask_b32_e64":
+            return ["v_cndmask_b32_e64 %s, %s, %s, %s" % (o[0], o[1], o[2], reg(a[3], True))]
+        if m == "v_mov_b32_dpp_swap":
+            return ["v_mov_b32_dpp %s, %s quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" % (o[0], o[1])]
         if m == "ds_write_b64":
             return ["ds_write_b64 %s, %s offset:%d" % (o[0], o[1], a[2])]
         if m == "ds_read_b64":
@@ -119,7 +123,7 @@ class Renderer:
         return out
 
 
-def kernel_asm(name, code, lds_bytes, nargs=5):
+def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256):
     body = Renderer(code).text()
     args = "\n".join(
         "      - .offset: %d\n        .size: 8\n        .value_kind: %s%s" % (
@@ -166,14 +170,15 @@ amdhsa.kernels:
     .private_segment_fixed_size: 0
     .wavefront_size: 64
     .sgpr_count: 102
-    .vgpr_count: 512
-    .agpr_count: 256
+    .vgpr_count: {nfree}
+    .agpr_count: {nagpr}
     .max_flat_workgroup_size: 64
     .args:
 {args}
 ...
 \t.end_amdgpu_metadata
-""".format(name=name, body="\n".join(body), lds=lds_bytes, kb=8 * nargs, args=args)
+""".format(name=name, body="\n".join(body), lds=lds_bytes, kb=8 * nargs, args=args,
+           nfree=512 if lanes == 1 else 256, aoff=nvgpr, nagpr=(512 if lanes == 1 else 256) - nvgpr)
 
 
 def assemble(asm_text, out_hsaco, workdir):

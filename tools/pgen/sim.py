@@ -20,10 +20,16 @@ def sx64(x):
 
 
 class Sim:
-    def __init__(self, code, lane=0):
+    """lanes: the simulated lanes (one, or the two lanes of a pair); VALU /
+    memory instructions run per lane, SALU once, DPP reads the partner."""
+
+    def __init__(self, code, lane=0, lanes=None):
         self.code = code
-        self.v = [0] * 256
-        self.a = [0] * 256
+        self.lanes = lanes or [lane]
+        self.vf = {ln: [0] * 256 for ln in self.lanes}
+        self.af = {ln: [0] * 256 for ln in self.lanes}
+        self.v = self.vf[self.lanes[0]]
+        self.a = self.af[self.lanes[0]]
         self.s = [0] * 108
         self.scc = 0
         self.mem = {}       # dword address -> u32
@@ -69,6 +75,10 @@ class Sim:
         m = (m & ~(1 << b)) | (int(bool(bit)) << b)
         self.s[106], self.s[107] = m & M32, m >> 32
 
+    def vcc_of(self, ln):
+        m = self.s[106] | (self.s[107] << 32)
+        return (m >> (ln % 64)) & 1
+
     def vcc(self):
         m = self.s[106] | (self.s[107] << 32)
         return (m >> (self.lane % 64)) & 1
@@ -89,7 +99,19 @@ class Sim:
             self.count += 1
             if self.count > max_steps:
                 raise RuntimeError("step limit")
-            nxt = self.step(t)
+            m = t[0]
+            if m.startswith("v_") or m.startswith("ds_") or m.startswith("global_") or m == "mark":
+                if m == "v_mov_b32_dpp_swap":
+                    src = {ln: self.vf[ln][t[2]] for ln in self.lanes}
+                    for ln in self.lanes:
+                        self.vf[ln][t[1]] = src[ln ^ 1] if (ln ^ 1) in src else 0
+                    nxt = None
+                else:
+                    for ln in self.lanes:
+                        self.lane, self.v, self.a = ln, self.vf[ln], self.af[ln]
+                        nxt = self.step(t)
+            else:
+                nxt = self.step(t)
             if nxt == "end":
                 return
             pc = self.labels[nxt] if nxt is not None else pc + 1
@@ -140,6 +162,11 @@ class Sim:
             wr(a[0], (msk & rd(a[2])) | (~msk & rd(a[3])))
         elif m == "v_cndmask_b32":
             wr(a[0], rd(a[2]) if self.vcc() else rd(a[1]))
+        elif m == "v_cndmask_b32_e64":
+            msk = rd64(a[3])
+            wr(a[0], rd(a[2]) if (msk >> (self.lane % 64)) & 1 else rd(a[1]))
+        elif m == "v_mul_u32_u24":
+            wr(a[0], (rd(a[1]) & 0xffffff) * (rd(a[2]) & 0xffffff))
         elif m == "v_mov_b32" or m == "v_accvgpr_write_b32" or m == "v_accvgpr_read_b32":
             wr(a[0], rd(a[1]))
         elif m == "v_mov_b64":
@@ -210,17 +237,24 @@ class Sim:
             self.scc = (rd64(a[0]) >> (rd(a[1]) & 63)) & 1
         elif m == "s_mul_i32":
             wr(a[0], rd(a[1]) * rd(a[2]))
+        elif m == "s_lshl_b32":
+            wr(a[0], rd(a[1]) << (rd(a[2]) & 31))
         elif m == "s_mul_hi_u32":
             wr(a[0], (rd(a[1]) * rd(a[2])) >> 32)
         elif m == "s_and_saveexec_b64":
-            if not self.vcc():
+            if not all(self.vcc_of(ln) for ln in self.lanes):
                 return "end"
         elif m == "mark":
             if self.trace is not None:
-                while True:
-                    vid, limbs, op = next(self.trace)
-                    if vid == a[0]:
-                        break
+                if self.lane == self.lanes[0]:
+                    while True:
+                        vid, limbs, op = next(self.trace)
+                        if vid == a[0]:
+                            break
+                    self.cur_mark = (limbs, op)
+                limbs, op = self.cur_mark
+                if len(self.lanes) == 2:
+                    limbs = limbs[self.lanes.index(self.lane)]
                 got = tuple(self.v[a[1] + i] for i in range(14))
                 if got != tuple(limbs):
                     raise AssertionError("first divergence at %r (instr %d): got %s want %s" % (
@@ -240,9 +274,10 @@ class Sim:
         return None
 
 
-def run_lane(code, args, buffers, lane=0, max_steps=10 ** 9, trace=None):
-    """args: 5 u64 kernel arguments; buffers: {base_address: list of u64}"""
-    sm = Sim(code, lane)
+def run_lane(code, args, buffers, lane=0, max_steps=10 ** 9, trace=None, pair=False):
+    """args: 5 u64 kernel arguments; buffers: {base_address: list of u64};
+    pair: simulate lanes (lane & ~1, lane | 1) together"""
+    sm = Sim(code, lane, [lane & ~1, lane | 1] if pair else None)
     sm.trace = iter(trace) if trace is not None else None
     for base, words in buffers.items():
         for i, w in enumerate(words):
@@ -254,6 +289,7 @@ def run_lane(code, args, buffers, lane=0, max_steps=10 ** 9, trace=None):
         sm.mem[karg + 8 * i + 4] = x >> 32
     sm.s[0], sm.s[1] = karg, 0
     sm.s[2] = lane // 64
-    sm.v[0] = lane % 64
+    for ln in sm.lanes:
+        sm.vf[ln][0] = ln % 64
     sm.run(max_steps)
     return sm

@@ -30,7 +30,12 @@ def check(which, seed=5, lane=3, debug=True):
     trace = []
     rng = random.Random(seed)
     IN, OUT, AUX, WS = 0x100000, 0x200000, 0x300000, 0x400000
-    if which in ("small", "fe"):
+    pair = prog.lanes == 2
+    if pair:   # lanes 2*lane, 2*lane+1 handle pairing `lane`
+        sim_lane = 2 * lane
+    else:
+        sim_lane = lane
+    if which in ("small", "fe", "fe2"):
         ins = [rng.randrange(dsl.Q) for _ in range(12)]
         rec = [0] * (72 * lane) + words(ins)
         want = dsl.evaluate(prog, {k: ins[k] for k in range(12)}, trace=trace)
@@ -45,7 +50,7 @@ def check(which, seed=5, lane=3, debug=True):
         args = [IN, AUX, OUT, lane + 1, WS]
         bufs = {IN: prec, AUX: qrec}
     t = time.time()
-    sm = sim.run_lane(code, args, bufs, lane=lane, trace=trace if debug else None)
+    sm = sim.run_lane(code, args, bufs, lane=sim_lane, trace=trace if debug else None, pair=pair)
     got = []
     for k in range(12):
         base = OUT + 576 * lane + 48 * k

@@ -1,0 +1,75 @@
+"""The tower on a lane pair: lane r holds coordinate r of every Fq2 value
+(a "distributed" Fq2 is one DSL Val); Fq values outside Fq2 (P's
+coordinates, the norm inverted in Fq2 inversion) are replicated on both
+lanes.  Fq6 / Fq12 code is inherited unchanged from tower.Tower -- only the
+Fq2 primitives are redefined here, each as per-lane operations plus the
+partner exchange (swap: DPP quad_perm [1,0,3,2]) and lane selects.
+
+Products: lane 0 computes c0 = a0 b0 - a1 b1, lane 1 c1 = a0 b1 + a1 b0,
+both as the same two-term leaf sop(X, b, Z, b'), with b' = swap(b) and
+X = (a0 | a0), Z = (-a1 | a1) formed by selects.  Every field value equals
+the one-lane tower's (checked by dsl.evaluate against the C oracle).
+"""
+from dsl import SUBCU
+from tower import Tower
+
+
+class Tower2(Tower):
+    # ---------------- distributed Fq2 ----------------
+    def add2(self, a, b): return self.p.add(a, b)
+    def sub2(self, a, b): return self.p.sub(a, b)
+    def neg2(self, a): return self.p.neg(a)
+    def dbl2(self, a): return self.p.add(a, a)
+    def red2(self, a): return self.p.red(a)
+    def u2(self, a): return a.u
+
+    def xi(self, a):
+        """(a0 - a1, a0 + a1): mine + (lane 0 ? -other : other)"""
+        p = self.p
+        o = p.swap(a)
+        return p.add(a, p.sel(p.neg(o), o))
+
+    def conj2(self, a):
+        p = self.p
+        return p.sel(a, p.neg(a))
+
+    def mul2(self, a, b):
+        p = self.p
+        if SUBCU[a.u] * b.u > a.u * SUBCU[b.u]:
+            a, b = b, a
+        oa, ob = p.swap(a), p.swap(b)
+        x = p.sel(a, oa)              # a0 on both lanes
+        z = p.sel(p.neg(oa), a)       # -a1 | a1
+        return p.sop(x, b, z, ob)     # lane 0: a0 b0 - a1 b1; lane 1: a0 b1 + a1 b0
+
+    def sqr2(self, a):
+        """lane 0: (a0 + a1)(a0 - a1); lane 1: 2 a0 a1"""
+        p = self.p
+        if a.u > 1:
+            a = p.red(a)
+        o = p.swap(a)
+        x = p.add(o, p.sel(a, o))     # a0 + a1 | 2 a0
+        y = p.sel(p.sub(a, o), a)     # a0 - a1 | a1
+        return p.mul(x, y)
+
+    def mul_fq(self, a, b):
+        return self.p.mul(a, b)       # b replicated
+
+    def lim2(self, a):
+        return a if a.u <= 2 else self.p.red(a)
+
+    def const2(self, c):
+        p = self.p
+        return p.sel(p.const(c[0]), p.const(c[1]))
+
+    def one2(self):
+        return self.const2((1, 0))
+
+    # ---------------- inversion ----------------
+    def inv2(self, a, tag):
+        """fq2.rs:138-155: the norm a0^2 + a1^2 is formed on both lanes and
+        inverted redundantly (replicated Fq)"""
+        p = self.p
+        sq = p.mul(a, a)
+        t = self.inv_fq(p.red(p.add(sq, p.swap(sq))), tag)
+        return p.mul(self.conj2(a), t)
