@@ -158,17 +158,29 @@ __global__ void __launch_bounds__(64) k64(uint32_t* out, int iters) {
   if (iters < 0) out[threadIdx.x] = 1;
 }
 int main() {
-  uint32_t* d; hipMalloc(&d, 4096); hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1); float ms;
-  k1<<<1024, 64>>>(d, 512); hipEventRecord(e0); k1<<<1024, 64>>>(d, 512); hipEventRecord(e1); hipEventSynchronize(e1);
-  hipEventElapsedTime(&ms, e0, e1); printf("K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per wave\n", 1, 1 * 3.8, ms, ms * 1e6 / 512);
-  k4<<<1024, 64>>>(d, 128); hipEventRecord(e0); k4<<<1024, 64>>>(d, 128); hipEventRecord(e1); hipEventSynchronize(e1);
-  hipEventElapsedTime(&ms, e0, e1); printf("K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per wave\n", 4, 4 * 3.8, ms, ms * 1e6 / 512);
-  k8<<<1024, 64>>>(d, 64); hipEventRecord(e0); k8<<<1024, 64>>>(d, 64); hipEventRecord(e1); hipEventSynchronize(e1);
-  hipEventElapsedTime(&ms, e0, e1); printf("K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per wave\n", 8, 8 * 3.8, ms, ms * 1e6 / 512);
-  k16<<<1024, 64>>>(d, 32); hipEventRecord(e0); k16<<<1024, 64>>>(d, 32); hipEventRecord(e1); hipEventSynchronize(e1);
-  hipEventElapsedTime(&ms, e0, e1); printf("K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per wave\n", 16, 16 * 3.8, ms, ms * 1e6 / 512);
-  k32<<<1024, 64>>>(d, 16); hipEventRecord(e0); k32<<<1024, 64>>>(d, 16); hipEventRecord(e1); hipEventSynchronize(e1);
-  hipEventElapsedTime(&ms, e0, e1); printf("K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per wave\n", 32, 32 * 3.8, ms, ms * 1e6 / 512);
-  k64<<<1024, 64>>>(d, 8); hipEventRecord(e0); k64<<<1024, 64>>>(d, 8); hipEventRecord(e1); hipEventSynchronize(e1);
-  hipEventElapsedTime(&ms, e0, e1); printf("K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per wave\n", 64, 64 * 3.8, ms, ms * 1e6 / 512);
+  uint32_t* d; (void)hipMalloc(&d, 4096); hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); float ms;
+  k1<<<1024 * 1, 64>>>(d, 512); (void)hipEventRecord(e0); k1<<<1024 * 1, 64>>>(d, 512); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=1 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 1, 1 * 3.8, ms, ms * 1e6 / 512 / 1);
+  k4<<<1024 * 1, 64>>>(d, 128); (void)hipEventRecord(e0); k4<<<1024 * 1, 64>>>(d, 128); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=1 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 4, 4 * 3.8, ms, ms * 1e6 / 512 / 1);
+  k8<<<1024 * 1, 64>>>(d, 64); (void)hipEventRecord(e0); k8<<<1024 * 1, 64>>>(d, 64); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=1 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 8, 8 * 3.8, ms, ms * 1e6 / 512 / 1);
+  k16<<<1024 * 1, 64>>>(d, 32); (void)hipEventRecord(e0); k16<<<1024 * 1, 64>>>(d, 32); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=1 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 16, 16 * 3.8, ms, ms * 1e6 / 512 / 1);
+  k32<<<1024 * 1, 64>>>(d, 16); (void)hipEventRecord(e0); k32<<<1024 * 1, 64>>>(d, 16); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=1 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 32, 32 * 3.8, ms, ms * 1e6 / 512 / 1);
+  k64<<<1024 * 1, 64>>>(d, 8); (void)hipEventRecord(e0); k64<<<1024 * 1, 64>>>(d, 8); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=1 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 64, 64 * 3.8, ms, ms * 1e6 / 512 / 1);
+  k1<<<1024 * 2, 64>>>(d, 512); (void)hipEventRecord(e0); k1<<<1024 * 2, 64>>>(d, 512); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=2 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 1, 1 * 3.8, ms, ms * 1e6 / 512 / 2);
+  k4<<<1024 * 2, 64>>>(d, 128); (void)hipEventRecord(e0); k4<<<1024 * 2, 64>>>(d, 128); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=2 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 4, 4 * 3.8, ms, ms * 1e6 / 512 / 2);
+  k8<<<1024 * 2, 64>>>(d, 64); (void)hipEventRecord(e0); k8<<<1024 * 2, 64>>>(d, 64); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=2 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 8, 8 * 3.8, ms, ms * 1e6 / 512 / 2);
+  k16<<<1024 * 2, 64>>>(d, 32); (void)hipEventRecord(e0); k16<<<1024 * 2, 64>>>(d, 32); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=2 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 16, 16 * 3.8, ms, ms * 1e6 / 512 / 2);
+  k32<<<1024 * 2, 64>>>(d, 16); (void)hipEventRecord(e0); k32<<<1024 * 2, 64>>>(d, 16); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=2 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 32, 32 * 3.8, ms, ms * 1e6 / 512 / 2);
+  k64<<<1024 * 2, 64>>>(d, 8); (void)hipEventRecord(e0); k64<<<1024 * 2, 64>>>(d, 8); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=2 K=%3d body %7.1f KB: %8.3f ms, %.1f ns per product per SIMD\n", 64, 64 * 3.8, ms, ms * 1e6 / 512 / 2);
   return 0; }

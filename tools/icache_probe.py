@@ -21,10 +21,11 @@ for K in K_LIST:
     L.append("  if (iters < 0) out[threadIdx.x] = 1;")
     L.append("}")
 L.append("int main() {")
-L.append("  uint32_t* d; hipMalloc(&d, 4096); hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1); float ms;")
-for K in K_LIST:
-    it = 512 // K
-    L.append("  k%d<<<1024, 64>>>(d, %d); hipEventRecord(e0); k%d<<<1024, 64>>>(d, %d); hipEventRecord(e1); hipEventSynchronize(e1);" % (K, it, K, it))
-    L.append('  hipEventElapsedTime(&ms, e0, e1); printf("K=%%3d body %%7.1f KB: %%8.3f ms, %%.1f ns per product per wave\\n", %d, %d * 3.8, ms, ms * 1e6 / 512);' % (K, K))
+L.append("  uint32_t* d; (void)hipMalloc(&d, 4096); hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); float ms;")
+for W in (1, 2):
+    for K in K_LIST:
+        it = 512 // K
+        L.append("  k%d<<<1024 * %d, 64>>>(d, %d); (void)hipEventRecord(e0); k%d<<<1024 * %d, 64>>>(d, %d); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);" % (K, W, it, K, W, it))
+        L.append('  (void)hipEventElapsedTime(&ms, e0, e1); printf("waves/SIMD=%d K=%%3d body %%7.1f KB: %%8.3f ms, %%.1f ns per product per SIMD\\n", %d, %d * 3.8, ms, ms * 1e6 / 512 / %d);' % (W, K, K, W))
 L.append("  return 0; }")
 open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "icache_probe.hip"), "w").write("\n".join(L) + "\n")

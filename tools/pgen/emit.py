@@ -76,7 +76,7 @@ S_ODD = 40          # s[40:41] lane mask of the odd lanes (lane pairs: role 1)
 
 # storage configurations: (V slots, A slots, L slots)
 STORAGE = {1: (17, 18, 11),     # one wave per SIMD: 256 VGPR + 256 AGPR, 40 KB LDS
-           2: (11, 6, 5)}       # two waves per SIMD: 172 VGPR + 84 AGPR, 20 KB LDS
+           2: (17, 0, 5)}       # two waves per SIMD: 256 VGPR, no AGPR, 20 KB LDS
 
 
 class Emitter:
@@ -101,12 +101,28 @@ class Emitter:
         self.debug = False
         self.weight = 1
         self.ensuring = None
+        self.pending = {}            # V slot -> ("L" | "M", issue count after its last load)
+        self.vm_issued = 0
+        self.lgkm_issued = 0
+        self.items = None            # the block being allocated (prefetch lookahead)
         self.defer_vm_wait = False   # batch the waits of one operation's HBM reloads
         self.vm_wait_owed = False
 
     # ---------------- emission helpers ----------------
+    VMEM = ("global_load_dwordx2", "global_load_dword", "global_store_dwordx2", "global_store_byte",
+            "global_store_dwordx2_s", "global_load_dwordx2_s")
+
     def i(self, *t):
         self.code.append(t)
+        m = t[0]
+        if m in self.VMEM:
+            self.vm_issued += 1
+        elif m.startswith("ds_"):
+            self.lgkm_issued += 1
+        elif m == "s_waitcnt_vm0":
+            self.pending = {k: v for k, v in self.pending.items() if v[0] != "M"}
+        elif m == "s_waitcnt_lgkm0":
+            self.pending = {k: v for k, v in self.pending.items() if v[0] != "L"}
 
     def label(self):
         self.nlabel += 1
@@ -134,9 +150,30 @@ class Emitter:
                 return u
         return 1 << 30
 
+    def wait_pending(self, slots=None):
+        """complete the in-flight prefetches of the given V slots (default all),
+        with counters that leave younger memory operations outstanding"""
+        slots = list(self.pending) if slots is None else [k for k in slots if k in self.pending]
+        need = {"L": None, "M": None}
+        for k in slots:
+            kind, seq = self.pending[k]
+            need[kind] = seq if need[kind] is None else max(need[kind], seq)
+        if need["L"] is not None:
+            n = min(15, self.lgkm_issued - need["L"])
+            self.i("s_waitcnt_lgkm", n)
+            for k in [k for k, v in self.pending.items() if v[0] == "L" and v[1] <= self.lgkm_issued - n]:
+                del self.pending[k]
+        if need["M"] is not None:
+            n = min(63, self.vm_issued - need["M"])
+            self.i("s_waitcnt_vm", n)
+            for k in [k for k, v in self.pending.items() if v[0] == "M" and v[1] <= self.vm_issued - n]:
+                del self.pending[k]
+
     def get_vslot(self, pos, avoid=()):
         k = self.free_vslot()
         if k is not None:
+            if k in self.pending:
+                self.wait_pending([k])
             return k
         # Belady, cost-weighted: a value with a copy elsewhere is dropped for
         # free, so it is preferred unless it is needed much sooner
@@ -152,6 +189,8 @@ class Emitter:
                 best, bk = score, k
         if bk is None:
             raise AllocError("no evictable V slot")
+        if bk in self.pending:   # a late load must not land over the new value
+            self.wait_pending([bk])
         self.evict(bk, pos)
         return bk
 
@@ -249,8 +288,9 @@ class Emitter:
         vs.locs.clear()
 
     # ---------------- data movement ----------------
-    def copy(self, src, dst):
-        """move one Fq between locations (src and dst kinds may differ)"""
+    def copy(self, src, dst, wait=True):
+        """move one Fq between locations (src and dst kinds may differ);
+        wait=False leaves an L/M -> V load in flight (prefetch)"""
         sk, s = src
         dk, d = dst
         self.bump("move_%s%s" % (sk, dk))
@@ -269,7 +309,8 @@ class Emitter:
         elif sk == "L" and dk == "V":
             for j in range(7):
                 self.i("ds_read_b64", self.vbase(d) + 2 * j, LOFF, s * SLOT_BYTES + 512 * j)
-            self.i("s_waitcnt_lgkm0")
+            if wait:
+                self.i("s_waitcnt_lgkm0")
         elif sk == "V" and dk == "M":
             self.i("s_add_u32", S(S_TMP), S(S_WS), K(d * SLOT_BYTES))
             self.i("s_addc_u32", S(S_TMP + 1), S(S_WS + 1), K(0))
@@ -284,7 +325,9 @@ class Emitter:
             self.i("s_addc_u32", S(S_TMP + 1), S(S_WS + 1), K(0))
             for j in range(7):
                 self.i("global_load_dwordx2_s", self.vbase(d) + 2 * j, LOFF, S(S_TMP), 512 * j)
-            if self.defer_vm_wait:
+            if not wait:
+                pass
+            elif self.defer_vm_wait:
                 self.vm_wait_owed = True
             else:
                 self.i("s_waitcnt_vm0")
@@ -464,6 +507,8 @@ class Emitter:
         self.analyse(block)
         saved_ids = getattr(self, "local_ids", set())
         self.local_ids = self.block_vals(block)
+        saved_items = self.items
+        self.items = block.items
         vr = self.var_ranges(block) if top else {}
         for pos, it in enumerate(block.items):
             if top:
@@ -480,6 +525,8 @@ class Emitter:
                     if l == pos and name in self.home:
                         self.free_home(name, pos)
         # everything defined here is dead now
+        self.wait_pending()
+        self.items = saved_items
         for k in range(self.NV):
             vs = self.vslot[k]
             if vs is not None and vs.val.id in self.local_ids:
@@ -492,6 +539,7 @@ class Emitter:
     def park(self, block, pos):
         """before a construct: values of this block live after it leave the V
         slots (the body needs them all)"""
+        self.wait_pending()
         ids = self.block_vals(block)
         for k in range(self.NV):
             vs = self.vslot[k]
@@ -580,6 +628,11 @@ class Emitter:
                 dk = self.get_vslot(pos, avoid=self.pinned)
         else:
             dk = None
+        if any(x in self.pending for x in sk):
+            self.wait_pending(sk)
+        if dk is not None:
+            self.pinned.add(dk)
+        self.prefetch(pos)
         base = [self.vbase(x) for x in sk]
         d = self.vbase(dk) if dk is not None else None
         if k == "sop":
@@ -624,6 +677,65 @@ class Emitter:
             if not dvs.uses:
                 self.kill(dvs)
 
+    # ---------------- prefetch ----------------
+    COST = {"sop": None, "sqr": 460, "red": 62, "add": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
+            "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14}
+    AHEAD = {"L": 40, "M": 500}   # instructions of other work that hide the load latency
+    WINDOW = 2500
+
+    def op_cost(self, op):
+        if op.kind == "sop":
+            return 196 * (len(op.srcs) // 2 + 1) + 70
+        return self.COST.get(op.kind, 20)
+
+    def prefetch(self, pos):
+        """issue the LDS / HBM reloads of upcoming operations now, so their
+        latency hides behind the current operation's arithmetic"""
+        items = self.items
+        work = 0
+        for j in range(pos, min(len(items), pos + 40)):
+            it = items[j]
+            if not isinstance(it, Op):
+                break
+            if j > pos:
+                for v in it.srcs:
+                    vs = self.states.get(v.id)
+                    if vs is None or any(l[0] == "V" for l in vs.locs) or not vs.locs:
+                        continue
+                    src = self.best_src(vs)
+                    if src[0] == "A" or work < self.AHEAD[src[0]]:
+                        continue
+                    k = self.prefetch_slot(pos, j)
+                    if k is None:
+                        return
+                    self.copy(src, ("V", k), wait=False)
+                    self.vslot[k] = vs
+                    vs.locs.add(("V", k))
+                    self.pending[k] = (src[0], self.lgkm_issued if src[0] == "L" else self.vm_issued)
+                    self.bump("prefetch_" + src[0])
+            work += self.op_cost(it)
+            if work > self.WINDOW:
+                break
+
+    def prefetch_slot(self, pos, j):
+        """a V slot whose value is not needed before op j (free, or evictable)"""
+        for k in range(self.NV):
+            if self.vslot[k] is None and k not in self.pinned and k not in self.pending:
+                return k
+        best, bk = j, None
+        for k in range(self.NV):
+            if k in self.pinned or k in self.pending or self.vslot[k] is None:
+                continue
+            if len(self.vslot[k].locs) < 2:
+                continue    # dirty: evicting it would cost a spill
+            nu = self.next_use(self.vslot[k], pos)
+            if nu > best:
+                best, bk = nu, k
+        if bk is None:
+            return None
+        self.evict(bk, pos)
+        return bk
+
     def do_setvar(self, op, pos):
         name = op.imm
         vs = self.states[op.srcs[0].id]
@@ -638,6 +750,8 @@ class Emitter:
                 other.locs.discard(home)
         if home not in vs.locs:
             k = self.ensure_v(vs, pos, avoid=())
+            if k in self.pending:
+                self.wait_pending([k])
             self.copy(("V", k), home)
         if self.next_use(vs, pos) == 1 << 30:
             self.kill(vs)

@@ -78,8 +78,11 @@ def miller_loop_prog(homes=None, lanes=1):
     V = _Vars(p, lanes)
     for n in ("px", "py"):
         p.var(n, 1, homes.get(n))
-    p.set("px", p.load(0))
-    p.set("py", p.load(1))
+    if lanes == 1:
+        p.set("px", p.load(0))
+        p.set("py", p.load(1))
+    else:
+        p.set("px", p.load(0, 1))    # lane 0: px, lane 1: py
     for n in ("qx0", "qx1", "qy0", "qy1", "rx0", "rx1", "ry0", "ry1", "rz0", "rz1"):
         p.var(n, 1, homes.get(n))
     V.set2("qx", (p.load(2), p.load(3)) if lanes == 1 else p.load(2, 3))
@@ -99,7 +102,13 @@ def miller_loop_prog(homes=None, lanes=1):
             c, r = addition_step(T, r, V.get2("qx"), V.get2("qy"))
         for n, v in zip(("rx", "ry", "rz"), r):
             V.set2(n, v)
-        V.set12("f", ell(T, V.get12("f"), c, p.get("px"), p.get("py")))
+        if lanes == 1:
+            px, py = p.get("px"), p.get("py")
+        else:   # replicate P's coordinates from the packed (px | py) slot
+            pk = p.get("px")
+            o = p.swap(pk)
+            px, py = p.sel(pk, o), p.sel(o, pk)
+        V.set12("f", ell(T, V.get12("f"), c, px, py))
 
     with p.loop(62) as L:
         line("dbl")

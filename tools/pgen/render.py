@@ -108,6 +108,10 @@ class Renderer:
             return ["s_waitcnt lgkmcnt(0)"]
         if m == "s_waitcnt_vm0":
             return ["s_waitcnt vmcnt(0)"]
+        if m == "s_waitcnt_vm":
+            return ["s_waitcnt vmcnt(%d)" % a[0]]
+        if m == "s_waitcnt_lgkm":
+            return ["s_waitcnt lgkmcnt(%d)" % a[0]]
         if m == "s_nop":
             return ["s_nop %d" % a[0]]
         if m == "s_and_saveexec_b64":
@@ -152,7 +156,7 @@ def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256):
 \t\t.amdhsa_system_vgpr_workitem_id 0
 \t\t.amdhsa_next_free_vgpr 512
 \t\t.amdhsa_next_free_sgpr 96
-\t\t.amdhsa_accum_offset 256
+\t\t.amdhsa_accum_offset {aoff}
 \t\t.amdhsa_reserve_vcc 1
 \t\t.amdhsa_float_denorm_mode_32 3
 \t\t.amdhsa_float_denorm_mode_16_64 3

@@ -26,6 +26,8 @@ class Sim:
     def __init__(self, code, lane=0, lanes=None):
         self.code = code
         self.lanes = lanes or [lane]
+        self.inflight = {}   # (lane, vgpr) -> ("lgkm" | "vm", seq, value): loads not yet waited for
+        self.seq = {"lgkm": 0, "vm": 0}
         self.vf = {ln: [0] * 256 for ln in self.lanes}
         self.af = {ln: [0] * 256 for ln in self.lanes}
         self.v = self.vf[self.lanes[0]]
@@ -40,9 +42,16 @@ class Sim:
         self.trace = None
 
     # ---------- operand access ----------
+    def chk(self, x):
+        if (self.lane, x) in self.inflight:
+            raise AssertionError("v%d read/overwritten before its load was waited for (instr %d: %r)" % (
+                x, self.count, self.code[self.pc]))
+
     def rd(self, x):
         if isinstance(x, tuple):
             return x[1] & M32
+        if x < 256 and self.inflight:
+            self.chk(x)
         if x >= 512:
             return self.s[x - 512]
         if x >= 256:
@@ -52,12 +61,17 @@ class Sim:
     def rd64(self, x):
         if isinstance(x, tuple):
             return x[1] & M64
+        if x < 256 and self.inflight:
+            self.chk(x)
+            self.chk(x + 1)
         if x >= 512:
             return self.s[x - 512] | (self.s[x - 511] << 32)
         return self.v[x] | (self.v[x + 1] << 32)
 
     def wr(self, x, val):
         val &= M32
+        if x < 256 and self.inflight:
+            self.chk(x)
         if x >= 512:
             self.s[x - 512] = val
         elif x >= 256:
@@ -83,6 +97,18 @@ class Sim:
         m = self.s[106] | (self.s[107] << 32)
         return (m >> (self.lane % 64)) & 1
 
+    def async_wr(self, kind, x, val):
+        if self.inflight:
+            self.chk(x)
+        self.inflight[(self.lane, x)] = (kind, self.seq[kind], val & M32)
+
+    def complete(self, kind, keep=0):
+        """s_waitcnt <kind>(keep): all but the `keep` youngest operations are done"""
+        limit = self.seq[kind] - keep
+        for key in [k for k, (kd, sq, _) in self.inflight.items() if kd == kind and sq <= limit]:
+            ln, x = key
+            self.vf[ln][x] = self.inflight.pop(key)[2]
+
     def ld32(self, addr):
         return self.mem.get(addr, 0)
 
@@ -95,11 +121,16 @@ class Sim:
         pc = 0
         n = len(code)
         while pc < n:
+            self.pc = pc
             t = code[pc]
             self.count += 1
             if self.count > max_steps:
                 raise RuntimeError("step limit")
             m = t[0]
+            if m.startswith("ds_"):
+                self.seq["lgkm"] += 1
+            elif m.startswith("global_"):
+                self.seq["vm"] += 1
             if m.startswith("v_") or m.startswith("ds_") or m.startswith("global_") or m == "mark":
                 if m == "v_mov_b32_dpp_swap":
                     src = {ln: self.vf[ln][t[2]] for ln in self.lanes}
@@ -183,8 +214,8 @@ class Sim:
             self.lds[addr + 4] = rd(a[1] + 1)
         elif m == "ds_read_b64":
             addr = rd(a[1]) + a[2]
-            wr(a[0], self.lds.get(addr, 0))
-            wr(a[0] + 1, self.lds.get(addr + 4, 0))
+            self.async_wr("lgkm", a[0], self.lds.get(addr, 0))
+            self.async_wr("lgkm", a[0] + 1, self.lds.get(addr + 4, 0))
         elif m == "global_load_dwordx2":
             addr = rd64(a[1]) + a[2]
             wr(a[0], self.ld32(addr))
@@ -207,8 +238,8 @@ class Sim:
             self.st32(addr + 4, rd(a[1] + 1))
         elif m == "global_load_dwordx2_s":
             addr = rd64(a[2]) + rd(a[1]) + a[3]
-            wr(a[0], self.ld32(addr))
-            wr(a[0] + 1, self.ld32(addr + 4))
+            self.async_wr("vm", a[0], self.ld32(addr))
+            self.async_wr("vm", a[0] + 1, self.ld32(addr + 4))
         elif m == "s_load_dwordx2":
             addr = rd64(a[1]) + a[2]
             wr(a[0], self.ld32(addr))
@@ -259,7 +290,15 @@ class Sim:
                 if got != tuple(limbs):
                     raise AssertionError("first divergence at %r (instr %d): got %s want %s" % (
                         op, self.count, got, tuple(limbs)))
-        elif m in ("s_nop", "s_waitcnt_lgkm0", "s_waitcnt_vm0", "label"):
+        elif m == "s_waitcnt_lgkm0":
+            self.complete("lgkm")
+        elif m == "s_waitcnt_vm0":
+            self.complete("vm")
+        elif m == "s_waitcnt_lgkm":
+            self.complete("lgkm", a[0])
+        elif m == "s_waitcnt_vm":
+            self.complete("vm", a[0])
+        elif m in ("s_nop", "label"):
             pass
         elif m == "long_cbranch_scc1":
             return a[0] if self.scc else None
