@@ -37,8 +37,11 @@ hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, h
 }
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
-    char buf[256];
-    if (e != hipSuccess)
+    char buf[1024];
+    const char* detail = pa::gen_error_detail();
+    if (e != hipSuccess && detail[0])
+        snprintf(buf, sizeof buf, "%s: %s (%d) [%s]", what, hipGetErrorString(e), (int)e, detail);
+    else if (e != hipSuccess)
         snprintf(buf, sizeof buf, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
     else
         snprintf(buf, sizeof buf, "%s", what);

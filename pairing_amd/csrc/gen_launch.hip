@@ -27,6 +27,7 @@ struct GenDevice {
 
 std::mutex g_mu;
 GenDevice g_dev[64];
+thread_local std::string g_detail;   // the code object that failed to load, for pa_last_error
 
 // 0, 1: one lane per pairing; 2, 3: a lane pair per pairing
 const char* const kFile[4] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco", "pa_gen_miller_loop2.hsaco",
@@ -52,8 +53,11 @@ hipError_t load(GenDevice& d) {
     const std::string dir = lib_dir();
     for (int k = 0; k < 4; k++) {
         const std::string path = dir + "/" + kFile[k];
-        if ((d.err = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess) return d.err;
-        if ((d.err = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) return d.err;
+        if ((d.err = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess ||
+            (d.err = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) {
+            g_detail = "generated kernel " + path;
+            return d.err;
+        }
     }
     return hipSuccess;
 }
@@ -66,7 +70,10 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     std::lock_guard<std::mutex> lock(g_mu);
     GenDevice& d = g_dev[dev];
-    if ((e = load(d)) != hipSuccess) return e;
+    if ((e = load(d)) != hipSuccess) {
+        if (g_detail.empty()) g_detail = "generated kernels in " + lib_dir();
+        return e;
+    }
     const size_t blocks = (n * kLanes[which] + 63) / 64;
     size_t wave_bytes = 0;
     for (int k = 0; k < 4; k++) wave_bytes = kWaveBytes[k] > wave_bytes ? kWaveBytes[k] : wave_bytes;
@@ -92,6 +99,8 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
 }
 
 }  // namespace
+
+const char* gen_error_detail() { return g_detail.c_str(); }
 
 hipError_t launch_miller_loop_gen(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                   hipStream_t stream) {

@@ -50,6 +50,8 @@ hipError_t launch_final_exponentiation2(const uint64_t* in, uint64_t* out, uint8
 hipError_t launch_miller_loop_fl(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                  hipStream_t stream);
 hipError_t launch_final_exp_fl(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream);
+// non-empty after a generated code object failed to load (names the file)
+const char* gen_error_detail();
 // generated kernels (tools/pgen, gen_launch.hip); same results
 hipError_t launch_miller_loop_gen(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                   hipStream_t stream);

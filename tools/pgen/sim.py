@@ -39,6 +39,7 @@ class Sim:
         self.lane = lane
         self.labels = {t[1]: i for i, t in enumerate(code) if t[0] == "label"}
         self.count = 0
+        self.hist = {}
         self.trace = None
 
     # ---------- operand access ----------
@@ -127,6 +128,7 @@ class Sim:
             if self.count > max_steps:
                 raise RuntimeError("step limit")
             m = t[0]
+            self.hist[m] = self.hist.get(m, 0) + 1
             if m.startswith("ds_"):
                 self.seq["lgkm"] += 1
             elif m.startswith("global_"):

@@ -58,6 +58,9 @@ def check(which, seed=5, lane=3, debug=True):
     ok = got == [want[k] for k in range(12)]
     print("%s lane %d: %s (%d instructions simulated, %.1fs)" % (which, lane, "OK" if ok else "MISMATCH",
                                                               sm.count, time.time() - t))
+    if os.environ.get("PGEN_HIST"):
+        for m, c in sorted(sm.hist.items(), key=lambda x: -x[1]):
+            print("  %-28s %9d" % (m, c))
     return ok
 
 
