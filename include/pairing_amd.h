@@ -132,7 +132,53 @@ int pa_g1_batch_normalization(pa_g1 *v, size_t n);
  * the reference's; representation-independent PartialEq, ec.rs:45-85). */
 int pa_g1_wnaf_fixed_base(const pa_g1 *base, const pa_fr_repr *scalars, size_t n, pa_g1 *out);
 
+/* ---- point encodings and square roots (SURVEY.md §8 f, rank 1) ----
+ * Wire format of src/bls12_381/README.md "Serialization": big-endian
+ * coordinates (G2: x.c1, x.c0, y.c1, y.c0), flag bits in byte 0 (bit 7
+ * compressed, bit 6 infinity, bit 5 lexicographically largest y).  Record
+ * sizes: G1 uncompressed 96 B, compressed 48 B; G2 192 B / 96 B.
+ * status[i] is the GroupDecodingError (lib.rs:469-481) of record i: */
+#define PA_DECODE_OK 0
+#define PA_DECODE_NOT_ON_CURVE 1
+#define PA_DECODE_NOT_IN_SUBGROUP 2
+#define PA_DECODE_COORDINATE_X_C0 3   /* G1: "x coordinate"; G2: "x coordinate (c0)" */
+#define PA_DECODE_COORDINATE_X_C1 4   /* G2: "x coordinate (c1)" */
+#define PA_DECODE_COORDINATE_Y_C0 5   /* G1: "y coordinate"; G2: "y coordinate (c0)" */
+#define PA_DECODE_COORDINATE_Y_C1 6   /* G2: "y coordinate (c1)" */
+#define PA_DECODE_UNEXPECTED_COMPRESSION_MODE 7
+#define PA_DECODE_UNEXPECTED_INFORMATION 8
+/* EncodedPoint::into_affine (checked = 1: on-curve + subgroup checks,
+ * ec.rs:662-668, 785-792, 1322-1332, 1448-1455) or into_affine_unchecked
+ * (checked = 0).  Records that fail get status != 0 and out[i] = the point at
+ * infinity. */
+int pa_g1_decode_batch(const uint8_t *enc, size_t n, int compressed, int checked, pa_g1_affine *out,
+                       uint8_t *status);
+int pa_g2_decode_batch(const uint8_t *enc, size_t n, int compressed, int checked, pa_g2_affine *out,
+                       uint8_t *status);
+/* EncodedPoint::from_affine (ec.rs:737-752, 839-867, 1398-1415, 1510-1539) */
+int pa_g1_encode_batch(const pa_g1_affine *in, size_t n, int compressed, uint8_t *enc);
+int pa_g2_encode_batch(const pa_g2_affine *in, size_t n, int compressed, uint8_t *enc);
+/* SqrtField::sqrt, fq.rs:1147-1170 / fq2.rs:167-220; ok[i] = 0 for a non-residue */
+int pa_fq_sqrt_batch(const pa_fq *a, pa_fq *out, uint8_t *ok, size_t n);
+int pa_fq2_sqrt_batch(const pa_fq2 *a, pa_fq2 *out, uint8_t *ok, size_t n);
+
+/* ---- multi-pairing and multi-device (SURVEY.md §8 b, e, f rank 2) ---- */
+/* Engine::miller_loop over n (G1Affine, G2Affine) pairs -- prepare fused on
+ * device -- = the product of the per-pair loops (mod.rs:40-102); then, for
+ * pa_multi_pairing, Engine::final_exponentiation (mod.rs:104-160): the
+ * batch-verification shape e(P_1,Q_1)...e(P_n,Q_n).  ok = 0 iff the product
+ * Miller value is zero (None). */
+int pa_multi_miller_loop_affine(const pa_g1_affine *p, const pa_g2_affine *q, size_t n, pa_fq12 *out);
+int pa_multi_pairing(const pa_g1_affine *p, const pa_g2_affine *q, size_t n, pa_fq12 *out, uint8_t *ok);
+/* pa_pairing_batch split over devices 0..ndev-1 of this process (contiguous
+ * shards, one host thread per device); ndev <= pa_device_count. */
+int pa_pairing_batch_multi_gpu(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n, int ndev);
+
 /* ---- device-resident variants (pointers are device memory) ---- */
+int pa_g1_decode_batch_device(const uint8_t *enc, size_t n, int compressed, int checked, pa_g1_affine *out,
+                              uint8_t *status, void *stream);
+int pa_g2_decode_batch_device(const uint8_t *enc, size_t n, int compressed, int checked, pa_g2_affine *out,
+                              uint8_t *status, void *stream);
 int pa_g1_batch_normalization_device(pa_g1 *v, size_t n, void *stream);
 /* u64 words of the fixed-base table and of the scratch used to build it */
 size_t pa_g1_fixed_base_table_words(void);

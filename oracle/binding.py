@@ -96,6 +96,10 @@ def _declare(L):
         "o_g1_recommended_wnaf_for_scalar": [_P],
         "o_g2_recommended_wnaf_for_scalar": [_P],
         "o_sizeof": [_I],
+        "o_g1_decode_batch": [_P, _N, _I, _I, _P, _P, _I],
+        "o_g2_decode_batch": [_P, _N, _I, _I, _P, _P, _I],
+        "o_fq_sqrt_batch": [_P, _N, _P, _P],
+        "o_fq2_sqrt_batch": [_P, _N, _P, _P],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -294,6 +298,32 @@ def kg_vectors(group, count, compressed):
     fn = lib().o_g1_kg_vectors if group == 1 else lib().o_g2_kg_vectors
     fn(_p(o), count, int(bool(compressed)))
     return o.tobytes()
+
+
+# ---- point decoding (EncodedPoint::into_affine[_unchecked]) ----
+ENC_SIZE = {(1, False): 96, (1, True): 48, (2, False): 192, (2, True): 96}
+
+
+def decode(group, enc, compressed, checked=True, nthreads=1):
+    """enc: (n, size) uint8 records -> (affine points, status bytes)"""
+    enc = np.ascontiguousarray(enc, dtype=np.uint8)
+    n = enc.shape[0]
+    assert enc.shape[1] == ENC_SIZE[(group, bool(compressed))]
+    o = _out(n, W_G1A if group == 1 else W_G2A)
+    st = np.zeros(n, np.uint8)
+    fn = lib().o_g1_decode_batch if group == 1 else lib().o_g2_decode_batch
+    fn(_p(enc), n, int(bool(compressed)), int(bool(checked)), _p(o), _p(st), nthreads)
+    return o, st
+
+
+def fq_sqrt(a):
+    o = _out(_n(a), W_FQ); ok = np.zeros(_n(a), np.uint8)
+    lib().o_fq_sqrt_batch(_p(a), _n(a), _p(o), _p(ok)); return o, ok
+
+
+def fq2_sqrt(a):
+    o = _out(_n(a), W_FQ2); ok = np.zeros(_n(a), np.uint8)
+    lib().o_fq2_sqrt_batch(_p(a), _n(a), _p(o), _p(ok)); return o, ok
 
 
 # ---- pairing ----

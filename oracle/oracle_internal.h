@@ -71,4 +71,33 @@ void o_fq12_mul(o_fq12 *a, const o_fq12 *b);
 int o_fq12_inverse(o_fq12 *out, const o_fq12 *a);
 void o_fq12_pow(o_fq12 *out, const o_fq12 *a, const uint64_t *exp, size_t n);
 
+/* curve_impl instantiations used by the decoders (oracle_curve_impl.h) */
+int o_g1_is_zero(const o_g1 *p);
+int o_g2_is_zero(const o_g2 *p);
+o_g1_affine o_g1_affine_zero(void);
+o_g2_affine o_g2_affine_zero(void);
+o_g1 o_g1_affine_mul(const o_g1_affine *a, const uint64_t scalar[4]);
+o_g2 o_g2_affine_mul(const o_g2_affine *a, const uint64_t scalar[4]);
+int o_g1_is_on_curve(const o_g1_affine *a);
+int o_g2_is_on_curve(const o_g2_affine *a);
+
+/* decoding status = GroupDecodingError (lib.rs:469-481); same codes as
+ * PA_DECODE_* in include/pairing_amd.h.  CoordinateDecodingError carries the
+ * coordinate name: G1 "x coordinate" / "y coordinate" map to X_C0 / Y_C0. */
+enum {
+    O_DEC_OK = 0,
+    O_DEC_NOT_ON_CURVE = 1,
+    O_DEC_NOT_IN_SUBGROUP = 2,
+    O_DEC_X_C0 = 3,
+    O_DEC_X_C1 = 4,
+    O_DEC_Y_C0 = 5,
+    O_DEC_Y_C1 = 6,
+    O_DEC_UNEXPECTED_COMPRESSION_MODE = 7,
+    O_DEC_UNEXPECTED_INFORMATION = 8,
+};
+int o_fq_sqrt(o_fq *out, const o_fq *a);
+int o_fq2_sqrt(o_fq2 *out, const o_fq2 *a);
+int o_g1_decode(o_g1_affine *out, const uint8_t *enc, int compressed, int checked);
+int o_g2_decode(o_g2_affine *out, const uint8_t *enc, int compressed, int checked);
+
 #endif

@@ -26,6 +26,8 @@ __all__ = [
     "fq12_frobenius_map", "fq12_cyclotomic_square", "fq12_mul_by_014",
     "g1_batch_normalization", "g1_wnaf_fixed_base",
     "g2_prepare", "miller_loop_batch", "multi_miller_loop", "final_exponentiation", "pairing",
+    "multi_miller_loop_affine", "multi_pairing", "pairing_multi_gpu",
+    "fq_sqrt", "fq2_sqrt", "g1_decode", "g2_decode", "g1_encode", "g2_encode", "DECODE_STATUS",
 ]
 
 
@@ -191,3 +193,104 @@ def g1_wnaf_fixed_base(base, scalars):
     out = np.empty((s.shape[0], W_G1), np.uint64)
     call("pa_g1_wnaf_fixed_base", ptr(b), ptr(s), s.shape[0], ptr(out))
     return out
+
+
+# ---- multi-pairing (SURVEY.md §8 f rank 2) and in-process multi-device ----
+def _pairs(p, q):
+    p = as_rows(p, W_G1A, "p") if len(p) else np.zeros((0, W_G1A), np.uint64)
+    q = as_rows(q, W_G2A, "q") if len(q) else np.zeros((0, W_G2A), np.uint64)
+    if p.shape[0] != q.shape[0]:
+        raise ValueError("p and q lengths differ")
+    return p, q
+
+
+def multi_miller_loop_affine(p, q):
+    """Engine::miller_loop over (G1Affine, G2Affine) pairs, prepare fused on device:
+    the product of the per-pair loops (mod.rs:40-102)."""
+    p, q = _pairs(p, q)
+    out = np.empty((1, W_FQ12), np.uint64)
+    call("pa_multi_miller_loop_affine", ptr(p), ptr(q), p.shape[0], ptr(out))
+    return out[0]
+
+
+def multi_pairing(p, q):
+    """final_exponentiation(miller_loop(pairs)) -- the batch-verification product
+    e(P_1,Q_1)...e(P_n,Q_n); returns (Fq12, ok)."""
+    p, q = _pairs(p, q)
+    out = np.empty((1, W_FQ12), np.uint64)
+    ok = np.zeros(1, np.uint8)
+    call("pa_multi_pairing", ptr(p), ptr(q), p.shape[0], ptr(out), ptr(ok))
+    return out[0], bool(ok[0])
+
+
+def pairing_multi_gpu(p, q, ndev):
+    """pairing(p, q) split over devices 0..ndev-1 of this process."""
+    p, q = _pairs(p, q)
+    out = np.empty((p.shape[0], W_FQ12), np.uint64)
+    call("pa_pairing_batch_multi_gpu", ptr(p), ptr(q), ptr(out), p.shape[0], int(ndev))
+    return out
+
+
+# ---- square roots and point encodings (SURVEY.md §8 f rank 1) ----
+# status byte -> GroupDecodingError (lib.rs:469-481)
+DECODE_STATUS = {
+    0: "Ok", 1: "NotOnCurve", 2: "NotInSubgroup",
+    3: "CoordinateDecodingError(x / x.c0)", 4: "CoordinateDecodingError(x.c1)",
+    5: "CoordinateDecodingError(y / y.c0)", 6: "CoordinateDecodingError(y.c1)",
+    7: "UnexpectedCompressionMode", 8: "UnexpectedInformation",
+}
+ENCODED_SIZE = {(1, False): 96, (1, True): 48, (2, False): 192, (2, True): 96}
+
+
+def fq_sqrt(a):
+    """SqrtField::sqrt for Fq (fq.rs:1147-1170): (roots, ok); ok False for non-residues."""
+    return _inverse("pa_fq_sqrt_batch", a, W_FQ)
+
+
+def fq2_sqrt(a):
+    """SqrtField::sqrt for Fq2 (fq2.rs:167-220): (roots, ok)."""
+    return _inverse("pa_fq2_sqrt_batch", a, W_FQ2)
+
+
+def _decode(group, enc, compressed, checked):
+    size = ENCODED_SIZE[(group, bool(compressed))]
+    enc = np.ascontiguousarray(np.asarray(enc, dtype=np.uint8))
+    if enc.ndim == 1:
+        enc = enc.reshape(-1, size)
+    if enc.ndim != 2 or enc.shape[1] != size:
+        raise ValueError("encodings must have shape (n, %d), got %s" % (size, enc.shape))
+    n = enc.shape[0]
+    out = np.empty((n, W_G1A if group == 1 else W_G2A), np.uint64)
+    status = np.zeros(n, np.uint8)
+    call("pa_g%d_decode_batch" % group, ptr(enc), n, int(bool(compressed)), int(bool(checked)), ptr(out),
+         ptr(status))
+    return out, status
+
+
+def g1_decode(enc, compressed, checked=True):
+    """G1Uncompressed / G1Compressed ::into_affine (checked) or ::into_affine_unchecked
+    (ec.rs:662-837) for (n, 96|48) uint8 records: (affine points, status bytes)."""
+    return _decode(1, enc, compressed, checked)
+
+
+def g2_decode(enc, compressed, checked=True):
+    """G2Uncompressed / G2Compressed ::into_affine[_unchecked] (ec.rs:1322-1509)."""
+    return _decode(2, enc, compressed, checked)
+
+
+def _encode(group, pts, compressed):
+    pts = as_rows(pts, W_G1A if group == 1 else W_G2A, "points")
+    size = ENCODED_SIZE[(group, bool(compressed))]
+    enc = np.zeros((pts.shape[0], size), np.uint8)
+    call("pa_g%d_encode_batch" % group, ptr(pts), pts.shape[0], int(bool(compressed)), ptr(enc))
+    return enc
+
+
+def g1_encode(pts, compressed):
+    """EncodedPoint::from_affine for G1 (ec.rs:737-752, 839-867)."""
+    return _encode(1, pts, compressed)
+
+
+def g2_encode(pts, compressed):
+    """EncodedPoint::from_affine for G2 (ec.rs:1398-1415, 1510-1539)."""
+    return _encode(2, pts, compressed)

@@ -74,6 +74,17 @@ _SIGS = {
     "pa_miller_loop_fused_batch_device": [_P, _P, _P, _N, _P],
     "pa_final_exponentiation_batch_device": [_P, _P, _P, _N, _P],
     "pa_pairing_batch_device": [_P, _P, _P, _P, _N, _P],
+    "pa_g1_decode_batch": [_P, _N, ctypes.c_int, ctypes.c_int, _P, _P],
+    "pa_g2_decode_batch": [_P, _N, ctypes.c_int, ctypes.c_int, _P, _P],
+    "pa_g1_encode_batch": [_P, _N, ctypes.c_int, _P],
+    "pa_g2_encode_batch": [_P, _N, ctypes.c_int, _P],
+    "pa_fq_sqrt_batch": [_P, _P, _P, _N],
+    "pa_fq2_sqrt_batch": [_P, _P, _P, _N],
+    "pa_multi_miller_loop_affine": [_P, _P, _N, _P],
+    "pa_multi_pairing": [_P, _P, _N, _P, _P],
+    "pa_pairing_batch_multi_gpu": [_P, _P, _P, _N, ctypes.c_int],
+    "pa_g1_decode_batch_device": [_P, _N, ctypes.c_int, ctypes.c_int, _P, _P, _P],
+    "pa_g2_decode_batch_device": [_P, _N, ctypes.c_int, ctypes.c_int, _P, _P, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_lib, _name)

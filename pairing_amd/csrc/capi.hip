@@ -7,6 +7,8 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/pairing_amd.h"
 #include "launch.h"
@@ -280,6 +282,130 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
     return download(out, dout, 576 * n);
 }
 
+int pa_pairing_batch_multi_gpu(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n, int ndev) {
+    int count = 0;
+    PA_TRY(hipGetDeviceCount(&count), "hipGetDeviceCount");
+    if (ndev < 1 || ndev > count) return fail(PA_ERR_INVALID_ARGUMENT, "ndev out of range");
+    if (n == 0) return PA_OK;
+    if (!p || !q || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    // contiguous shards (SURVEY.md §8 e); each worker thread owns one device
+    std::vector<int> rcs(ndev, PA_OK);
+    std::vector<std::string> errs(ndev);
+    std::vector<std::thread> workers;
+    const size_t base = n / ndev, extra = n % ndev;
+    size_t lo = 0;
+    for (int d = 0; d < ndev; d++) {
+        const size_t cnt = base + ((size_t)d < extra ? 1 : 0);
+        workers.emplace_back([=, &rcs, &errs] {
+            hipError_t e = hipSetDevice(d);
+            if (e != hipSuccess) {
+                rcs[d] = fail(hip_code(e), "hipSetDevice", e);
+            } else {
+                rcs[d] = pa_pairing_batch(p + lo, q + lo, out + lo, cnt);
+            }
+            if (rcs[d] != PA_OK) errs[d] = g_last_error;
+        });
+        lo += cnt;
+    }
+    for (auto& t : workers) t.join();
+    for (int d = 0; d < ndev; d++)
+        if (rcs[d] != PA_OK) {
+            g_last_error = "device " + std::to_string(d) + ": " + errs[d];
+            return rcs[d];
+        }
+    return PA_OK;
+}
+
+int pa_multi_miller_loop_affine(const pa_g1_affine* p, const pa_g2_affine* q, size_t n, pa_fq12* out) {
+    if (!out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (n == 0) return pa_multi_miller_loop(nullptr, nullptr, 0, out);
+    if (!p || !q) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf dp, dq, dwork, dout;
+    int rc;
+    if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_affine) * n)))
+        return rc;
+    PA_TRY(dwork.alloc(576 * n), "hipMalloc");
+    PA_TRY(dout.alloc(576), "hipMalloc");
+    // per-pair loops (infinity pairs give one, as mod.rs:50-54 skips them), then the product tree
+    PA_TRY(ml_launch(dp.as<uint64_t>(), dq.as<uint64_t>(), dwork.as<uint64_t>(), n, nullptr), "kernel launch");
+    PA_TRY(pa::launch_fq12_product(dwork.as<uint64_t>(), n, dout.as<uint64_t>(), nullptr), "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, 576);
+}
+
+int pa_multi_pairing(const pa_g1_affine* p, const pa_g2_affine* q, size_t n, pa_fq12* out, uint8_t* ok) {
+    if (!out || !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    pa_fq12 ml;
+    int rc = pa_multi_miller_loop_affine(p, q, n, &ml);
+    if (rc) return rc;
+    return pa_final_exponentiation_batch(&ml, out, ok, 1);
+}
+
+// ---- point encodings ----
+namespace {
+constexpr size_t enc_size(int group, int compressed) { return (group == 1 ? 48 : 96) * (compressed ? 1 : 2); }
+int host_decode(int group, const uint8_t* enc, size_t n, int compressed, int checked, void* out, uint8_t* status) {
+    if (n == 0) return PA_OK;
+    if (!enc || !out || !status) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const size_t rec = group == 1 ? sizeof(pa_g1_affine) : sizeof(pa_g2_affine);
+    DevBuf de, dout, dst;
+    int rc;
+    if ((rc = upload(de, enc, enc_size(group, compressed) * n))) return rc;
+    PA_TRY(dout.alloc(rec * n), "hipMalloc");
+    PA_TRY(dst.alloc(n), "hipMalloc");
+    PA_TRY(pa::launch_decode(group, compressed, checked, de.as<uint8_t>(), n, dout.as<uint64_t>(),
+                             dst.as<uint8_t>(), nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    if ((rc = download(out, dout, rec * n))) return rc;
+    return download(status, dst, n);
+}
+int host_encode(int group, const void* in, size_t n, int compressed, uint8_t* enc) {
+    if (n == 0) return PA_OK;
+    if (!in || !enc) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const size_t rec = group == 1 ? sizeof(pa_g1_affine) : sizeof(pa_g2_affine);
+    DevBuf din, de;
+    int rc;
+    if ((rc = upload(din, in, rec * n))) return rc;
+    PA_TRY(de.alloc(enc_size(group, compressed) * n), "hipMalloc");
+    PA_TRY(pa::launch_encode(group, compressed, din.as<uint64_t>(), n, de.as<uint8_t>(), nullptr), "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(enc, de, enc_size(group, compressed) * n);
+}
+int host_sqrt(int degree, const void* a, void* out, uint8_t* ok, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!a || !out || !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const size_t bytes = 48 * (size_t)degree * n;
+    DevBuf da, dout, dok;
+    int rc;
+    if ((rc = upload(da, a, bytes))) return rc;
+    PA_TRY(dout.alloc(bytes), "hipMalloc");
+    PA_TRY(dok.alloc(n), "hipMalloc");
+    PA_TRY(pa::launch_sqrt(degree, da.as<uint64_t>(), n, dout.as<uint64_t>(), dok.as<uint8_t>(), nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    if ((rc = download(out, dout, bytes))) return rc;
+    return download(ok, dok, n);
+}
+}  // namespace
+
+int pa_g1_decode_batch(const uint8_t* enc, size_t n, int compressed, int checked, pa_g1_affine* out,
+                       uint8_t* status) {
+    return host_decode(1, enc, n, compressed != 0, checked != 0, out, status);
+}
+int pa_g2_decode_batch(const uint8_t* enc, size_t n, int compressed, int checked, pa_g2_affine* out,
+                       uint8_t* status) {
+    return host_decode(2, enc, n, compressed != 0, checked != 0, out, status);
+}
+int pa_g1_encode_batch(const pa_g1_affine* in, size_t n, int compressed, uint8_t* enc) {
+    return host_encode(1, in, n, compressed != 0, enc);
+}
+int pa_g2_encode_batch(const pa_g2_affine* in, size_t n, int compressed, uint8_t* enc) {
+    return host_encode(2, in, n, compressed != 0, enc);
+}
+int pa_fq_sqrt_batch(const pa_fq* a, pa_fq* out, uint8_t* ok, size_t n) { return host_sqrt(1, a, out, ok, n); }
+int pa_fq2_sqrt_batch(const pa_fq2* a, pa_fq2* out, uint8_t* ok, size_t n) { return host_sqrt(2, a, out, ok, n); }
+
 int pa_g1_batch_normalization(pa_g1* v, size_t n) {
     if (n == 0) return PA_OK;
     if (!v) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
@@ -309,6 +435,20 @@ int pa_g1_wnaf_fixed_base(const pa_g1* base, const pa_fr_repr* scalars, size_t n
 }
 
 // ---- device-resident variants ----
+int pa_g1_decode_batch_device(const uint8_t* enc, size_t n, int compressed, int checked, pa_g1_affine* out,
+                              uint8_t* status, void* stream) {
+    if (n && (!enc || !out || !status)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_decode(1, compressed != 0, checked != 0, enc, n, (uint64_t*)out, status, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+int pa_g2_decode_batch_device(const uint8_t* enc, size_t n, int compressed, int checked, pa_g2_affine* out,
+                              uint8_t* status, void* stream) {
+    if (n && (!enc || !out || !status)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_decode(2, compressed != 0, checked != 0, enc, n, (uint64_t*)out, status, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
 int pa_g1_batch_normalization_device(pa_g1* v, size_t n, void* stream) {
     if (n && !v) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     PA_TRY(pa::launch_g1_batch_normalize((uint64_t*)v, n, (hipStream_t)stream), "kernel launch");

@@ -1,0 +1,405 @@
+// Point decoding / encoding and square roots (SURVEY.md §8 f, rank 1): the
+// step in front of every pairing in a verifier.
+//
+//   EncodedPoint::into_affine[_unchecked] for G1Uncompressed (ec.rs:662-736),
+//   G1Compressed (ec.rs:785-837), G2Uncompressed (ec.rs:1322-1397),
+//   G2Compressed (ec.rs:1448-1509); EncodedPoint::from_affine (ec.rs:737-752,
+//   839-867, 1398-1415, 1510-1539); SqrtField::sqrt for Fq (fq.rs:1147-1170)
+//   and Fq2 (fq2.rs:167-220).
+//
+// One lane per record.  Every output is canonical (affine coordinates, status
+// codes, bytes), so the only freedom used is in how the subgroup membership
+// r*P == 0 (ec.rs:142-144) is evaluated: MSB-first double-and-add from the top
+// set bit of r with the reference's Jacobian formulas (curve.h).  Records are
+// read as 32-bit words and byte-swapped (the wire format is big-endian).
+#include <type_traits>
+
+#include "curve.h"
+#include "launch.h"
+
+namespace pa {
+namespace {
+
+// (q - 3) / 4 and (q - 1) / 2: fq.rs:1152-1159, fq2.rs:174-181, 207-214
+__constant__ const uint64_t kQm3Div4[6] = {0xee7fbfffffffeaaaULL, 0x07aaffffac54ffffULL, 0xd9cc34a83dac3d89ULL,
+                                           0xd91dd2e13ce144afULL, 0x92c6e9ed90d2eb35ULL, 0x0680447a8e5ff9a6ULL};
+__constant__ const uint64_t kQm1Div2[6] = {0xdcff7fffffffd555ULL, 0x0f55ffff58a9ffffULL, 0xb39869507b587b12ULL,
+                                           0xb23ba5c279c2895fULL, 0x258dd3db21a5d66bULL, 0x0d0088f51cbff34dULL};
+// Fr::char() = r, fr.rs:5-10
+__constant__ const uint64_t kFrModulus[4] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL,
+                                             0x73eda753299d7d48ULL};
+// R^2 mod q (fq.rs:33-40) and -1 (fq.rs:501-508), Montgomery
+__constant__ const uint64_t kR2[6] = {0xf4df1f341c341746ULL, 0x0a76e6a609d104f1ULL, 0x8de5476c4c95b6d5ULL,
+                                      0x67eb88a9939d83c0ULL, 0x9a793e85b519952dULL, 0x11988fe592cae3aaULL};
+__constant__ const uint64_t kNegOne[6] = {0x43f5fffffffcaaaeULL, 0x32b7fff2ed47fffdULL, 0x07e83a49a2e99d69ULL,
+                                          0xeca8f3318332bb7aULL, 0xef148d1ea0f4c069ULL, 0x040ab3263eff0206ULL};
+// b = 4 (Montgomery), ec.rs:885-887 / 1557-1562
+__constant__ const uint64_t kB[6] = {0xaa270000000cfff3ULL, 0x53cc0032fc34000aULL, 0x478fe97a6b0a807fULL,
+                                     0xb1d37ebee6ba24d7ULL, 0x8ec9733bbf78ab2fULL, 0x09d645513d83de7eULL};
+
+enum : uint8_t {
+    DEC_OK = 0,
+    DEC_NOT_ON_CURVE = 1,
+    DEC_NOT_IN_SUBGROUP = 2,
+    DEC_X_C0 = 3,
+    DEC_X_C1 = 4,
+    DEC_Y_C0 = 5,
+    DEC_Y_C1 = 6,
+    DEC_UNEXPECTED_COMPRESSION_MODE = 7,
+    DEC_UNEXPECTED_INFORMATION = 8,
+};
+
+PA_DEV void fq_const(Fq& r, const uint64_t* c) { fq_from_u64(r, c); }
+
+// a^e, MSB first; `top` = index of e's top set bit, Field::pow lib.rs:306-324; e is wave-uniform
+template <class F>
+__device__ __noinline__ void pow_fixed(F& r, const F& a, const uint64_t* e, int top) {
+    F acc = a;
+#pragma unroll 1
+    for (int bit = top - 1; bit >= 0; bit--) {
+        sqr(acc, acc);
+        if ((e[bit >> 6] >> (bit & 63)) & 1) mul(acc, acc, a);
+    }
+    r = acc;
+}
+
+// canonical (into_repr) words of a Montgomery element: a * 1 * R^-1
+PA_DEV void fq_canonical(uint32_t c[12], const Fq& a) {
+    Fq one_raw, t;
+    fq_zero(one_raw);
+    one_raw.w[0] = 1;
+    fq_mul(t, a, one_raw);
+#pragma unroll
+    for (int i = 0; i < 12; i++) c[i] = t.w[i];
+}
+// PartialOrd of Fq (canonical comparison): -1, 0, 1
+PA_DEV int fq_cmp(const Fq& a, const Fq& b) {
+    uint32_t ca[12], cb[12];
+    fq_canonical(ca, a);
+    fq_canonical(cb, b);
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+        if (r == 0 && ca[11 - i] != cb[11 - i]) r = ca[11 - i] < cb[11 - i] ? -1 : 1;
+    }
+    return r;
+}
+PA_DEV int cmp(const Fq& a, const Fq& b) { return fq_cmp(a, b); }
+PA_DEV int cmp(const Fq2& a, const Fq2& b) {  // fq2.rs:21-30: c1 first
+    const int c = fq_cmp(a.c1, b.c1);
+    return c != 0 ? c : fq_cmp(a.c0, b.c0);
+}
+
+// SqrtField::sqrt, fq.rs:1147-1170
+PA_DEV bool sqrt(Fq& r, const Fq& a) {
+    Fq a1, a0, m1;
+    pow_fixed(a1, a, kQm3Div4, 378);
+    fq_sqr(a0, a1);
+    fq_mul(a0, a0, a);
+    fq_const(m1, kNegOne);
+    if (fq_eq(a0, m1)) return false;
+    fq_mul(r, a1, a);
+    return true;
+}
+// SqrtField::sqrt, fq2.rs:167-220 (Algorithm 9 of eprint 2012/685)
+PA_DEV bool sqrt(Fq2& r, const Fq2& a) {
+    if (is_zero(a)) {
+        zero(r);
+        return true;
+    }
+    Fq2 a1, alpha, a0, m1;
+    pow_fixed(a1, a, kQm3Div4, 378);
+    sqr(alpha, a1);
+    mul(alpha, alpha, a);
+    frobenius_map(a0, alpha, 1);
+    mul(a0, a0, alpha);
+    fq_const(m1.c0, kNegOne);
+    fq_zero(m1.c1);
+    if (eq(a0, m1)) return false;
+    mul(a1, a1, a);
+    if (eq(alpha, m1)) {
+        Fq2 u;
+        fq_zero(u.c0);
+        fq_one(u.c1);
+        mul(r, a1, u);
+    } else {
+        Fq2 one2, t;
+        one(one2);
+        add(alpha, alpha, one2);
+        pow_fixed(t, alpha, kQm1Div2, 379);
+        mul(r, a1, t);
+    }
+    return true;
+}
+
+PA_DEV void coeff_b(Fq& b) { fq_const(b, kB); }
+PA_DEV void coeff_b(Fq2& b) {
+    fq_const(b.c0, kB);
+    fq_const(b.c1, kB);
+}
+
+// x^3 + b
+template <class F>
+PA_DEV void curve_rhs(F& r, const F& x) {
+    F b;
+    sqr(r, x);
+    mul(r, r, x);
+    coeff_b(b);
+    add(r, r, b);
+}
+
+// get_point_from_x, ec.rs:100-121
+template <class F>
+PA_DEV bool point_from_x(Aff<F>& out, const F& x, bool greatest) {
+    F rhs, y, negy;
+    curve_rhs(rhs, x);
+    if (!sqrt(y, rhs)) return false;
+    neg(negy, y);
+    out.x = x;
+    out.y = ((cmp(y, negy) < 0) != greatest) ? y : negy;
+    out.inf = false;
+    return true;
+}
+
+// is_on_curve, ec.rs:125-140 (affine, not infinity)
+template <class F>
+PA_DEV bool on_curve(const Aff<F>& a) {
+    F y2, rhs;
+    sqr(y2, a.y);
+    curve_rhs(rhs, a.x);
+    return eq(y2, rhs);
+}
+
+// is_in_correct_subgroup_assuming_on_curve, ec.rs:142-144: r * P == 0
+template <class F>
+__device__ __noinline__ bool in_subgroup(const Aff<F>& a) {
+    if (a.inf) return true;
+    Jac<F> acc;
+    jac_from_affine(acc, a);  // bit 254, the top set bit of r
+#pragma unroll 1
+    for (int bit = 253; bit >= 0; bit--) {
+        jac_double(acc);
+        if ((kFrModulus[bit >> 6] >> (bit & 63)) & 1) jac_add_mixed(acc, a);
+    }
+    return jac_is_zero(acc);
+}
+
+// 48 big-endian bytes (word-aligned) -> 12 little-endian u32 words
+PA_DEV void read_be48(uint32_t w[12], const uint8_t* src) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+#pragma unroll
+    for (int j = 0; j < 12; j++) w[11 - j] = __builtin_bswap32(s[j]);
+}
+PA_DEV void write_be48(uint8_t* dst, const uint32_t w[12]) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+    for (int j = 0; j < 12; j++) d[j] = __builtin_bswap32(w[11 - j]);
+}
+
+// PrimeField::from_repr, fq.rs:747-756: canonical words < q, then * R^2
+PA_DEV bool from_repr(Fq& r, const uint32_t w[12]) {
+    int c = 0;
+#pragma unroll
+    for (int i = 11; i >= 0; i--) {
+        if (c == 0 && w[i] != q_word(i)) c = w[i] < q_word(i) ? -1 : 1;
+    }
+    if (c >= 0) return false;
+    Fq x, r2;
+#pragma unroll
+    for (int i = 0; i < 12; i++) x.w[i] = w[i];
+    fq_const(r2, kR2);
+    fq_mul(r, x, r2);
+    return true;
+}
+
+// The flag handling shared by the four into_affine_unchecked bodies.  `b` are
+// the record's words in wire order (byte-swapped per word: b[0] holds bytes
+// 0..3 with byte 0 in bits 31..24).  Returns -1 to go on decoding.
+PA_DEV int check_flags(uint32_t* b, int nwords, bool compressed, bool& greatest) {
+    greatest = false;
+    const uint32_t top = b[0] >> 24;
+    if (((top >> 7) & 1) != (compressed ? 1u : 0u)) return DEC_UNEXPECTED_COMPRESSION_MODE;
+    if (top & 0x40) {
+        uint32_t any = b[0] & 0x3fffffffu;
+        for (int j = 1; j < nwords; j++) any |= b[j];
+        return any ? DEC_UNEXPECTED_INFORMATION : DEC_OK;
+    }
+    if (top & 0x20) {
+        if (!compressed) return DEC_UNEXPECTED_INFORMATION;
+        greatest = true;
+    }
+    b[0] &= 0x1fffffffu;
+    return -1;
+}
+
+// words of coordinate k (48-byte chunk k) of a wire record in little-endian order
+PA_DEV void chunk(uint32_t w[12], const uint32_t* b, int k) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) w[11 - j] = b[12 * k + j];
+}
+
+template <class F>
+PA_DEV void aff_zero(Aff<F>& a) {
+    zero(a.x);
+    one(a.y);
+    a.inf = true;
+}
+
+// G1 / G2 decode of one record; returns the status
+template <int G, bool COMPRESSED>
+PA_DEV int decode_one(Aff<typename std::conditional<G == 1, Fq, Fq2>::type>& out, const uint8_t* rec, bool checked) {
+    using F = typename std::conditional<G == 1, Fq, Fq2>::type;
+    constexpr int coords = (G == 1 ? 1 : 2) * (COMPRESSED ? 1 : 2);
+    constexpr int nwords = 12 * coords;
+    uint32_t b[nwords];
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(rec);
+#pragma unroll
+    for (int j = 0; j < nwords; j++) b[j] = __builtin_bswap32(s[j]);
+    bool greatest;
+    int st = check_flags(b, nwords, COMPRESSED, greatest);
+    aff_zero(out);
+    if (st >= 0) return st;
+    uint32_t w[12];
+    F x, y;
+    if constexpr (G == 1) {
+        chunk(w, b, 0);
+        if (!from_repr(x, w)) return DEC_X_C0;
+        if (!COMPRESSED) {
+            chunk(w, b, 1);
+            if (!from_repr(y, w)) return DEC_Y_C0;
+        }
+    } else {
+        // wire order x.c1, x.c0[, y.c1, y.c0]; the reference decodes c0 first
+        chunk(w, b, 1);
+        if (!from_repr(x.c0, w)) return DEC_X_C0;
+        chunk(w, b, 0);
+        if (!from_repr(x.c1, w)) return DEC_X_C1;
+        if (!COMPRESSED) {
+            chunk(w, b, 3);
+            if (!from_repr(y.c0, w)) return DEC_Y_C0;
+            chunk(w, b, 2);
+            if (!from_repr(y.c1, w)) return DEC_Y_C1;
+        }
+    }
+    Aff<F> a;
+    if (COMPRESSED) {
+        if (!point_from_x(a, x, greatest)) return DEC_NOT_ON_CURVE;
+    } else {
+        a.x = x;
+        a.y = y;
+        a.inf = false;
+        if (checked && !on_curve(a)) return DEC_NOT_ON_CURVE;
+    }
+    if (checked && !in_subgroup(a)) return DEC_NOT_IN_SUBGROUP;
+    out = a;
+    return DEC_OK;
+}
+
+template <int G, bool COMPRESSED>
+__global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ enc, size_t n, int checked,
+                                               uint64_t* __restrict__ out, uint8_t* __restrict__ status) {
+    using F = typename std::conditional<G == 1, Fq, Fq2>::type;
+    constexpr int size = (G == 1 ? 48 : 96) * (COMPRESSED ? 1 : 2);
+    constexpr int W = FieldWords<F>::n;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Aff<F> a;
+    const int st = decode_one<G, COMPRESSED>(a, enc + (size_t)size * i, checked != 0);
+    store_aff(out + (size_t)(2 * W + 1) * i, a);
+    status[i] = (uint8_t)st;
+}
+
+// EncodedPoint::from_affine
+template <int G, bool COMPRESSED>
+__global__ void __launch_bounds__(64) k_encode(const uint64_t* __restrict__ in, size_t n, uint8_t* __restrict__ enc) {
+    using F = typename std::conditional<G == 1, Fq, Fq2>::type;
+    constexpr int size = (G == 1 ? 48 : 96) * (COMPRESSED ? 1 : 2);
+    constexpr int W = FieldWords<F>::n;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Aff<F> a;
+    load_aff(a, in + (size_t)(2 * W + 1) * i);
+    uint8_t* rec = enc + (size_t)size * i;
+    uint32_t* d = reinterpret_cast<uint32_t*>(rec);
+    if (a.inf) {
+        for (int j = 0; j < size / 4; j++) d[j] = 0;
+        d[0] = __builtin_bswap32((COMPRESSED ? 0x80u : 0u) << 24 | 0x40u << 24);
+        return;
+    }
+    uint32_t w[12];
+    if constexpr (G == 1) {
+        fq_canonical(w, a.x);
+        write_be48(rec, w);
+        if (!COMPRESSED) {
+            fq_canonical(w, a.y);
+            write_be48(rec + 48, w);
+        }
+    } else {
+        fq_canonical(w, a.x.c1);
+        write_be48(rec, w);
+        fq_canonical(w, a.x.c0);
+        write_be48(rec + 48, w);
+        if (!COMPRESSED) {
+            fq_canonical(w, a.y.c1);
+            write_be48(rec + 96, w);
+            fq_canonical(w, a.y.c0);
+            write_be48(rec + 144, w);
+        }
+    }
+    if (COMPRESSED) {
+        F negy;
+        neg(negy, a.y);
+        uint32_t flags = 0x80u;
+        if (cmp(a.y, negy) > 0) flags |= 0x20u;  // ec.rs:861-864
+        rec[0] |= (uint8_t)flags;
+    }
+}
+
+template <class F>
+__global__ void __launch_bounds__(64) k_sqrt(const uint64_t* __restrict__ in, size_t n, uint64_t* __restrict__ out,
+                                             uint8_t* __restrict__ ok) {
+    constexpr int W = FieldWords<F>::n;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    F a, r;
+    load(a, in + (size_t)W * i);
+    const bool s = sqrt(r, a);
+    if (!s) zero(r);
+    store(out + (size_t)W * i, r);
+    ok[i] = s ? 1 : 0;
+}
+
+unsigned blocks_for(size_t n) { return (unsigned)((n + 63) / 64); }
+
+}  // namespace
+
+hipError_t launch_decode(int group, int compressed, int checked, const uint8_t* enc, size_t n, uint64_t* out,
+                         uint8_t* status, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const unsigned b = blocks_for(n);
+    if (group == 1 && compressed) k_decode<1, true><<<b, 64, 0, stream>>>(enc, n, checked, out, status);
+    else if (group == 1) k_decode<1, false><<<b, 64, 0, stream>>>(enc, n, checked, out, status);
+    else if (compressed) k_decode<2, true><<<b, 64, 0, stream>>>(enc, n, checked, out, status);
+    else k_decode<2, false><<<b, 64, 0, stream>>>(enc, n, checked, out, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode(int group, int compressed, const uint64_t* in, size_t n, uint8_t* enc, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const unsigned b = blocks_for(n);
+    if (group == 1 && compressed) k_encode<1, true><<<b, 64, 0, stream>>>(in, n, enc);
+    else if (group == 1) k_encode<1, false><<<b, 64, 0, stream>>>(in, n, enc);
+    else if (compressed) k_encode<2, true><<<b, 64, 0, stream>>>(in, n, enc);
+    else k_encode<2, false><<<b, 64, 0, stream>>>(in, n, enc);
+    return hipGetLastError();
+}
+
+hipError_t launch_sqrt(int degree, const uint64_t* in, size_t n, uint64_t* out, uint8_t* ok, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const unsigned b = blocks_for(n);
+    if (degree == 1) k_sqrt<Fq><<<b, 64, 0, stream>>>(in, n, out, ok);
+    else k_sqrt<Fq2><<<b, 64, 0, stream>>>(in, n, out, ok);
+    return hipGetLastError();
+}
+
+}  // namespace pa

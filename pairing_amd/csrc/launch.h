@@ -62,6 +62,13 @@ hipError_t launch_final_exp_gen2(const uint64_t* in, uint64_t* out, uint8_t* ok,
 // out[0] = prod_i in[i] (Fq12), in-place tree reduction over `work` (n entries, clobbered)
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
 
+// point decoding / encoding (group 1 or 2; records in the wire format) and
+// square roots (degree 1: Fq, 2: Fq2), kernels_decode.hip
+hipError_t launch_decode(int group, int compressed, int checked, const uint8_t* enc, size_t n, uint64_t* out,
+                         uint8_t* status, hipStream_t stream);
+hipError_t launch_encode(int group, int compressed, const uint64_t* in, size_t n, uint8_t* enc, hipStream_t stream);
+hipError_t launch_sqrt(int degree, const uint64_t* in, size_t n, uint64_t* out, uint8_t* ok, hipStream_t stream);
+
 // G1 batch_normalization in place (n Jacobian records of 18 u64)
 hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream);
 // fixed-base comb: table (g1_comb_table_words() u64) built from `base` using

@@ -120,7 +120,7 @@ PA_NOINLINE void cyc_sqr2(Fq6& z, const Fq6& x, bool r) {
     sel(own[2], r, x.c2, x.c0);
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        Fq2 F, X, Y, s, t, xy, op1, op2, prod, other, a, b;
+        Fq2 F, X, Y, s, t, op1, op2, prod, other, a, b;
         pswap(F, E[k]);
         // component (x, y): A = (a0, b1) and C = (a1, b2) have x on role 0; B = (b0, a2) has x on role 1
         const bool x_on_role1 = (k == 1);
@@ -212,7 +212,7 @@ PA_NOINLINE void doubling_step2(EllCoeff& out, Jac<Fq2>& R, bool r) {
     sel(tmp1, r, o1, s1);   // y^2
     sel(zsq, r, s2, o2);    // z^2
     sel(zy2, r, o2, s2);    // (z+y)^2
-    Fq2 tmp4, b1, b2, u1, u2;
+    Fq2 tmp4, b1, b2, u1;
     dbl(tmp4, tmp0);
     add(tmp4, tmp4, tmp0);  // 3 x^2
     sel(b1, r, tmp1, tmp4);

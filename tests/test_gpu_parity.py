@@ -152,6 +152,56 @@ def test_multi_miller_loop_is_product(gpu, oracle, pairs):
     np.testing.assert_array_equal(gpu.multi_miller_loop(p[:0], prep[:0]), fq12_one()[0])
 
 
+def test_multi_miller_loop_affine_is_product(gpu, oracle, pairs, lanes):
+    """prepare fused on device, then the product tree (mod.rs:40-102)"""
+    p, q = pairs
+    exp = oracle.miller_loop(p[:41], oracle.g2_prepare(q[:41], NT))   # includes infinity pairs 5, 17, 40
+    np.testing.assert_array_equal(gpu.multi_miller_loop_affine(p[:41], q[:41]), exp)
+    np.testing.assert_array_equal(gpu.multi_miller_loop_affine(p[:0], q[:0]), fq12_one()[0])
+
+
+def _neg_g1(aff):
+    out = aff.copy()
+    for k in range(out.shape[0]):
+        y = sum(int(w) << (64 * i) for i, w in enumerate(out[k, 6:12])) * pow(RMONT, -1, Q) % Q
+        out[k, 6:12] = limbs((Q - y) % Q * RMONT % Q)
+    return out
+
+
+def test_multi_pairing_batch_verification(gpu, oracle):
+    """e(aP, Q) * e(-P, aQ) == 1 (the verifier shape, engine.rs:50-92 product
+    semantics) and multi_pairing == final_exponentiation(product)"""
+    g = rng(35)
+    a = random_scalars(g, 4)
+    s = random_scalars(g, 4)
+    t = random_scalars(g, 4)
+    for k in range(4):
+        sp = oracle.g1_mul_generator(s[k:k + 1])
+        tq = oracle.g2_mul_generator(t[k:k + 1])
+        sa = limbs(sum(int(w) << (64 * i) for i, w in enumerate(s[k])) *
+                   sum(int(w) << (64 * i) for i, w in enumerate(a[k])) % R_ORDER, 4)
+        ta = limbs(sum(int(w) << (64 * i) for i, w in enumerate(t[k])) *
+                   sum(int(w) << (64 * i) for i, w in enumerate(a[k])) % R_ORDER, 4)
+        p = np.concatenate([oracle.g1_mul_generator(np.array([sa], np.uint64)), _neg_g1(sp)])
+        q = np.concatenate([tq, oracle.g2_mul_generator(np.array([ta], np.uint64))])
+        out, ok = gpu.multi_pairing(p, q)
+        assert ok
+        np.testing.assert_array_equal(out, fq12_one()[0])
+    p = oracle.g1_mul_generator(s)
+    q = oracle.g2_mul_generator(t)
+    exp, eok = oracle.final_exponentiation(oracle.miller_loop(p, oracle.g2_prepare(q))[None, :].copy())
+    out, ok = gpu.multi_pairing(p, q)
+    assert ok and eok[0]
+    np.testing.assert_array_equal(out, exp[0])
+
+
+def test_pairing_multi_gpu_entry(gpu, oracle, pairs):
+    p, q = pairs
+    np.testing.assert_array_equal(gpu.pairing_multi_gpu(p, q, 1), gpu.pairing(p, q))
+    with pytest.raises(gpu.PairingError):
+        gpu.pairing_multi_gpu(p, q, gpu.device_count() + 1)
+
+
 def test_final_exponentiation_matches_oracle(gpu, oracle, pairs, lanes):
     p, q = pairs
     f = oracle.miller_loop_batch(p[:32], oracle.g2_prepare(q[:32], NT), NT)
