@@ -30,11 +30,14 @@ def block(chains, prods):
     """prods: list of (chain, x_expr, y_expr, y_is_sgpr) for one asm statement."""
     text = []
     used = sorted({c for c, *_ in prods})
-    # outputs: acc_c (+v 64), ov_c (+v), carry_c (=&s 64)
+    # outputs: acc_c (+&v 64), ov_c (+&v), carry_c (=&s 64).  The accumulators
+    # are early-clobber: they are written before later inputs are read, and
+    # without '&' the compiler may give an input that holds the same value
+    # (e.g. a zero word of a constant operand) the accumulator's register.
     out_list = []
     for c in used:
-        out_list.append(('"+v"', "acc%s" % chains[c]))
-        out_list.append(('"+v"', "ov%s" % chains[c]))
+        out_list.append(('"+&v"', "acc%s" % chains[c]))
+        out_list.append(('"+&v"', "ov%s" % chains[c]))
     for c in used:
         out_list.append(('"=&s"', "cf%s" % chains[c]))
     in_list = []
