@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 16, help="pairings per GPU per step")
-    ap.add_argument("--workload", choices=["pairing", "fq_mul", "wnaf"], default="pairing")
+    ap.add_argument("--workload", choices=["pairing", "fq_mul", "wnaf", "decode"], default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -98,6 +98,28 @@ def cpu_baseline_pairing(p, q, seconds):
     return {"value": n / wall, "unit": "pairings/s", "cores": threads, "kind": "port",
             "sample": "%d pairings of the same synthetic batch, C restatement of the reference "
                       "(oracle/), OpenMP over pairs, %.1f s wall" % (n, wall)}
+
+
+def cpu_baseline_decode(enc1, enc2, seconds):
+    """The reference's into_affine for compressed G2 + G1 records, restated in C (OpenMP over records)."""
+    from oracle import binding as oracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))
+    t0 = time.perf_counter()
+    oracle.decode(2, enc2[:threads], True, True, threads)
+    oracle.decode(1, enc1[:threads], True, True, threads)
+    per = max(time.perf_counter() - t0, 1e-4)
+    n = int(max(threads, min(len(enc1), threads * seconds / per)))
+    t0 = time.perf_counter()
+    oracle.decode(2, enc2[:n], True, True, threads)
+    oracle.decode(1, enc1[:n], True, True, threads)
+    wall = time.perf_counter() - t0
+    return {"value": n / wall, "unit": "point pairs/s", "cores": threads, "kind": "port",
+            "sample": "%d G2+G1 compressed records of the same batch, C restatement of the reference "
+                      "(oracle/), OpenMP over records, %.1f s wall" % (n, wall)}
 
 
 def cpu_baseline_wnaf(base, scalars, seconds):
@@ -198,6 +220,28 @@ def main():
             pdev.g1_batch_normalization(out, stream)
             if timed:
                 ev[2].record(stream)
+    elif args.workload == "decode":
+        # SURVEY.md §8 f rank 1: the verifier's front end -- compressed G1 and G2
+        # records decoded with the on-curve (square root) and subgroup (r*P) checks
+        p_np, q_np = make_pairs(n, rank)
+        enc1_np = pairing_amd.g1_encode(p_np, True)
+        enc2_np = pairing_amd.g2_encode(q_np, True)
+        enc1 = torch.from_numpy(enc1_np).to(dev)
+        enc2 = torch.from_numpy(enc2_np).to(dev)
+        out1 = pdev.empty_records(n, 13, dev)
+        out2 = pdev.empty_records(n, 25, dev)
+        st1 = torch.empty(n, dtype=torch.uint8, device=dev)
+        st2 = torch.empty(n, dtype=torch.uint8, device=dev)
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            pdev.decode(2, enc2, True, True, out2, st2, stream)
+            if timed:
+                ev[1].record(stream)
+            pdev.decode(1, enc1, True, True, out1, st1, stream)
+            if timed:
+                ev[2].record(stream)
     else:
         g = np.random.default_rng(rank)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -225,7 +269,7 @@ def main():
         # per-kernel durations from HIP events on the launch stream
         torch.cuda.synchronize()
         k_ms["a"].append(ev[0].elapsed_time(ev[1]))
-        if args.workload in ("pairing", "wnaf"):
+        if args.workload in ("pairing", "wnaf", "decode"):
             k_ms["b"].append(ev[1].elapsed_time(ev[2]))
     barrier()
     elapsed = time.perf_counter() - t0
@@ -257,6 +301,15 @@ def main():
             config = {"workload": "Wnaf::base(g, 2^18).scalar(s_i) then G1::batch_normalization",
                       "batch_per_gpu": n, "global_batch": n * ws,
                       "kernel_ms": {"table+fixed_base_mul": round(mul_ms, 3), "batch_normalize": round(norm_ms, 3)}}
+        elif args.workload == "decode":
+            g2_ms, g1_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
+            dom_name, dom_ms, dom_bytes = ("g2_decode_compressed", g2_ms, 96 + 200 + 1) if g2_ms >= g1_ms else \
+                ("g1_decode_compressed", g1_ms, 48 + 104 + 1)
+            value = ws * n * args.steps / elapsed
+            metric, unit = "compressed G1+G2 point pairs decoded (checked) per second at batch 2^16", "point pairs/s"
+            config = {"workload": "G2Compressed + G1Compressed ::into_affine (sqrt + on-curve + r*P subgroup check)",
+                      "batch_per_gpu": n, "global_batch": n * ws,
+                      "kernel_ms": {"g2_decode": round(g2_ms, 3), "g1_decode": round(g1_ms, 3)}}
         else:
             dom_name, dom_ms, dom_bytes = "fq_mul_batch", float(np.mean(k_ms["a"])), 144
             value = ws * n * args.steps / elapsed
@@ -293,11 +346,15 @@ def main():
                 cpu = cpu_baseline_pairing(p_np, q_np, args.cpu_seconds)
             elif args.workload == "wnaf":
                 cpu = cpu_baseline_wnaf(base_np, s_np, args.cpu_seconds)
+            elif args.workload == "decode":
+                cpu = cpu_baseline_decode(enc1_np, enc2_np, args.cpu_seconds)
             else:
                 cpu = cpu_baseline_fq_mul(a_np, b_np, args.cpu_seconds)
         line = {"metric": metric, "value": value, "unit": unit, "n_gpus": ws, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "u32 (384-bit Montgomery, 12 x u32 limbs)",
+                "scaling": "weak", "vs_baseline": None,
+                "dtype": "u32 (14 x 28-bit lazy Montgomery limbs)" if args.workload == "pairing"
+                else "u32 (384-bit Montgomery, 12 x u32 limbs)",
                 "data": "synthetic (seeded random points k*G)", "config": config,
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)

@@ -9,9 +9,9 @@ the C ABI of include/pairing_amd.h.
 Two layers:
   * batch functions over numpy arrays in the ABI layout (this module), e.g.
     `pairing(p, q)` for n independent pairs;
-  * `pairing_amd.engine`: a mirror of the reference's trait surface
-    (`Bls12.pairing`, `Bls12.miller_loop`, `Bls12.final_exponentiation`,
-    `G1Affine.prepare`, ...) so code written against the crate reads the same.
+  * include/pairing_amd.hpp: the C++ mirror of the reference's trait surface
+    (`Bls12::pairing`, `Bls12::miller_loop`, `G1Affine::prepare`,
+    `G1Compressed::into_affine`, `Wnaf`, ...) over the same C ABI.
 Device-resident entry points for torch tensors live in `pairing_amd.device`.
 """
 import numpy as np

@@ -72,3 +72,19 @@ def g1_fixed_base_mul(table, scalars, out, stream=None):
 
 def g1_batch_normalization(v, stream=None):
     call("pa_g1_batch_normalization_device", _dptr(v, W_G1, "v"), v.shape[0], _stream_ptr(stream))
+
+
+def decode(group, enc, compressed, checked, out, status, stream=None):
+    """EncodedPoint::into_affine[_unchecked] over records resident in HBM:
+    enc (n, 48|96|192) uint8, out (n, 13|25) int64 affine records, status (n,) uint8."""
+    size = (48 if group == 1 else 96) * (1 if compressed else 2)
+    if not enc.is_cuda or not enc.is_contiguous() or enc.dtype != torch.uint8 or enc.dim() != 2 \
+            or enc.shape[1] != size:
+        raise ValueError("enc must be a contiguous (n, %d) uint8 CUDA tensor" % size)
+    if not status.is_cuda or status.dtype != torch.uint8 or status.numel() != enc.shape[0]:
+        raise ValueError("status must be an (n,) uint8 CUDA tensor")
+    width = W_G1A if group == 1 else W_G2A
+    call("pa_g%d_decode_batch_device" % group, ctypes.c_void_p(enc.data_ptr()), enc.shape[0],
+         int(bool(compressed)), int(bool(checked)), _dptr(out, width, "out"), ctypes.c_void_p(status.data_ptr()),
+         _stream_ptr(stream))
+
