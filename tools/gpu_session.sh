@@ -23,8 +23,8 @@ run() {  # name limit cmd...
 for step in "$@"; do
     case $step in
         valu) run valu 120 ./tools/valu_rates ;;
-        tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
-        alltests) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+        alltests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         bench1) run bench_word32 600 env PA_PAIRING_KERNEL=1 python bench.py --no-cpu-baseline ;;
