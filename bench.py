@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 16, help="pairings per GPU per step")
-    ap.add_argument("--workload", choices=["pairing", "fq_mul", "wnaf", "decode"], default="pairing")
+    ap.add_argument("--workload", choices=["pairing", "fq_mul", "fr_mul", "wnaf", "decode", "msm"], default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -150,6 +150,42 @@ def cpu_baseline_fq_mul(a, b, seconds):
             "sample": "%d Fq::mul_assign, C restatement (oracle/), 1 thread" % n}
 
 
+def cpu_baseline_fr_mul(a, b):
+    from oracle import binding as oracle
+    n = min(len(a), 1 << 20)
+    t0 = time.perf_counter()
+    oracle.fr_mul(np.ascontiguousarray(a[:n]), np.ascontiguousarray(b[:n]))
+    wall = time.perf_counter() - t0
+    return {"value": n / wall, "unit": "muls/s", "cores": 1, "kind": "port",
+            "sample": "%d Fr::mul_assign, C restatement (oracle/), 1 thread" % n}
+
+
+def cpu_baseline_msm(base, k, s, seconds):
+    """The reference-style sum of CurveAffine::mul terms (C restatement), OpenMP over terms,
+    on a bounded prefix of the same bases (k_i * G, made by the oracle)."""
+    from oracle import binding as oracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))
+    m = 64 * threads
+    pts = oracle.g1_mul_generator(np.ascontiguousarray(k[:m]), threads)
+    t0 = time.perf_counter()
+    oracle.g1_multiexp(pts, np.ascontiguousarray(s[:m]), threads)
+    per = max(time.perf_counter() - t0, 1e-4) / m
+    m2 = int(max(m, min(len(k), 0.5 * seconds / per)))
+    if m2 > m:
+        pts = oracle.g1_mul_generator(np.ascontiguousarray(k[:m2]), threads)
+        m = m2
+    t0 = time.perf_counter()
+    oracle.g1_multiexp(pts, np.ascontiguousarray(s[:m]), threads)
+    wall = time.perf_counter() - t0
+    return {"value": m / wall, "unit": "terms/s", "cores": threads, "kind": "port",
+            "sample": "%d terms: CurveAffine::mul per term + add_assign, C restatement (oracle/), "
+                      "OpenMP over terms, %.1f s wall" % (m, wall)}
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -242,6 +278,59 @@ def main():
             pdev.decode(1, enc1, True, True, out1, st1, stream)
             if timed:
                 ev[2].record(stream)
+    elif args.workload == "msm":
+        # SURVEY.md §8 f rank 3: one G1 multi-scalar multiplication of 2^20 terms
+        # (the prover's multiexp).  Distinct bases k_i*G made on the device
+        # (fixed-base comb + batch_normalization), random 255-bit scalars.
+        n = args.batch if args.batch != (1 << 16) else (1 << 20)
+        d = np.load(os.path.join(ROOT, "tests", "golden", "bench_points.npz"))
+        base_np = np.zeros((1, 18), np.uint64)
+        base_np[0, :12] = d["g1"][0, :12]
+        base_np[0, 12:18] = np.array([0x760900000002fffd, 0xebf4000bc40c0002, 0x5f48985753c758ba,
+                                      0x77ce585370525745, 0x5c071a97a256ec6d, 0x15f65ec3fa80e493], np.uint64)
+        g = np.random.default_rng(1234 + rank)
+        k_np = g.integers(0, 1 << 63, size=(n, 4), dtype=np.uint64)
+        s_np = g.integers(0, 1 << 63, size=(n, 4), dtype=np.uint64)
+        k_np[:, 0] ^= np.arange(n, dtype=np.uint64)            # distinct k_i
+        k_np[:, 3] &= np.uint64(0x0fffffffffffffff)            # < r
+        s_np[:, 3] &= np.uint64(0x0fffffffffffffff)
+        base = torch.from_numpy(base_np.view(np.int64)).to(dev)
+        kk = torch.from_numpy(k_np.view(np.int64)).to(dev)
+        jac = pdev.empty_records(n, 18, dev)
+        table, _ = pdev.g1_fixed_base_table(base, stream)
+        pdev.g1_fixed_base_mul(table, kk, jac, stream)
+        pdev.g1_batch_normalization(jac, stream)
+        bases = torch.zeros((n, 13), dtype=torch.int64, device=dev)
+        bases[:, :12] = jac[:, :12]
+        del jac, table
+        scal = torch.from_numpy(s_np.view(np.int64)).to(dev)
+        msm_out = pdev.empty_records(1, 18, dev)
+        msm_ws = pdev.multiexp_workspace(1, n, dev)
+        torch.cuda.synchronize()
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            pdev.multiexp(1, bases, scal, msm_out, msm_ws, stream)
+            if timed:
+                ev[1].record(stream)
+    elif args.workload == "fr_mul":
+        g = np.random.default_rng(rank)
+        n = args.batch if args.batch != (1 << 16) else (1 << 20)
+        a_np = g.integers(0, 1 << 63, size=(4096, 4), dtype=np.uint64)[np.arange(n) % 4096]
+        b_np = g.integers(0, 1 << 63, size=(4096, 4), dtype=np.uint64)[(np.arange(n) * 7 + 3) % 4096]
+        a_np[:, 3] &= np.uint64(0x0fffffffffffffff)
+        b_np[:, 3] &= np.uint64(0x0fffffffffffffff)
+        a = torch.from_numpy(np.ascontiguousarray(a_np).view(np.int64)).to(dev)
+        b = torch.from_numpy(np.ascontiguousarray(b_np).view(np.int64)).to(dev)
+        out = pdev.empty_records(n, 4, dev)
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            pdev.fr_mul(a, b, out, stream)
+            if timed:
+                ev[1].record(stream)
     else:
         g = np.random.default_rng(rank)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -310,6 +399,21 @@ def main():
             config = {"workload": "G2Compressed + G1Compressed ::into_affine (sqrt + on-curve + r*P subgroup check)",
                       "batch_per_gpu": n, "global_batch": n * ws,
                       "kernel_ms": {"g2_decode": round(g2_ms, 3), "g1_decode": round(g1_ms, 3)}}
+        elif args.workload == "msm":
+            dom_name, dom_ms = "g1_multiexp", float(np.mean(k_ms["a"]))
+            # per term: W = ceil(257/16) = 17 windows x (104 B base gather + 8 B sort key/value)
+            # + 32 B scalar read; the buckets' own traffic is per bucket, not per term
+            dom_bytes = 17 * (104 + 8) + 32
+            value = ws * n * args.steps / elapsed
+            metric, unit = "G1 multi-scalar multiplication terms per second at n = 2^20", "terms/s"
+            config = {"workload": "one G1 MSM sum_i s_i P_i over 2^20 distinct affine bases (Pippenger, c = 16)",
+                      "batch_per_gpu": n, "global_batch": n * ws, "kernel_ms": {"multiexp": round(dom_ms, 3)}}
+        elif args.workload == "fr_mul":
+            dom_name, dom_ms, dom_bytes = "fr_mul_batch", float(np.mean(k_ms["a"])), 96
+            value = ws * n * args.steps / elapsed
+            metric, unit = "Fr::mul_assign per second at batch 2^20", "muls/s"
+            config = {"workload": "2^20 Fr Montgomery multiplications (AoS 4x u64)", "batch_per_gpu": n,
+                      "global_batch": n * ws}
         else:
             dom_name, dom_ms, dom_bytes = "fq_mul_batch", float(np.mean(k_ms["a"])), 144
             value = ws * n * args.steps / elapsed
@@ -348,12 +452,17 @@ def main():
                 cpu = cpu_baseline_wnaf(base_np, s_np, args.cpu_seconds)
             elif args.workload == "decode":
                 cpu = cpu_baseline_decode(enc1_np, enc2_np, args.cpu_seconds)
+            elif args.workload == "msm":
+                cpu = cpu_baseline_msm(base_np, k_np, s_np, args.cpu_seconds)
+            elif args.workload == "fr_mul":
+                cpu = cpu_baseline_fr_mul(a_np, b_np)
             else:
                 cpu = cpu_baseline_fq_mul(a_np, b_np, args.cpu_seconds)
         line = {"metric": metric, "value": value, "unit": unit, "n_gpus": ws, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None,
                 "dtype": "u32 (14 x 28-bit lazy Montgomery limbs)" if args.workload == "pairing"
+                else "u32 (256-bit Montgomery, 8 x u32 limbs)" if args.workload == "fr_mul"
                 else "u32 (384-bit Montgomery, 12 x u32 limbs)",
                 "data": "synthetic (seeded random points k*G)", "config": config,
                 "roofline": roof, "cpu_baseline": cpu}

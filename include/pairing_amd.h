@@ -59,7 +59,8 @@ typedef struct { uint64_t l[6]; } pa_fq;
 typedef struct { pa_fq c0, c1; } pa_fq2;
 typedef struct { pa_fq2 c0, c1, c2; } pa_fq6;
 typedef struct { pa_fq6 c0, c1; } pa_fq12;
-typedef struct { uint64_t l[4]; } pa_fr_repr;
+typedef struct { uint64_t l[4]; } pa_fr_repr;   /* canonical scalar, fr.rs:58 */
+typedef struct { uint64_t l[4]; } pa_fr;        /* Montgomery form (R = 2^256), < r, fr.rs:247 */
 typedef struct { pa_fq x, y; uint8_t infinity; uint8_t _pad[7]; } pa_g1_affine;
 typedef struct { pa_fq2 x, y; uint8_t infinity; uint8_t _pad[7]; } pa_g2_affine;
 typedef struct { pa_fq x, y, z; } pa_g1;
@@ -174,6 +175,48 @@ int pa_multi_pairing(const pa_g1_affine *p, const pa_g2_affine *q, size_t n, pa_
  * shards, one host thread per device); ndev <= pa_device_count. */
 int pa_pairing_batch_multi_gpu(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n, int ndev);
 
+/* ---- variable-base scalar multiplication and MSM (SURVEY.md §8 f, rank 3) ----
+ * Scalars are FrRepr (canonical 4 x u64 LE; any 256-bit value, as the
+ * reference's BitIterator takes).  Per-item outputs are Jacobian and equal
+ * the reference's X, Y, Z words bit for bit. */
+/* CurveAffine::mul, ec.rs:174-177 (mul_bits ec.rs:88-95): out[i] = s[i] * p[i] */
+int pa_g1_affine_mul_batch(const pa_g1_affine *p, const pa_fr_repr *s, pa_g1 *out, size_t n);
+int pa_g2_affine_mul_batch(const pa_g2_affine *p, const pa_fr_repr *s, pa_g2 *out, size_t n);
+/* CurveProjective::mul_assign, ec.rs:534-553: out[i] = s[i] * p[i] (p Jacobian) */
+int pa_g1_mul_assign_batch(const pa_g1 *p, const pa_fr_repr *s, pa_g1 *out, size_t n);
+int pa_g2_mul_assign_batch(const pa_g2 *p, const pa_fr_repr *s, pa_g2 *out, size_t n);
+/* Multi-scalar multiplication: *out = sum_i s[i] * bases[i] (Pippenger buckets
+ * on the device), the prover's multiexp over CurveAffine::mul + add_assign.
+ * The Jacobian result is equal as a point (PartialEq, ec.rs:45-85) to the
+ * reference's sum; n = 0 gives the zero point.  n < 2^31. */
+int pa_g1_multiexp(const pa_g1_affine *bases, const pa_fr_repr *s, size_t n, pa_g1 *out);
+int pa_g2_multiexp(const pa_g2_affine *bases, const pa_fr_repr *s, size_t n, pa_g2 *out);
+/* device workspace bytes for pa_g{1,2}_multiexp_device (group 1 or 2) */
+size_t pa_multiexp_workspace_bytes(int group, size_t n);
+
+/* ---- scalar field Fr (src/bls12_381/fr.rs; SURVEY.md §8 f, rank 4) ----
+ * pa_fr = 4 x u64 LE limbs, Montgomery form with R = 2^256, < r: the
+ * reference's `Fr` in memory.  Every result is canonical, so it equals the
+ * reference's bit for bit. */
+int pa_fr_mul_batch(const pa_fr *a, const pa_fr *b, pa_fr *out, size_t n);  /* mul_assign fr.rs:438-465 */
+int pa_fr_square_batch(const pa_fr *a, pa_fr *out, size_t n);              /* square fr.rs:467-500 */
+int pa_fr_add_batch(const pa_fr *a, const pa_fr *b, pa_fr *out, size_t n);  /* add_assign fr.rs:341-348 */
+int pa_fr_sub_batch(const pa_fr *a, const pa_fr *b, pa_fr *out, size_t n);  /* sub_assign fr.rs:359-367 */
+int pa_fr_double_batch(const pa_fr *a, pa_fr *out, size_t n);              /* double fr.rs:350-357 */
+int pa_fr_negate_batch(const pa_fr *a, pa_fr *out, size_t n);              /* negate fr.rs:369-375 */
+/* inverse fr.rs:377-431; ok[i] = 0 (None) for zero */
+int pa_fr_inverse_batch(const pa_fr *a, pa_fr *out, uint8_t *ok, size_t n);
+/* PrimeField::from_repr fr.rs:279-288; ok[i] = 0 = Err(NotInField) when repr >= r (out[i] = 0) */
+int pa_fr_from_repr_batch(const pa_fr_repr *repr, pa_fr *out, uint8_t *ok, size_t n);
+/* PrimeField::into_repr fr.rs:290-303 */
+int pa_fr_into_repr_batch(const pa_fr *a, pa_fr_repr *out, size_t n);
+/* Field::pow lib.rs:306-324 with one exponent (exp_words u64, LE) for every element */
+int pa_fr_pow_batch(const pa_fr *a, const uint64_t *exp, size_t exp_words, pa_fr *out, size_t n);
+/* SqrtField::legendre fr.rs:575-590: out[i] = 0 Zero, 1 QuadraticResidue, -1 QuadraticNonResidue */
+int pa_fr_legendre_batch(const pa_fr *a, int8_t *out, size_t n);
+/* SqrtField::sqrt fr.rs:592-646 (the reference's Tonelli-Shanks root); ok[i] = 0 (None) for a non-residue */
+int pa_fr_sqrt_batch(const pa_fr *a, pa_fr *out, uint8_t *ok, size_t n);
+
 /* ---- device-resident variants (pointers are device memory) ---- */
 int pa_g1_decode_batch_device(const uint8_t *enc, size_t n, int compressed, int checked, pa_g1_affine *out,
                               uint8_t *status, void *stream);
@@ -187,6 +230,11 @@ int pa_g1_fixed_base_table_device(const pa_g1 *base, uint64_t *table, uint64_t *
 int pa_g1_fixed_base_mul_device(const uint64_t *table, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
                                 void *stream);
 int pa_fq_mul_batch_device(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n, void *stream);
+int pa_fr_mul_batch_device(const pa_fr *a, const pa_fr *b, pa_fr *out, size_t n, void *stream);
+int pa_g1_multiexp_device(const pa_g1_affine *bases, const pa_fr_repr *s, size_t n, pa_g1 *out, void *workspace,
+                          size_t workspace_bytes, void *stream);
+int pa_g2_multiexp_device(const pa_g2_affine *bases, const pa_fr_repr *s, size_t n, pa_g2 *out, void *workspace,
+                          size_t workspace_bytes, void *stream);
 int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
                                       void *stream);
 int pa_final_exponentiation_batch_device(const pa_fq12 *in, pa_fq12 *out, uint8_t *ok, size_t n, void *stream);

@@ -99,6 +99,23 @@ def _declare(L):
         "o_g1_decode_batch": [_P, _N, _I, _I, _P, _P, _I],
         "o_g2_decode_batch": [_P, _N, _I, _I, _P, _P, _I],
         "o_fq_sqrt_batch": [_P, _N, _P, _P],
+        "o_fr_mul_batch": [_P, _P, _P, _N],
+        "o_fr_square_batch": [_P, _P, _N],
+        "o_fr_add_batch": [_P, _P, _P, _N],
+        "o_fr_sub_batch": [_P, _P, _P, _N],
+        "o_fr_double_batch": [_P, _P, _N],
+        "o_fr_negate_batch": [_P, _P, _N],
+        "o_fr_inverse_batch": [_P, _P, _P, _N],
+        "o_fr_from_repr_batch": [_P, _N, _P, _P],
+        "o_fr_into_repr_batch": [_P, _N, _P],
+        "o_fr_pow_batch": [_P, _P, _N, _P, _N],
+        "o_fr_legendre_batch": [_P, _P, _N],
+        "o_fr_sqrt_batch": [_P, _N, _P, _P],
+        "o_fr_constants": [_P, _P, _P],
+        "o_g1_affine_mul_batch": [_P, _P, _N, _P, _I],
+        "o_g2_affine_mul_batch": [_P, _P, _N, _P, _I],
+        "o_g1_multiexp": [_P, _P, _N, _P, _I],
+        "o_g2_multiexp": [_P, _P, _N, _P, _I],
         "o_fq2_sqrt_batch": [_P, _N, _P, _P],
     }
     for name, args in sig.items():
@@ -195,6 +212,68 @@ def fq_into_repr(a):
     o = _out(_n(a), W_FQ); lib().o_fq_into_repr_batch(_p(a), _n(a), _p(o)); return o
 
 
+# ---- Fr (scalar field, fr.rs): (n,4) u64 Montgomery R = 2^256 ----
+W_FR = 4
+
+
+def fr_mul(a, b):
+    o = _out(_n(a), W_FR); lib().o_fr_mul_batch(_p(a), _p(b), _p(o), _n(a)); return o
+
+
+def fr_square(a):
+    o = _out(_n(a), W_FR); lib().o_fr_square_batch(_p(a), _p(o), _n(a)); return o
+
+
+def fr_add(a, b):
+    o = _out(_n(a), W_FR); lib().o_fr_add_batch(_p(a), _p(b), _p(o), _n(a)); return o
+
+
+def fr_sub(a, b):
+    o = _out(_n(a), W_FR); lib().o_fr_sub_batch(_p(a), _p(b), _p(o), _n(a)); return o
+
+
+def fr_double(a):
+    o = _out(_n(a), W_FR); lib().o_fr_double_batch(_p(a), _p(o), _n(a)); return o
+
+
+def fr_negate(a):
+    o = _out(_n(a), W_FR); lib().o_fr_negate_batch(_p(a), _p(o), _n(a)); return o
+
+
+def fr_inverse(a):
+    o = _out(_n(a), W_FR); ok = np.zeros(_n(a), np.uint8)
+    lib().o_fr_inverse_batch(_p(a), _p(o), _p(ok), _n(a)); return o, ok.astype(bool)
+
+
+def fr_from_repr(r):
+    o = _out(_n(r), W_FR); ok = np.zeros(_n(r), np.uint8)
+    lib().o_fr_from_repr_batch(_p(r), _n(r), _p(o), _p(ok)); return o, ok.astype(bool)
+
+
+def fr_into_repr(a):
+    o = _out(_n(a), W_FR); lib().o_fr_into_repr_batch(_p(a), _n(a), _p(o)); return o
+
+
+def fr_pow(a, exp_limbs):
+    e = np.ascontiguousarray(np.asarray(exp_limbs, dtype=np.uint64))
+    o = _out(_n(a), W_FR); lib().o_fr_pow_batch(_p(a), _p(e), e.size, _p(o), _n(a)); return o
+
+
+def fr_legendre(a):
+    o = np.zeros(_n(a), np.int8); lib().o_fr_legendre_batch(_p(a), _p(o), _n(a)); return o
+
+
+def fr_sqrt(a):
+    o = _out(_n(a), W_FR); ok = np.zeros(_n(a), np.uint8)
+    lib().o_fr_sqrt_batch(_p(a), _n(a), _p(o), _p(ok)); return o, ok.astype(bool)
+
+
+def fr_constants():
+    """(modulus, R, root_of_unity) as (4,) u64 arrays (fr.rs:4-56)."""
+    m, r, w = (np.zeros(4, np.uint64) for _ in range(3))
+    lib().o_fr_constants(_p(m), _p(r), _p(w)); return m, r, w
+
+
 # ---- curve ops ----
 def g1_mul_generator(scalars, nthreads=1):
     o = _out(_n(scalars), W_G1A); lib().o_g1_mul_generator_batch(_p(scalars), _n(scalars), _p(o), nthreads); return o
@@ -215,6 +294,24 @@ def g1_mul(p, scalars):
 
 def g2_mul(p, scalars):
     o = _out(_n(p), W_G2); lib().o_g2_mul_batch(_p(p), _p(scalars), _n(p), _p(o)); return o
+
+
+def g1_affine_mul(p, scalars, nthreads=1):
+    """CurveAffine::mul (ec.rs:174-177): Jacobian rows."""
+    o = _out(_n(p), W_G1); lib().o_g1_affine_mul_batch(_p(p), _p(scalars), _n(p), _p(o), nthreads); return o
+
+
+def g2_affine_mul(p, scalars, nthreads=1):
+    o = _out(_n(p), W_G2); lib().o_g2_affine_mul_batch(_p(p), _p(scalars), _n(p), _p(o), nthreads); return o
+
+
+def g1_multiexp(p, scalars, nthreads=1):
+    """sum_i s_i * P_i: CurveAffine::mul per term + add_assign in index order; (1, 18)."""
+    o = _out(1, W_G1); lib().o_g1_multiexp(_p(p), _p(scalars), _n(p), _p(o), nthreads); return o
+
+
+def g2_multiexp(p, scalars, nthreads=1):
+    o = _out(1, W_G2); lib().o_g2_multiexp(_p(p), _p(scalars), _n(p), _p(o), nthreads); return o
 
 
 def g1_double(p):

@@ -124,3 +124,35 @@ size_t o_sizeof(int which) {
         default: return 0;
     }
 }
+
+/* CurveAffine::mul (ec.rs:174-177 -> mul_bits ec.rs:88-95), Jacobian out. */
+void o_g1_affine_mul_batch(const o_g1_affine *p, const uint64_t *scalars, size_t n, o_g1 *out, int nthreads) {
+#pragma omp parallel for schedule(dynamic, 4) NT(nthreads)
+    for (size_t k = 0; k < n; k++) out[k] = o_g1_affine_mul(&p[k], &scalars[4 * k]);
+}
+void o_g2_affine_mul_batch(const o_g2_affine *p, const uint64_t *scalars, size_t n, o_g2 *out, int nthreads) {
+#pragma omp parallel for schedule(dynamic, 4) NT(nthreads)
+    for (size_t k = 0; k < n; k++) out[k] = o_g2_affine_mul(&p[k], &scalars[4 * k]);
+}
+/* sum_i s_i * P_i the way a caller of the reference writes it: CurveAffine::mul
+ * per term, then add_assign (ec.rs:356-444) in index order.  The terms are
+ * computed in parallel; the sum is serial, so the result does not depend on
+ * the thread count. */
+void o_g1_multiexp(const o_g1_affine *p, const uint64_t *scalars, size_t n, o_g1 *out, int nthreads) {
+    o_g1 *t = (o_g1 *)malloc(sizeof(o_g1) * (n ? n : 1));
+    o_g1_affine_mul_batch(p, scalars, n, t, nthreads);
+    o_g1 acc = t[0];
+    if (n == 0) { o_g1_affine z = o_g1_affine_zero(); acc = o_g1_from_affine(&z); }
+    for (size_t k = 1; k < n; k++) o_g1_add(&acc, &t[k]);
+    *out = acc;
+    free(t);
+}
+void o_g2_multiexp(const o_g2_affine *p, const uint64_t *scalars, size_t n, o_g2 *out, int nthreads) {
+    o_g2 *t = (o_g2 *)malloc(sizeof(o_g2) * (n ? n : 1));
+    o_g2_affine_mul_batch(p, scalars, n, t, nthreads);
+    o_g2 acc = t[0];
+    if (n == 0) { o_g2_affine z = o_g2_affine_zero(); acc = o_g2_from_affine(&z); }
+    for (size_t k = 1; k < n; k++) o_g2_add(&acc, &t[k]);
+    *out = acc;
+    free(t);
+}

@@ -16,7 +16,7 @@ Device-resident entry points for torch tensors live in `pairing_amd.device`.
 """
 import numpy as np
 
-from ._native import (W_FQ, W_FQ2, W_FQ6, W_FQ12, W_G1A, W_G1, W_G2A, W_G2, W_G2P, PairingError,
+from ._native import (W_FQ, W_FQ2, W_FQ6, W_FQ12, W_FR, W_G1A, W_G1, W_G2A, W_G2, W_G2P, PairingError,
                       as_rows, call, device_count, ptr, set_device, set_pairing_kernel, version)
 
 __all__ = [
@@ -28,6 +28,9 @@ __all__ = [
     "g2_prepare", "miller_loop_batch", "multi_miller_loop", "final_exponentiation", "pairing",
     "multi_miller_loop_affine", "multi_pairing", "pairing_multi_gpu",
     "fq_sqrt", "fq2_sqrt", "g1_decode", "g2_decode", "g1_encode", "g2_encode", "DECODE_STATUS",
+    "fr_mul", "fr_square", "fr_add", "fr_sub", "fr_double", "fr_negate", "fr_inverse",
+    "fr_from_repr", "fr_into_repr", "fr_pow", "fr_legendre", "fr_sqrt",
+    "g1_affine_mul", "g2_affine_mul", "g1_mul_assign", "g2_mul_assign", "g1_multiexp", "g2_multiexp",
 ]
 
 
@@ -294,3 +297,124 @@ def g1_encode(pts, compressed):
 def g2_encode(pts, compressed):
     """EncodedPoint::from_affine for G2 (ec.rs:1398-1415, 1510-1539)."""
     return _encode(2, pts, compressed)
+
+
+# ---- Fr: src/bls12_381/fr.rs (rows (n,4): Montgomery Fr or canonical FrRepr) ----
+def fr_mul(a, b):
+    """Fr::mul_assign (fr.rs:438-465) elementwise."""
+    return _binary("pa_fr_mul_batch", a, b, W_FR)
+
+
+def fr_square(a):
+    """Fr::square (fr.rs:467-500)."""
+    return _unary("pa_fr_square_batch", a, W_FR)
+
+
+def fr_add(a, b):
+    """Fr::add_assign (fr.rs:341-348)."""
+    return _binary("pa_fr_add_batch", a, b, W_FR)
+
+
+def fr_sub(a, b):
+    """Fr::sub_assign (fr.rs:359-367)."""
+    return _binary("pa_fr_sub_batch", a, b, W_FR)
+
+
+def fr_double(a):
+    """Fr::double (fr.rs:350-357)."""
+    return _unary("pa_fr_double_batch", a, W_FR)
+
+
+def fr_negate(a):
+    """Fr::negate (fr.rs:369-375)."""
+    return _unary("pa_fr_negate_batch", a, W_FR)
+
+
+def fr_inverse(a):
+    """Fr::inverse (fr.rs:377-431): (values, ok), ok False where the reference returns None."""
+    return _inverse("pa_fr_inverse_batch", a, W_FR)
+
+
+def fr_from_repr(repr_rows):
+    """PrimeField::from_repr (fr.rs:279-288): (values, ok), ok False = Err(NotInField)."""
+    r = as_rows(repr_rows, W_FR, "repr")
+    out = np.empty_like(r)
+    ok = np.zeros(r.shape[0], np.uint8)
+    call("pa_fr_from_repr_batch", ptr(r), ptr(out), ptr(ok), r.shape[0])
+    return out, ok.astype(bool)
+
+
+def fr_into_repr(a):
+    """PrimeField::into_repr (fr.rs:290-303): canonical FrRepr rows."""
+    return _unary("pa_fr_into_repr_batch", a, W_FR)
+
+
+def fr_pow(a, exp_limbs):
+    """Field::pow (lib.rs:306-324) of every element by one exponent (u64 LE limbs)."""
+    a = as_rows(a, W_FR, "a")
+    e = np.ascontiguousarray(np.asarray(exp_limbs, dtype=np.uint64).reshape(-1))
+    out = np.empty_like(a)
+    call("pa_fr_pow_batch", ptr(a), ptr(e), e.size, ptr(out), a.shape[0])
+    return out
+
+
+def fr_legendre(a):
+    """SqrtField::legendre (fr.rs:575-590): int8 0 Zero, 1 QuadraticResidue, -1 QuadraticNonResidue."""
+    a = as_rows(a, W_FR, "a")
+    out = np.zeros(a.shape[0], np.int8)
+    call("pa_fr_legendre_batch", ptr(a), ptr(out), a.shape[0])
+    return out
+
+
+def fr_sqrt(a):
+    """SqrtField::sqrt (fr.rs:592-646): (roots, ok), ok False where the reference returns None."""
+    return _inverse("pa_fr_sqrt_batch", a, W_FR)
+
+
+# ---- variable-base scalar multiplication and MSM (ec.rs:88-95, 174-177, 534-553) ----
+def _scalar_mul(name, p, scalars, in_width, out_width):
+    p = as_rows(p, in_width, "points")
+    s = as_rows(scalars, 4, "scalars")
+    if p.shape[0] != s.shape[0]:
+        raise ValueError("points and scalars differ in length: %d vs %d" % (p.shape[0], s.shape[0]))
+    out = np.zeros((p.shape[0], out_width), np.uint64)
+    call(name, ptr(p), ptr(s), ptr(out), p.shape[0])
+    return out
+
+
+def g1_affine_mul(p, scalars):
+    """CurveAffine::mul (ec.rs:174-177): Jacobian s_i * P_i, bit-exact with the reference."""
+    return _scalar_mul("pa_g1_affine_mul_batch", p, scalars, W_G1A, W_G1)
+
+
+def g2_affine_mul(p, scalars):
+    return _scalar_mul("pa_g2_affine_mul_batch", p, scalars, W_G2A, W_G2)
+
+
+def g1_mul_assign(p, scalars):
+    """CurveProjective::mul_assign (ec.rs:534-553) on Jacobian points, bit-exact."""
+    return _scalar_mul("pa_g1_mul_assign_batch", p, scalars, W_G1, W_G1)
+
+
+def g2_mul_assign(p, scalars):
+    return _scalar_mul("pa_g2_mul_assign_batch", p, scalars, W_G2, W_G2)
+
+
+def _multiexp(name, bases, scalars, in_width, out_width):
+    b = as_rows(bases, in_width, "bases") if len(bases) else np.zeros((0, in_width), np.uint64)
+    s = as_rows(scalars, 4, "scalars") if len(scalars) else np.zeros((0, 4), np.uint64)
+    if b.shape[0] != s.shape[0]:
+        raise ValueError("bases and scalars differ in length: %d vs %d" % (b.shape[0], s.shape[0]))
+    out = np.zeros((1, out_width), np.uint64)
+    call(name, ptr(b), ptr(s), b.shape[0], ptr(out))
+    return out
+
+
+def g1_multiexp(bases, scalars):
+    """sum_i s_i * P_i over G1 affine bases (Pippenger on the device): one Jacobian row,
+    equal as a point to the reference's sum of CurveAffine::mul results."""
+    return _multiexp("pa_g1_multiexp", bases, scalars, W_G1A, W_G1)
+
+
+def g2_multiexp(bases, scalars):
+    return _multiexp("pa_g2_multiexp", bases, scalars, W_G2A, W_G2)

@@ -8,6 +8,7 @@ Array convention (numpy uint64, C-contiguous, the ABI layout of
 include/pairing_amd.h):
   Fq (n,6)  Fq2 (n,12)  Fq6 (n,36)  Fq12 (n,72)
   G1Affine (n,13)  G2Affine (n,25)  G1 (n,18)  G2 (n,36)  G2Prepared (n,2449)
+  Fr / FrRepr (n,4)
 """
 import ctypes
 import os
@@ -20,6 +21,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libpairing_amd.so")
 W_FQ, W_FQ2, W_FQ6, W_FQ12 = 6, 12, 36, 72
 W_G1A, W_G1, W_G2A, W_G2 = 13, 18, 25, 36
 W_G2P = 68 * 3 * 12 + 1
+W_FR = 4
 
 PA_OK = 0
 
@@ -85,6 +87,27 @@ _SIGS = {
     "pa_pairing_batch_multi_gpu": [_P, _P, _P, _N, ctypes.c_int],
     "pa_g1_decode_batch_device": [_P, _N, ctypes.c_int, ctypes.c_int, _P, _P, _P],
     "pa_g2_decode_batch_device": [_P, _N, ctypes.c_int, ctypes.c_int, _P, _P, _P],
+    "pa_fr_mul_batch": [_P, _P, _P, _N],
+    "pa_fr_square_batch": [_P, _P, _N],
+    "pa_fr_add_batch": [_P, _P, _P, _N],
+    "pa_fr_sub_batch": [_P, _P, _P, _N],
+    "pa_fr_double_batch": [_P, _P, _N],
+    "pa_fr_negate_batch": [_P, _P, _N],
+    "pa_fr_inverse_batch": [_P, _P, _P, _N],
+    "pa_fr_from_repr_batch": [_P, _P, _P, _N],
+    "pa_fr_into_repr_batch": [_P, _P, _N],
+    "pa_fr_pow_batch": [_P, _P, _N, _P, _N],
+    "pa_fr_legendre_batch": [_P, _P, _N],
+    "pa_fr_sqrt_batch": [_P, _P, _P, _N],
+    "pa_fr_mul_batch_device": [_P, _P, _P, _N, _P],
+    "pa_g1_affine_mul_batch": [_P, _P, _P, _N],
+    "pa_g2_affine_mul_batch": [_P, _P, _P, _N],
+    "pa_g1_mul_assign_batch": [_P, _P, _P, _N],
+    "pa_g2_mul_assign_batch": [_P, _P, _P, _N],
+    "pa_g1_multiexp": [_P, _P, _N, _P],
+    "pa_g2_multiexp": [_P, _P, _N, _P],
+    "pa_g1_multiexp_device": [_P, _P, _N, _P, _P, _N, _P],
+    "pa_g2_multiexp_device": [_P, _P, _N, _P, _P, _N, _P],
 }
 for _name, _args in _SIGS.items():
     _fn = getattr(_lib, _name)
@@ -94,6 +117,8 @@ _lib.pa_version.restype = ctypes.c_char_p
 _lib.pa_g1_fixed_base_table_words.restype = ctypes.c_size_t
 _lib.pa_g1_fixed_base_workspace_words.restype = ctypes.c_size_t
 _lib.pa_last_error.restype = ctypes.c_char_p
+_lib.pa_multiexp_workspace_bytes.argtypes = [ctypes.c_int, _N]
+_lib.pa_multiexp_workspace_bytes.restype = ctypes.c_size_t
 
 
 def version():

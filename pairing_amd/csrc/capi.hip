@@ -12,6 +12,7 @@
 
 #include "../../include/pairing_amd.h"
 #include "launch.h"
+#include "launch_msm.h"
 
 namespace {
 
@@ -492,6 +493,157 @@ int pa_pairing_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq1
     PA_TRY(ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)scratch, n, (hipStream_t)stream),
            "kernel launch");
     PA_TRY(fe_launch((const uint64_t*)scratch, (uint64_t*)out, nullptr, n, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
+
+// ---- scalar field Fr (fr.rs) ----
+namespace {
+bool fr_op_needs_b(int op) { return op == pa::FR_MUL || op == pa::FR_ADD || op == pa::FR_SUB; }
+int host_fr_op(int op, const void* a, const void* b, void* out, uint8_t* flag, const uint64_t* exp, size_t exp_words,
+               size_t n) {
+    if (n == 0) return PA_OK;
+    const bool has_out = op != pa::FR_LEGENDRE;
+    const bool has_flag = op == pa::FR_INV || op == pa::FR_FROM_REPR || op == pa::FR_SQRT || op == pa::FR_LEGENDRE;
+    if (!a || (has_out && !out) || (fr_op_needs_b(op) && !b) || (has_flag && !flag) ||
+        (op == pa::FR_POW && exp_words && !exp))
+        return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (exp_words > (1u << 20)) return fail(PA_ERR_INVALID_ARGUMENT, "exponent too long");
+    DevBuf da, db, dout, dflag, dexp;
+    int rc;
+    const size_t bytes = 32 * n;
+    if ((rc = upload(da, a, bytes))) return rc;
+    if (fr_op_needs_b(op) && (rc = upload(db, b, bytes))) return rc;
+    if (op == pa::FR_POW && (rc = upload(dexp, exp, 8 * exp_words))) return rc;
+    PA_TRY(dout.alloc(bytes), "hipMalloc");
+    if (has_flag) PA_TRY(dflag.alloc(n), "hipMalloc");
+    PA_TRY(pa::launch_fr_op(op, da.as<uint64_t>(), db.as<uint64_t>(), dout.as<uint64_t>(), dflag.as<uint8_t>(),
+                            dexp.as<uint64_t>(), (int)exp_words, n, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    if (has_out && (rc = download(out, dout, bytes))) return rc;
+    if (has_flag && (rc = download(flag, dflag, n))) return rc;
+    return PA_OK;
+}
+}  // namespace
+
+int pa_fr_mul_batch(const pa_fr* a, const pa_fr* b, pa_fr* out, size_t n) {
+    return host_fr_op(pa::FR_MUL, a, b, out, nullptr, nullptr, 0, n);
+}
+int pa_fr_square_batch(const pa_fr* a, pa_fr* out, size_t n) {
+    return host_fr_op(pa::FR_SQR, a, nullptr, out, nullptr, nullptr, 0, n);
+}
+int pa_fr_add_batch(const pa_fr* a, const pa_fr* b, pa_fr* out, size_t n) {
+    return host_fr_op(pa::FR_ADD, a, b, out, nullptr, nullptr, 0, n);
+}
+int pa_fr_sub_batch(const pa_fr* a, const pa_fr* b, pa_fr* out, size_t n) {
+    return host_fr_op(pa::FR_SUB, a, b, out, nullptr, nullptr, 0, n);
+}
+int pa_fr_double_batch(const pa_fr* a, pa_fr* out, size_t n) {
+    return host_fr_op(pa::FR_DBL, a, nullptr, out, nullptr, nullptr, 0, n);
+}
+int pa_fr_negate_batch(const pa_fr* a, pa_fr* out, size_t n) {
+    return host_fr_op(pa::FR_NEG, a, nullptr, out, nullptr, nullptr, 0, n);
+}
+int pa_fr_inverse_batch(const pa_fr* a, pa_fr* out, uint8_t* ok, size_t n) {
+    return host_fr_op(pa::FR_INV, a, nullptr, out, ok, nullptr, 0, n);
+}
+int pa_fr_from_repr_batch(const pa_fr_repr* repr, pa_fr* out, uint8_t* ok, size_t n) {
+    return host_fr_op(pa::FR_FROM_REPR, repr, nullptr, out, ok, nullptr, 0, n);
+}
+int pa_fr_into_repr_batch(const pa_fr* a, pa_fr_repr* out, size_t n) {
+    return host_fr_op(pa::FR_INTO_REPR, a, nullptr, out, nullptr, nullptr, 0, n);
+}
+int pa_fr_pow_batch(const pa_fr* a, const uint64_t* exp, size_t exp_words, pa_fr* out, size_t n) {
+    return host_fr_op(pa::FR_POW, a, nullptr, out, nullptr, exp, exp_words, n);
+}
+int pa_fr_legendre_batch(const pa_fr* a, int8_t* out, size_t n) {
+    return host_fr_op(pa::FR_LEGENDRE, a, nullptr, nullptr, (uint8_t*)out, nullptr, 0, n);
+}
+int pa_fr_sqrt_batch(const pa_fr* a, pa_fr* out, uint8_t* ok, size_t n) {
+    return host_fr_op(pa::FR_SQRT, a, nullptr, out, ok, nullptr, 0, n);
+}
+int pa_fr_mul_batch_device(const pa_fr* a, const pa_fr* b, pa_fr* out, size_t n, void* stream) {
+    if (n && (!a || !b || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_fr_mul_batch((const uint64_t*)a, (const uint64_t*)b, (uint64_t*)out, n, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+
+// ---- variable-base scalar multiplication and MSM (kernels_msm.hip) ----
+namespace {
+int host_scalar_mul(int group, int projective, const void* p, const pa_fr_repr* s, void* out, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!p || !s || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const size_t in_rec = projective ? (group == 1 ? sizeof(pa_g1) : sizeof(pa_g2))
+                                     : (group == 1 ? sizeof(pa_g1_affine) : sizeof(pa_g2_affine));
+    const size_t out_rec = group == 1 ? sizeof(pa_g1) : sizeof(pa_g2);
+    DevBuf dp, ds, dout;
+    int rc;
+    if ((rc = upload(dp, p, in_rec * n)) || (rc = upload(ds, s, sizeof(pa_fr_repr) * n))) return rc;
+    PA_TRY(dout.alloc(out_rec * n), "hipMalloc");
+    PA_TRY(pa::launch_scalar_mul(group, projective, dp.as<uint64_t>(), ds.as<uint64_t>(), n, dout.as<uint64_t>(),
+                                 nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, out_rec * n);
+}
+int host_multiexp(int group, const void* bases, const pa_fr_repr* s, size_t n, void* out) {
+    if (!out || (n && (!bases || !s))) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (n >= 0x80000000ull) return fail(PA_ERR_INVALID_ARGUMENT, "multiexp supports n < 2^31");
+    const size_t in_rec = group == 1 ? sizeof(pa_g1_affine) : sizeof(pa_g2_affine);
+    const size_t out_rec = group == 1 ? sizeof(pa_g1) : sizeof(pa_g2);
+    DevBuf db, ds, dout, dws;
+    int rc;
+    if ((rc = upload(db, bases, in_rec * n)) || (rc = upload(ds, s, sizeof(pa_fr_repr) * n))) return rc;
+    PA_TRY(dout.alloc(out_rec), "hipMalloc");
+    const size_t ws = pa::msm_workspace_bytes(group, n);
+    PA_TRY(dws.alloc(ws), "hipMalloc");
+    PA_TRY(pa::launch_msm(group, db.as<uint64_t>(), ds.as<uint64_t>(), n, dout.as<uint64_t>(), dws.p, ws, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, out_rec);
+}
+}  // namespace
+
+int pa_g1_affine_mul_batch(const pa_g1_affine* p, const pa_fr_repr* s, pa_g1* out, size_t n) {
+    return host_scalar_mul(1, 0, p, s, out, n);
+}
+int pa_g2_affine_mul_batch(const pa_g2_affine* p, const pa_fr_repr* s, pa_g2* out, size_t n) {
+    return host_scalar_mul(2, 0, p, s, out, n);
+}
+int pa_g1_mul_assign_batch(const pa_g1* p, const pa_fr_repr* s, pa_g1* out, size_t n) {
+    return host_scalar_mul(1, 1, p, s, out, n);
+}
+int pa_g2_mul_assign_batch(const pa_g2* p, const pa_fr_repr* s, pa_g2* out, size_t n) {
+    return host_scalar_mul(2, 1, p, s, out, n);
+}
+int pa_g1_multiexp(const pa_g1_affine* bases, const pa_fr_repr* scalars, size_t n, pa_g1* out) {
+    return host_multiexp(1, bases, scalars, n, out);
+}
+int pa_g2_multiexp(const pa_g2_affine* bases, const pa_fr_repr* scalars, size_t n, pa_g2* out) {
+    return host_multiexp(2, bases, scalars, n, out);
+}
+size_t pa_multiexp_workspace_bytes(int group, size_t n) {
+    return (group == 1 || group == 2) ? pa::msm_workspace_bytes(group, n) : 0;
+}
+int pa_g1_multiexp_device(const pa_g1_affine* bases, const pa_fr_repr* scalars, size_t n, pa_g1* out,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+    if (!out || (n && (!bases || !scalars || !workspace))) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (n && workspace_bytes < pa::msm_workspace_bytes(1, n))
+        return fail(PA_ERR_INVALID_ARGUMENT, "workspace smaller than pa_multiexp_workspace_bytes");
+    PA_TRY(pa::launch_msm(1, (const uint64_t*)bases, (const uint64_t*)scalars, n, (uint64_t*)out, workspace,
+                          workspace_bytes, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+int pa_g2_multiexp_device(const pa_g2_affine* bases, const pa_fr_repr* scalars, size_t n, pa_g2* out,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+    if (!out || (n && (!bases || !scalars || !workspace))) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (n && workspace_bytes < pa::msm_workspace_bytes(2, n))
+        return fail(PA_ERR_INVALID_ARGUMENT, "workspace smaller than pa_multiexp_workspace_bytes");
+    PA_TRY(pa::launch_msm(2, (const uint64_t*)bases, (const uint64_t*)scalars, n, (uint64_t*)out, workspace,
+                          workspace_bytes, (hipStream_t)stream),
+           "kernel launch");
     return PA_OK;
 }
 

@@ -1,0 +1,399 @@
+// Variable-base scalar multiplication and multi-scalar multiplication (MSM)
+// for G1 and G2 (SURVEY.md §8 f, rank 3).
+//
+// Per-lane scalar multiplication, bit-exact Jacobian output:
+//   CurveAffine::mul (ec.rs:174-177 -> mul_bits ec.rs:88-95): for every one of
+//     the 256 scalar bits, MSB first: double, then add_assign_mixed(base) if set.
+//   CurveProjective::mul_assign (ec.rs:534-553): double-and-add with full
+//     add_assign(self), doubling only after the first set bit.
+// Both replay the reference's exact formula sequence (curve.h), so the X, Y, Z
+// words equal the reference's, not just the point.
+//
+// MSM  sum_i s_i * P_i  (affine bases, FrRepr scalars: the shape of the
+// downstream provers' multiexp over `CurveAffine::mul` + `add_assign`).  The
+// result is equal *as a point* to the reference's sum (PartialEq, ec.rs:45-85);
+// Jacobian words differ because the addition chain is Pippenger's:
+//   1. k_msm_digits: signed c-bit digits per window (|d| <= 2^(c-1)); item
+//      (window, |d|) -> sort key, (i | sign<<31) -> value.   c*W >= 257 so any
+//      256-bit FrRepr (also >= r, as the reference's BitIterator allows) fits.
+//   2. hipcub radix sort of the W*n (key, value) pairs: each bucket's points
+//      become contiguous (stable, so the result is deterministic).
+//   3. k_msm_bucket_bounds: [start, end) per bucket from the sorted keys.
+//   4. k_msm_bucket_acc: one lane per bucket, mixed additions (madd-2007-bl)
+//      of the affine bases gathered from HBM (y negated for negative digits).
+//   5. k_msm_segments: per window, sum_m m*B_m by running sums over segments of
+//      L buckets (T += B_m; S += T, top down), plus a*T for the segment offset.
+//   6. k_msm_group_sum (repeated): segment results -> one sum per window.
+//   7. k_msm_horner: one lane, sum_w 2^(c*w) S_w.
+// Work: n*W mixed additions + ~2*W*2^(c-1) additions + ~256 doublings.
+#include <hipcub/hipcub.hpp>
+
+#include "curve.h"
+#include "launch_msm.h"
+
+namespace pa {
+
+template <int G> struct Grp;
+template <> struct Grp<1> {
+    using F = Fq;
+    static constexpr int AW = 13;  // u64 words per affine record (pa_g1_affine)
+    static constexpr int JW = 18;  // u64 words per Jacobian record (pa_g1)
+};
+template <> struct Grp<2> {
+    using F = Fq2;
+    static constexpr int AW = 25;
+    static constexpr int JW = 36;
+};
+
+// ---------------- per-lane scalar multiplication ----------------
+template <int G>
+__global__ void __launch_bounds__(64) k_affine_mul(const uint64_t* __restrict__ p, const uint64_t* __restrict__ s,
+                                                   uint64_t* __restrict__ out, size_t n) {
+    using F = typename Grp<G>::F;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Aff<F> a;
+    load_aff(a, p + (size_t)Grp<G>::AW * i);
+    uint64_t k[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) k[w] = s[4 * i + w];
+    Jac<F> acc;
+    jac_zero(acc);
+#pragma unroll 1
+    for (int bit = 255; bit >= 0; bit--) {  // mul_bits, ec.rs:88-95
+        jac_double(acc);
+        if ((k[bit >> 6] >> (bit & 63)) & 1) jac_add_mixed(acc, a);
+    }
+    store_jac(out + (size_t)Grp<G>::JW * i, acc);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_proj_mul(const uint64_t* __restrict__ p, const uint64_t* __restrict__ s,
+                                                 uint64_t* __restrict__ out, size_t n) {
+    using F = typename Grp<G>::F;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Jac<F> base, acc;
+    load_jac(base, p + (size_t)Grp<G>::JW * i);
+    uint64_t k[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) k[w] = s[4 * i + w];
+    jac_zero(acc);
+    bool found_one = false;
+#pragma unroll 1
+    for (int bit = 255; bit >= 0; bit--) {  // mul_assign, ec.rs:534-553
+        const bool b = (k[bit >> 6] >> (bit & 63)) & 1;
+        if (found_one) jac_double(acc);
+        else found_one = b;
+        if (b) jac_add(acc, base);
+    }
+    store_jac(out + (size_t)Grp<G>::JW * i, acc);
+}
+
+// ---------------- MSM ----------------
+struct MsmPlan {
+    uint32_t c, W, B, L;        // window bits, windows, buckets per window, segment length
+    uint32_t key_bits;          // radix-sort key width
+    size_t items;               // W * n
+    size_t off_keys_in, off_keys_out, off_vals_in, off_vals_out, off_start, off_end;
+    size_t off_buckets, off_segs, off_tmp, off_sort;
+    size_t sort_bytes, total;
+};
+
+static inline uint32_t msm_window_bits(size_t n) {
+    int lg = 0;
+    while (lg < 40 && ((size_t)1 << (lg + 1)) <= n) lg++;
+    int c = lg - 3;
+    if (c < 4) c = 4;
+    if (c > 16) c = 16;
+    return (uint32_t)c;
+}
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
+    p.c = msm_window_bits(n);
+    p.W = (257 + p.c - 1) / p.c;
+    p.B = 1u << (p.c - 1);
+    p.L = p.B < 32 ? p.B : 32;
+    p.items = (size_t)p.W * n;
+    const uint64_t sentinel = (uint64_t)p.W * p.B;
+    p.key_bits = 1;
+    while (((uint64_t)1 << p.key_bits) <= sentinel) p.key_bits++;
+    const size_t jw = 8 * (size_t)(group == 1 ? Grp<1>::JW : Grp<2>::JW);
+    const size_t nb = (size_t)p.W * p.B;
+    const size_t nseg = (size_t)p.W * (p.B / p.L);
+    size_t off = 0;
+    p.off_keys_in = off; off = align256(off + 4 * p.items);
+    p.off_keys_out = off; off = align256(off + 4 * p.items);
+    p.off_vals_in = off; off = align256(off + 4 * p.items);
+    p.off_vals_out = off; off = align256(off + 4 * p.items);
+    p.off_start = off; off = align256(off + 4 * nb);
+    p.off_end = off; off = align256(off + 4 * nb);
+    p.off_buckets = off; off = align256(off + jw * nb);
+    p.off_segs = off; off = align256(off + jw * nseg);
+    p.off_tmp = off; off = align256(off + jw * nseg);
+    p.sort_bytes = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, p.sort_bytes, (const uint32_t*)nullptr,
+                                                      (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                                      (uint32_t*)nullptr, (int)p.items, 0, (int)p.key_bits);
+    if (e != hipSuccess) return e;
+    p.off_sort = off; off = align256(off + p.sort_bytes);
+    p.total = off;
+    return hipSuccess;
+}
+
+__global__ void __launch_bounds__(256) k_msm_digits(const uint64_t* __restrict__ scalars, size_t n, uint32_t c,
+                                                    uint32_t W, uint32_t B, uint32_t* __restrict__ keys,
+                                                    uint32_t* __restrict__ vals) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t k[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) k[w] = scalars[4 * i + w];
+    const uint32_t sentinel = W * B;
+    const uint32_t mask = (1u << c) - 1;
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < W; w++) {
+        const uint32_t bit = w * c;
+        uint32_t raw = 0;
+        if (bit < 256) {
+            const uint32_t word = bit >> 6, sh = bit & 63;
+            uint64_t v = k[word] >> sh;
+            if (sh + c > 64 && word < 3) v |= k[word + 1] << (64 - sh);
+            raw = (uint32_t)v & mask;
+        }
+        raw += carry;
+        int d;
+        if (raw > B) {
+            d = (int)raw - (int)(1u << c);
+            carry = 1;
+        } else {
+            d = (int)raw;
+            carry = 0;
+        }
+        const size_t at = (size_t)w * n + i;
+        if (d == 0) {
+            keys[at] = sentinel;
+            vals[at] = (uint32_t)i;
+        } else {
+            const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+            keys[at] = w * B + (mag - 1);
+            vals[at] = (uint32_t)i | (d < 0 ? 0x80000000u : 0u);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_msm_bucket_bounds(const uint32_t* __restrict__ keys, size_t items,
+                                                           uint32_t sentinel, uint32_t* __restrict__ start,
+                                                           uint32_t* __restrict__ end) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= items) return;
+    const uint32_t k = keys[j];
+    if (k >= sentinel) return;
+    if (j == 0 || keys[j - 1] != k) start[k] = (uint32_t)j;
+    if (j + 1 == items || keys[j + 1] != k) end[k] = (uint32_t)(j + 1);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_msm_bucket_acc(const uint64_t* __restrict__ bases,
+                                                       const uint32_t* __restrict__ vals,
+                                                       const uint32_t* __restrict__ start,
+                                                       const uint32_t* __restrict__ end, size_t nb,
+                                                       uint64_t* __restrict__ buckets) {
+    using F = typename Grp<G>::F;
+    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    Jac<F> acc;
+    jac_zero(acc);
+    const uint32_t e = end[b];
+#pragma unroll 1
+    for (uint32_t j = start[b]; j < e; j++) {
+        const uint32_t v = vals[j];
+        Aff<F> p;
+        load_aff(p, bases + (size_t)Grp<G>::AW * (v & 0x7fffffffu));
+        if (v >> 31) neg(p.y, p.y);
+        jac_add_mixed(acc, p);
+    }
+    store_jac(buckets + (size_t)Grp<G>::JW * b, acc);
+}
+
+// One lane per segment of L buckets of one window: sum_m m * B_m over the segment.
+template <int G>
+__global__ void __launch_bounds__(64) k_msm_segments(const uint64_t* __restrict__ buckets, uint32_t B, uint32_t L,
+                                                     size_t nseg, uint64_t* __restrict__ segs) {
+    using F = typename Grp<G>::F;
+    constexpr int JW = Grp<G>::JW;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg) return;
+    const uint32_t spw = B / L;
+    const size_t w = t / spw;
+    const uint32_t j = (uint32_t)(t % spw);
+    const uint64_t* bw = buckets + (size_t)JW * (w * B);
+    Jac<F> T, S;
+    jac_zero(T);
+    jac_zero(S);
+#pragma unroll 1
+    for (uint32_t m = (j + 1) * L; m > j * L; m--) {  // magnitudes (j*L, (j+1)*L], top down
+        Jac<F> bk;
+        load_jac(bk, bw + (size_t)JW * (m - 1));
+        jac_add(T, bk);
+        jac_add(S, T);
+    }
+    const uint32_t a = j * L;  // S = sum (m - a) B_m; add a * T
+    if (a && !jac_is_zero(T)) {
+        Jac<F> aT;
+        jac_zero(aT);
+#pragma unroll 1
+        for (int bit = 31; bit >= 0; bit--) {
+            jac_double(aT);
+            if ((a >> bit) & 1) jac_add(aT, T);
+        }
+        jac_add(S, aT);
+    }
+    store_jac(segs + (size_t)JW * t, S);
+}
+
+// out[w*gpw + g] = sum_{k<G} in[w*count + g*G + k]  (indices < count)
+template <int G>
+__global__ void __launch_bounds__(64) k_msm_group_sum(const uint64_t* __restrict__ in, uint32_t count,
+                                                      uint32_t group, uint32_t gpw, uint32_t W,
+                                                      uint64_t* __restrict__ out) {
+    using F = typename Grp<G>::F;
+    constexpr int JW = Grp<G>::JW;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)W * gpw) return;
+    const size_t w = t / gpw;
+    const uint32_t g = (uint32_t)(t % gpw);
+    Jac<F> acc;
+    jac_zero(acc);
+#pragma unroll 1
+    for (uint32_t k = 0; k < group; k++) {
+        const uint32_t idx = g * group + k;
+        if (idx >= count) break;
+        Jac<F> x;
+        load_jac(x, in + (size_t)JW * (w * count + idx));
+        jac_add(acc, x);
+    }
+    store_jac(out + (size_t)JW * t, acc);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ wsum, uint32_t W, uint32_t c,
+                                                   uint64_t* __restrict__ out) {
+    using F = typename Grp<G>::F;
+    constexpr int JW = Grp<G>::JW;
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    Jac<F> acc;
+    load_jac(acc, wsum + (size_t)JW * (W - 1));
+#pragma unroll 1
+    for (int w = (int)W - 2; w >= 0; w--) {
+#pragma unroll 1
+        for (uint32_t k = 0; k < c; k++) jac_double(acc);
+        Jac<F> x;
+        load_jac(x, wsum + (size_t)JW * w);
+        jac_add(acc, x);
+    }
+    store_jac(out, acc);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_jac_zero_out(uint64_t* __restrict__ out) {
+    using F = typename Grp<G>::F;
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    Jac<F> z;
+    jac_zero(z);
+    store_jac(out, z);
+}
+
+static inline unsigned msm_blocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+size_t msm_workspace_bytes(int group, size_t n) {
+    if (n == 0) return 0;
+    MsmPlan p;
+    if (msm_plan(p, group, n) != hipSuccess) return 0;
+    return p.total;
+}
+
+template <int G>
+static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t n, uint64_t* out, void* ws,
+                          size_t ws_bytes, hipStream_t s) {
+    constexpr int JW = Grp<G>::JW;
+    if (n == 0) {
+        hipLaunchKernelGGL(k_jac_zero_out<G>, dim3(1), dim3(64), 0, s, out);
+        return hipGetLastError();
+    }
+    MsmPlan p;
+    hipError_t e = msm_plan(p, G, n);
+    if (e != hipSuccess) return e;
+    if (ws_bytes < p.total || !ws) return hipErrorInvalidValue;
+    char* base = static_cast<char*>(ws);
+    uint32_t* keys_in = reinterpret_cast<uint32_t*>(base + p.off_keys_in);
+    uint32_t* keys_out = reinterpret_cast<uint32_t*>(base + p.off_keys_out);
+    uint32_t* vals_in = reinterpret_cast<uint32_t*>(base + p.off_vals_in);
+    uint32_t* vals_out = reinterpret_cast<uint32_t*>(base + p.off_vals_out);
+    uint32_t* start = reinterpret_cast<uint32_t*>(base + p.off_start);
+    uint32_t* end = reinterpret_cast<uint32_t*>(base + p.off_end);
+    uint64_t* buckets = reinterpret_cast<uint64_t*>(base + p.off_buckets);
+    uint64_t* segs = reinterpret_cast<uint64_t*>(base + p.off_segs);
+    uint64_t* tmp = reinterpret_cast<uint64_t*>(base + p.off_tmp);
+    const size_t nb = (size_t)p.W * p.B;
+
+    hipLaunchKernelGGL(k_msm_digits, dim3(msm_blocks(n, 256)), dim3(256), 0, s, scalars, n, p.c, p.W, p.B, keys_in,
+                       vals_in);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t sort_bytes = p.sort_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(base + p.off_sort, sort_bytes, keys_in, keys_out, vals_in, vals_out,
+                                           (int)p.items, 0, (int)p.key_bits, s);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(start, 0, 4 * nb, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(end, 0, 4 * nb, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_msm_bucket_bounds, dim3(msm_blocks(p.items, 256)), dim3(256), 0, s, keys_out, p.items,
+                       p.W * p.B, start, end);
+    hipLaunchKernelGGL(k_msm_bucket_acc<G>, dim3(msm_blocks(nb, 64)), dim3(64), 0, s, bases, vals_out, start, end,
+                       nb, buckets);
+    const uint32_t spw = p.B / p.L;
+    const size_t nseg = (size_t)p.W * spw;
+    hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(nseg, 64)), dim3(64), 0, s, buckets, p.B, p.L, nseg,
+                       segs);
+    // segment sums -> one per window, 32 at a time (ping-pong segs <-> tmp)
+    uint32_t count = spw;
+    uint64_t* src = segs;
+    uint64_t* dst = tmp;
+    while (count > 1) {
+        const uint32_t group = 32;
+        const uint32_t gpw = (count + group - 1) / group;
+        hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks((size_t)p.W * gpw, 64)), dim3(64), 0, s, src, count,
+                           group, gpw, p.W, dst);
+        count = gpw;
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+    }
+    hipLaunchKernelGGL(k_msm_horner<G>, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
+    (void)JW;
+    return hipGetLastError();
+}
+
+hipError_t launch_msm(int group, const uint64_t* bases, const uint64_t* scalars, size_t n, uint64_t* out, void* ws,
+                      size_t ws_bytes, hipStream_t stream) {
+    if (n >= 0x80000000ull) return hipErrorInvalidValue;
+    return group == 1 ? msm_run<1>(bases, scalars, n, out, ws, ws_bytes, stream)
+                      : msm_run<2>(bases, scalars, n, out, ws, ws_bytes, stream);
+}
+
+hipError_t launch_scalar_mul(int group, int projective, const uint64_t* p, const uint64_t* scalars, size_t n,
+                             uint64_t* out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const dim3 g(msm_blocks(n, 64)), b(64);
+    if (group == 1) {
+        if (projective) hipLaunchKernelGGL(k_proj_mul<1>, g, b, 0, stream, p, scalars, out, n);
+        else hipLaunchKernelGGL(k_affine_mul<1>, g, b, 0, stream, p, scalars, out, n);
+    } else {
+        if (projective) hipLaunchKernelGGL(k_proj_mul<2>, g, b, 0, stream, p, scalars, out, n);
+        else hipLaunchKernelGGL(k_affine_mul<2>, g, b, 0, stream, p, scalars, out, n);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace pa

@@ -79,4 +79,25 @@ hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_aff, uint6
 hipError_t launch_g1_comb_mul(const uint64_t* table_aff, const uint64_t* scalars, uint64_t* out, size_t n,
                               hipStream_t stream);
 
+// Scalar field Fr (kernels_fr.hip).  `flag` receives the Option / Result byte
+// (inverse, from_repr, sqrt) or the LegendreSymbol as int8 (0, 1, -1);
+// `exp` / `exp_words` is the device-resident exponent of FR_POW.
+enum FrOp : int {
+    FR_MUL = 0,
+    FR_SQR,
+    FR_ADD,
+    FR_SUB,
+    FR_DBL,
+    FR_NEG,
+    FR_INV,
+    FR_FROM_REPR,
+    FR_INTO_REPR,
+    FR_POW,
+    FR_LEGENDRE,
+    FR_SQRT,
+};
+hipError_t launch_fr_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, uint8_t* flag,
+                        const uint64_t* exp, int exp_words, size_t n, hipStream_t stream);
+hipError_t launch_fr_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, hipStream_t stream);
+
 }  // namespace pa

@@ -88,3 +88,23 @@ def decode(group, enc, compressed, checked, out, status, stream=None):
          int(bool(compressed)), int(bool(checked)), _dptr(out, width, "out"), ctypes.c_void_p(status.data_ptr()),
          _stream_ptr(stream))
 
+
+
+def fr_mul(a, b, out, stream=None):
+    """Fr::mul_assign (fr.rs:438-465) over a batch resident in HBM, rows (n, 4)."""
+    call("pa_fr_mul_batch_device", _dptr(a, 4, "a"), _dptr(b, 4, "b"), _dptr(out, 4, "out"), a.shape[0],
+         _stream_ptr(stream))
+
+
+def multiexp_workspace(group, n, device):
+    """A device workspace sized for pa_g{group}_multiexp_device over n terms."""
+    nbytes = int(_lib.pa_multiexp_workspace_bytes(int(group), int(n)))
+    return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+
+
+def multiexp(group, bases, scalars, out, workspace, stream=None):
+    """out (1, 18|36) = sum_i scalars[i] * bases[i] (affine records (n, 13|25), FrRepr (n, 4))."""
+    aw, jw = (W_G1A, W_G1) if group == 1 else (W_G2A, 36)
+    call("pa_g%d_multiexp_device" % group, _dptr(bases, aw, "bases"), _dptr(scalars, 4, "scalars"),
+         bases.shape[0], _dptr(out, jw, "out"), ctypes.c_void_p(workspace.data_ptr()), workspace.numel(),
+         _stream_ptr(stream))

@@ -8,6 +8,9 @@ and writes them as JSON.  No reference source text is stored.
 
   kat_limbs.json   -- the hex limb arrays of the reference's KAT tests, by
                       test name, in the order they appear in the test body:
+                        fr.rs   test_fr_add_assign / sub_assign / mul_assign /
+                                squaring / from_into_repr / legendre
+                                                         (fr.rs:911-1505, FrRepr arrays)
                         fq.rs   test_fq_mul_assign       (fq.rs:2558-2584)
                         fq.rs   test_fq_squaring         (fq.rs:2630-2651)
                         fq2.rs  test_fq2_squaring        (fq2.rs:272-345)
@@ -53,8 +56,21 @@ def repr_arrays(body):
     return out
 
 
+def fr_repr_arrays(body):
+    out = []
+    for arr in re.findall(r"FrRepr\(\[(.*?)\]\)", body, re.S):
+        words = [w.strip() for w in arr.split(",") if w.strip()]
+        if len(words) == 4:
+            out.append([int(w, 16) for w in words])
+    return out
+
+
 def main():
     kats = {}
+    src = open(os.path.join(REF, "fr.rs")).read()
+    for t in ("test_fr_add_assign", "test_fr_sub_assign", "test_fr_mul_assign", "test_fr_squaring",
+              "test_fr_from_into_repr", "test_fr_legendre"):
+        kats[t] = [["%016x" % w for w in a] for a in fr_repr_arrays(test_body(src, t))]
     for fname, tests in (
         ("fq.rs", ["test_fq_mul_assign", "test_fq_squaring"]),
         ("fq2.rs", ["test_fq2_squaring", "test_fq2_mul", "test_fq2_inverse"]),

@@ -1,0 +1,139 @@
+"""Variable-base scalar multiplication and multi-scalar multiplication
+(SURVEY.md §8 f, rank 3).
+
+Per-item products (CurveAffine::mul ec.rs:174-177 / mul_bits 88-95,
+CurveProjective::mul_assign ec.rs:534-553) are bit-exact Jacobian words.
+The MSM sum is compared as a point (PartialEq, ec.rs:45-85) with the oracle's
+sum of CurveAffine::mul terms, and -- at sizes where the oracle's sum would be
+slow -- with the size-independent identity
+    sum_i s_i * (a_i G) = ((sum_i s_i a_i) mod r) * G
+whose right side is the k*G path the reference's .dat vectors pin."""
+import numpy as np
+import pytest
+
+from helpers import R_ORDER, from_limbs, limbs, random_scalars, rng, set_infinity, small_scalars
+
+NT = 8
+
+
+def edge_scalars():
+    return small_scalars([0, 1, 2, 3, R_ORDER - 1, R_ORDER, R_ORDER + 1, (1 << 256) - 1, 1 << 255, 0xffff])
+
+
+def combined_scalar(a, s):
+    tot = sum(from_limbs(x) * from_limbs(y) for x, y in zip(a, s)) % R_ORDER
+    return small_scalars([tot])
+
+
+# ---------------- oracle ----------------
+
+def test_oracle_affine_mul_matches_projective_mul(oracle):
+    g = rng(31)
+    s = np.concatenate([edge_scalars(), random_scalars(g, 22)])
+    for gen, mul_aff, from_aff, mul_proj, eq in (
+            (oracle.g1_mul_generator, oracle.g1_affine_mul, oracle.g1_from_affine, oracle.g1_mul, oracle.g1_eq),
+            (oracle.g2_mul_generator, oracle.g2_affine_mul, oracle.g2_from_affine, oracle.g2_mul, oracle.g2_eq)):
+        p = gen(random_scalars(g, len(s)), NT)
+        set_infinity(p, [3])
+        a = mul_aff(p, s, NT)
+        b = mul_proj(from_aff(p), s)
+        assert eq(a, b).all()
+
+
+def test_oracle_affine_mul_of_generator_is_kg(oracle):
+    # into_affine(G.mul(k)) equals the k*G path pinned by the reference's .dat vectors
+    g = rng(32)
+    k = np.concatenate([edge_scalars(), random_scalars(g, 6)])
+    one = small_scalars([1])
+    for gen, mul_aff, into in ((oracle.g1_mul_generator, oracle.g1_affine_mul, oracle.g1_into_affine),
+                               (oracle.g2_mul_generator, oracle.g2_affine_mul, oracle.g2_into_affine)):
+        base = np.repeat(gen(one), len(k), axis=0)
+        np.testing.assert_array_equal(into(mul_aff(base, k)), gen(k))
+
+
+def test_oracle_multiexp_identity(oracle):
+    g = rng(33)
+    n = 40
+    a = random_scalars(g, n)
+    s = np.concatenate([edge_scalars(), random_scalars(g, n - 10)])
+    for gen, msm, eq, into in ((oracle.g1_mul_generator, oracle.g1_multiexp, oracle.g1_eq, oracle.g1_into_affine),
+                               (oracle.g2_mul_generator, oracle.g2_multiexp, oracle.g2_eq, oracle.g2_into_affine)):
+        got = msm(gen(a, NT), s, NT)
+        np.testing.assert_array_equal(into(got), gen(combined_scalar(a, s)))
+        zero = msm(gen(a[:0]), s[:0])
+        assert into(zero)[0, -1] == 1   # empty sum = zero point
+
+
+def test_python_layer_rejects_mismatched_lengths():
+    import pairing_amd as pa
+    with pytest.raises(ValueError):
+        pa.g1_multiexp(np.zeros((3, 13), np.uint64), np.zeros((2, 4), np.uint64))
+    with pytest.raises(ValueError):
+        pa.g2_affine_mul(np.zeros((3, 25), np.uint64), np.zeros((4, 4), np.uint64))
+    with pytest.raises(ValueError):
+        pa.g1_mul_assign(np.zeros((3, 13), np.uint64), np.zeros((3, 4), np.uint64))
+
+
+# ---------------- GPU parity ----------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", [1, 2])
+def test_scalar_mul_bit_exact(gpu, oracle, group):
+    g = rng(40 + group)
+    s = np.concatenate([edge_scalars(), random_scalars(g, 118)])
+    gen = oracle.g1_mul_generator if group == 1 else oracle.g2_mul_generator
+    p = gen(random_scalars(g, len(s)), NT)
+    set_infinity(p, [5, 77])
+    if group == 1:
+        np.testing.assert_array_equal(gpu.g1_affine_mul(p, s), oracle.g1_affine_mul(p, s, NT))
+        pj = oracle.g1_mul(oracle.g1_from_affine(p), small_scalars([7] * len(s)))  # non-normalized z
+        np.testing.assert_array_equal(gpu.g1_mul_assign(pj, s), oracle.g1_mul(pj, s))
+    else:
+        np.testing.assert_array_equal(gpu.g2_affine_mul(p, s), oracle.g2_affine_mul(p, s, NT))
+        pj = oracle.g2_mul(oracle.g2_from_affine(p), small_scalars([7] * len(s)))
+        np.testing.assert_array_equal(gpu.g2_mul_assign(pj, s), oracle.g2_mul(pj, s))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 17, 300, 4099])
+def test_g1_multiexp_matches_oracle(gpu, oracle, n):
+    g = rng(50 + n)
+    p = oracle.g1_mul_generator(random_scalars(g, n), NT)
+    s = random_scalars(g, n)
+    if n >= 17:
+        s[:10] = edge_scalars()
+        set_infinity(p, [11])
+        p[12] = p[13]            # equal bases and digits: doubling inside a bucket
+        s[12] = s[13]
+        p[14] = p[15]            # P and -P
+        p[14, 6:12] = oracle.fq_sub(np.zeros((1, 6), np.uint64), p[15:16, 6:12])[0]
+        s[14] = s[15]
+    got = gpu.g1_multiexp(p, s)
+    exp = oracle.g1_multiexp(p, s, NT)
+    assert oracle.g1_eq(got, exp).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 5, 200])
+def test_g2_multiexp_matches_oracle(gpu, oracle, n):
+    g = rng(60 + n)
+    p = oracle.g2_mul_generator(random_scalars(g, n), NT)
+    s = random_scalars(g, n)
+    if n >= 5:
+        s[:4] = small_scalars([0, 1, R_ORDER - 1, (1 << 256) - 1])
+        set_infinity(p, [4])
+    got = gpu.g2_multiexp(p, s)
+    exp = oracle.g2_multiexp(p, s, NT)
+    assert oracle.g2_eq(got, exp).all()
+
+
+@pytest.mark.gpu
+def test_g1_multiexp_large_identity(gpu, oracle):
+    # 2^16 terms, window c = 13: sum s_i (a_i G) == (sum s_i a_i mod r) G
+    g = rng(70)
+    n = 1 << 16
+    a = random_scalars(g, n)
+    s = random_scalars(g, n)
+    p = oracle.g1_mul_generator(a, NT)
+    got = oracle.g1_into_affine(gpu.g1_multiexp(p, s))
+    np.testing.assert_array_equal(got, oracle.g1_mul_generator(combined_scalar(a, s)))

@@ -32,6 +32,10 @@ for step in "$@"; do
         benchgen2) run bench_gen2 600 env PA_PAIRING_KERNEL=4 python bench.py --no-cpu-baseline ;;
         wnafbench) run bench_wnaf 300 python bench.py --workload wnaf --steps 5 --warmup 1 ;;
         decbench) run bench_decode 300 python bench.py --workload decode --steps 5 --warmup 1 ;;
+        newtests) run pytest_new 600 python -u -m pytest tests/test_fr.py tests/test_msm.py -m gpu -v --timeout 300 --timeout-method thread ;;
+        frbench) run bench_fr 300 python bench.py --workload fr_mul --steps 20 --warmup 3 ;;
+        msmbench) run bench_msm 400 python bench.py --workload msm --steps 5 --warmup 1 ;;
+        profmsm) run prof_msm 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_msm -o run -- python bench.py --workload msm --steps 3 --warmup 1 --no-cpu-baseline ;;
         fqbench) run bench_fq 300 python bench.py --workload fq_mul --steps 20 --warmup 3 --no-cpu-baseline ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
         proffq) run prof_fq 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fq -o run -- python bench.py --workload fq_mul --steps 10 --warmup 2 --no-cpu-baseline ;;
