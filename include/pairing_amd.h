@@ -85,6 +85,8 @@ int pa_synchronize(void);
  *   3 = generated kernels (tools/pgen: own register allocation, code objects
  *       lib/pa_gen_*.hsaco loaded at first use), one lane per pairing (default)
  *   4 = generated kernels, a lane pair per pairing (two waves per SIMD)
+ *   5 = generated kernels with lazy reduction (Fq2 products kept double-width
+ *       and reduced once per output, pa_gen_*_lazy.hsaco), one lane per pairing
  * Not part of the reference interface; for A/B measurement. */
 int pa_set_pairing_kernel(int variant);
 

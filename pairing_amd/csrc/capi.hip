@@ -26,6 +26,7 @@ hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t
         case 2: return pa::launch_miller_loop_fused2(p, q, out, n, s);
         case 3: return pa::launch_miller_loop_gen(p, q, out, n, s);
         case 4: return pa::launch_miller_loop_gen2(p, q, out, n, s);
+        case 5: return pa::launch_miller_loop_gen_lazy(p, q, out, n, s);
         default: return pa::launch_miller_loop_fl(p, q, out, n, s);
     }
 }
@@ -35,6 +36,7 @@ hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, h
         case 2: return pa::launch_final_exponentiation2(in, out, ok, n, s);
         case 3: return pa::launch_final_exp_gen(in, out, ok, n, s);
         case 4: return pa::launch_final_exp_gen2(in, out, ok, n, s);
+        case 5: return pa::launch_final_exp_gen_lazy(in, out, ok, n, s);
         default: return pa::launch_final_exp_fl(in, out, ok, n, s);
     }
 }
@@ -132,7 +134,7 @@ int pa_set_device(int device) {
     return PA_OK;
 }
 int pa_set_pairing_kernel(int variant) {
-    if (variant < 0 || variant > 4) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..4");
+    if (variant < 0 || variant > 5) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..5");
     g_pairing_kernel = variant;
     return PA_OK;
 }

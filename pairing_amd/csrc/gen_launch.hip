@@ -16,11 +16,13 @@
 namespace pa {
 namespace {
 
+constexpr int kKernels = 6;
+
 struct GenDevice {
     bool loaded = false;
     hipError_t err = hipSuccess;
-    hipModule_t mod[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipFunction_t fn[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipModule_t mod[kKernels] = {};
+    hipFunction_t fn[kKernels] = {};
     void* ws = nullptr;
     size_t ws_bytes = 0;
 };
@@ -29,13 +31,18 @@ std::mutex g_mu;
 GenDevice g_dev[64];
 thread_local std::string g_detail;   // the code object that failed to load, for pa_last_error
 
-// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing
-const char* const kFile[4] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco", "pa_gen_miller_loop2.hsaco",
-                              "pa_gen_final_exp2.hsaco"};
-const char* const kName[4] = {"pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2", "pa_gen_final_exp2"};
-const size_t kWaveBytes[4] = {PA_GEN_MILLER_LOOP_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_MEM_SLOTS * 3584ull,
-                              PA_GEN_MILLER_LOOP2_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP2_MEM_SLOTS * 3584ull};
-const int kLanes[4] = {1, 1, 2, 2};
+// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing; 4, 5: one lane,
+// lazy reduction (tower.TowerLazy)
+const char* const kFile[kKernels] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco",
+                                     "pa_gen_miller_loop2.hsaco", "pa_gen_final_exp2.hsaco",
+                                     "pa_gen_miller_loop_lazy.hsaco", "pa_gen_final_exp_lazy.hsaco"};
+const char* const kName[kKernels] = {"pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2",
+                                     "pa_gen_final_exp2", "pa_gen_miller_loop_lazy", "pa_gen_final_exp_lazy"};
+const size_t kWaveBytes[kKernels] = {
+    PA_GEN_MILLER_LOOP_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_MEM_SLOTS * 3584ull,
+    PA_GEN_MILLER_LOOP2_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP2_MEM_SLOTS * 3584ull,
+    PA_GEN_MILLER_LOOP_LAZY_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_LAZY_MEM_SLOTS * 3584ull};
+const int kLanes[kKernels] = {1, 1, 2, 2, 1, 1};
 
 std::string lib_dir() {
     Dl_info info;
@@ -51,7 +58,7 @@ hipError_t load(GenDevice& d) {
     if (d.loaded) return d.err;
     d.loaded = true;
     const std::string dir = lib_dir();
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < kKernels; k++) {
         const std::string path = dir + "/" + kFile[k];
         if ((d.err = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess ||
             (d.err = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) {
@@ -76,7 +83,7 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
     }
     const size_t blocks = (n * kLanes[which] + 63) / 64;
     size_t wave_bytes = 0;
-    for (int k = 0; k < 4; k++) wave_bytes = kWaveBytes[k] > wave_bytes ? kWaveBytes[k] : wave_bytes;
+    for (int k = 0; k < kKernels; k++) wave_bytes = kWaveBytes[k] > wave_bytes ? kWaveBytes[k] : wave_bytes;
     const size_t need = blocks * wave_bytes;
     if (need > d.ws_bytes) {
         if (d.ws) (void)hipFree(d.ws);
@@ -115,6 +122,14 @@ hipError_t launch_miller_loop_gen2(const uint64_t* p_aff, const uint64_t* q_aff,
 }
 hipError_t launch_final_exp_gen2(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream) {
     return launch(3, in, out, ok, n, stream);
+}
+hipError_t launch_miller_loop_gen_lazy(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+                                       hipStream_t stream) {
+    return launch(4, p_aff, q_aff, out, n, stream);
+}
+hipError_t launch_final_exp_gen_lazy(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
+                                     hipStream_t stream) {
+    return launch(5, in, out, ok, n, stream);
 }
 
 }  // namespace pa

@@ -59,6 +59,10 @@ hipError_t launch_final_exp_gen(const uint64_t* in, uint64_t* out, uint8_t* ok, 
 hipError_t launch_miller_loop_gen2(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                    hipStream_t stream);
 hipError_t launch_final_exp_gen2(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream);
+// generated, lazy reduction (tools/pgen tower.TowerLazy); same results
+hipError_t launch_miller_loop_gen_lazy(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+                                       hipStream_t stream);
+hipError_t launch_final_exp_gen_lazy(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream);
 // out[0] = prod_i in[i] (Fq12), in-place tree reduction over `work` (n entries, clobbered)
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
 

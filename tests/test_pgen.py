@@ -45,18 +45,31 @@ def ref_pair(oracle):
     return ins, [_words(ml[0], k) for k in range(12)], [_words(fe[0], k) for k in range(12)]
 
 
-@pytest.mark.parametrize("lanes", [1, 2])
-def test_dsl_miller_loop_matches_oracle(ref_pair, lanes):
+@pytest.mark.parametrize("lanes,lazy", [(1, False), (2, False), (1, True)])
+def test_dsl_miller_loop_matches_oracle(ref_pair, lanes, lazy):
     ins, ml, _ = ref_pair
-    out = dsl.evaluate(kernels.miller_loop_prog(lanes=lanes), ins)
+    out = dsl.evaluate(kernels.miller_loop_prog(lanes=lanes, lazy=lazy), ins)
     assert [out[k] for k in range(12)] == ml
 
 
-@pytest.mark.parametrize("lanes", [1, 2])
-def test_dsl_final_exp_matches_oracle(ref_pair, lanes):
+@pytest.mark.parametrize("lanes,lazy", [(1, False), (2, False), (1, True)])
+def test_dsl_final_exp_matches_oracle(ref_pair, lanes, lazy):
     _, ml, fe = ref_pair
-    out = dsl.evaluate(kernels.final_exp_prog(lanes=lanes), {k: ml[k] for k in range(12)})
+    out = dsl.evaluate(kernels.final_exp_prog(lanes=lanes, lazy=lazy), {k: ml[k] for k in range(12)})
     assert [out[k] for k in range(12)] == fe
+
+
+def test_wide_values_exact():
+    """wide products / normalisation / reduction of the lazy tower equal
+    their integer meaning (tower.TowerLazy, dsl.wsop/wnorm/wred)"""
+    g = random.Random(9)
+    for _ in range(50):
+        a, b, c, d = (dsl.gen_fl.limbs(g.randrange(2 * dsl.Q)) for _ in range(4))
+        lo, hi = dsl.wide_product([(tuple(a), tuple(b)), (tuple(c), tuple(d))])
+        w = dsl.val_of(a) * dsl.val_of(b) + dsl.val_of(c) * dsl.val_of(d)
+        assert dsl.val_of(lo) + (dsl.val_of(hi) << (28 * dsl.NL)) == w
+        r = dsl.mont_reduce_wide(lo, hi)
+        assert (dsl.val_of(r) << (28 * dsl.NL)) % dsl.Q == w % dsl.Q
 
 
 def test_bounds_reject_column_overflow():
@@ -89,13 +102,13 @@ def test_sim_small_program():
     assert sim_check.check("small", debug=True)
 
 
-@pytest.mark.parametrize("which", ["ml", "ml2"])
+@pytest.mark.parametrize("which", ["ml", "ml2", "mlz"])
 def test_sim_miller_loop_kernel(which):
     assert sim_check.check(which, debug=True)
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("which", ["fe", "fe2"])
+@pytest.mark.parametrize("which", ["fe", "fe2", "fez"])
 def test_sim_final_exp_kernel(which):
     assert sim_check.check(which, debug=True)
 

@@ -59,9 +59,13 @@ PROGRAMS = {
     "fe": _mk(kernels.final_exp_prog, kcfg.FinalExpCfg, "pa_gen_final_exp"),
     "ml2": _mk(lambda: kernels.miller_loop_prog(lanes=2), kcfg.MillerLoopCfg2, "pa_gen_miller_loop2"),
     "fe2": _mk(lambda: kernels.final_exp_prog(lanes=2), kcfg.FinalExpCfg2, "pa_gen_final_exp2"),
+    # lazy reduction (tower.TowerLazy): wide products, one reduction per output Fq
+    "mlz": _mk(lambda: kernels.miller_loop_prog(lazy=True), kcfg.MillerLoopCfg, "pa_gen_miller_loop_lazy"),
+    "fez": _mk(lambda: kernels.final_exp_prog(lazy=True), kcfg.FinalExpCfg, "pa_gen_final_exp_lazy"),
 }
 FILES = {"small": "pa_gen_small.hsaco", "ml": "pa_gen_miller_loop.hsaco", "fe": "pa_gen_final_exp.hsaco",
-         "ml2": "pa_gen_miller_loop2.hsaco", "fe2": "pa_gen_final_exp2.hsaco"}
+         "ml2": "pa_gen_miller_loop2.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
+         "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco"}
 
 
 def build(which, outdir):
@@ -117,16 +121,17 @@ def main():
         del args[i:i + 2]
     os.makedirs(outdir, exist_ok=True)
     meta = {}
-    for w in args or ["ml", "fe", "ml2", "fe2"]:
+    for w in args or ["ml", "fe", "ml2", "fe2", "mlz", "fez"]:
         build(w, outdir)
         meta[w] = PROGRAMS[w].cache["r"][3]
     if "ml" in meta and "fe" in meta:
         write_work_json(outdir)
-    if all(k in meta for k in ("ml", "fe", "ml2", "fe2")):
+    if all(k in meta for k in ("ml", "fe", "ml2", "fe2", "mlz", "fez")):
         hdr = os.path.join(ROOT, "pairing_amd", "csrc", "pa_gen_meta.h")
         with open(hdr, "w") as f:
             f.write("// GENERATED by tools/pgen/build_gen.py -- spill workspace per wave (M slots)\n#pragma once\n")
-            for k, name in (("ml", "MILLER_LOOP"), ("fe", "FINAL_EXP"), ("ml2", "MILLER_LOOP2"), ("fe2", "FINAL_EXP2")):
+            for k, name in (("ml", "MILLER_LOOP"), ("fe", "FINAL_EXP"), ("ml2", "MILLER_LOOP2"), ("fe2", "FINAL_EXP2"),
+                            ("mlz", "MILLER_LOOP_LAZY"), ("fez", "FINAL_EXP_LAZY")):
                 f.write("#define PA_GEN_%s_MEM_SLOTS %d\n" % (name, meta[k]))
 
 

@@ -44,23 +44,28 @@ def val_of(limbs):
 
 
 class Val:
-    __slots__ = ("id", "u")
+    """An SSA value of 14 limbs.  `half`: one half (limbs 0..13 or 14..27) of a
+    double-width unreduced product ("wide" value, see Prog.wsop): only its
+    limb bound u is tracked here, the value bound of the pair is tracked by
+    the code that builds it (tower.py Wide)."""
+    __slots__ = ("id", "u", "half")
 
-    def __init__(self, id_, u):
-        self.id, self.u = id_, u
+    def __init__(self, id_, u, half=False):
+        self.id, self.u, self.half = id_, u, half
 
     def __repr__(self):
-        return "v%d/u%d" % (self.id, self.u)
+        return "v%d/u%d%s" % (self.id, self.u, "h" if self.half else "")
 
 
 class Op:
-    __slots__ = ("kind", "dst", "srcs", "imm")
+    __slots__ = ("kind", "dst", "srcs", "imm", "dst2")
 
-    def __init__(self, kind, dst, srcs, imm=None):
-        self.kind, self.dst, self.srcs, self.imm = kind, dst, srcs, imm
+    def __init__(self, kind, dst, srcs, imm=None, dst2=None):
+        self.kind, self.dst, self.srcs, self.imm, self.dst2 = kind, dst, srcs, imm, dst2
 
     def __repr__(self):
-        return "%s %s <- %s %s" % (self.kind, self.dst, self.srcs, "" if self.imm is None else self.imm)
+        return "%s %s%s <- %s %s" % (self.kind, self.dst, "" if self.dst2 is None else ",%r" % self.dst2, self.srcs,
+                                     "" if self.imm is None else self.imm)
 
 
 class Block:
@@ -101,29 +106,67 @@ class Prog:
         self.stack = []
 
     # ---- plumbing ----
-    def _val(self, u):
+    def _val(self, u, half=False):
         assert 1 <= u <= U_MAX, "bound %d out of range" % u
-        v = Val(self.nval, u)
+        v = Val(self.nval, u, half)
         self.nval += 1
         return v
 
     def _op(self, kind, srcs, u, imm=None):
-        v = self._val(u) if u else None
+        half = any(x.half for x in srcs) and kind in ("add", "csub", "getvar")
+        v = self._val(u, half) if u else None
         self.cur.items.append(Op(kind, v, list(srcs), imm))
         return v
 
+    @staticmethod
+    def _full(*vals):
+        assert not any(v.half for v in vals), "field op on a wide half"
+
     # ---- field ops ----
     def mul(self, a, b):
+        self._full(a, b)
         assert a.u * b.u <= COL_BOUND, "mul bound %d*%d" % (a.u, b.u)
         return self._op("sop", [a, b], 1)
 
     def sop(self, a, b, c, d):
+        self._full(a, b, c, d)
         assert a.u * b.u + c.u * d.u <= COL_BOUND, "sop bound %d*%d+%d*%d" % (a.u, b.u, c.u, d.u)
         return self._op("sop", [a, b, c, d], 1)
 
     def sqr(self, a):
+        self._full(a)
         assert a.u <= 3, "sqr bound %d" % a.u
         return self._op("sqr", [a], 1)
+
+    # ---- wide (double-width, unreduced) values: lazy reduction ----
+    def wsop(self, *args):
+        """sum a_i b_i over the pairs (a0, b0, a1, b1, ...) as a 28-limb
+        normalized integer, NOT reduced: returns its halves (lo, hi).  Costs
+        the products of a sop without its Montgomery reduction."""
+        self._full(*args)
+        assert len(args) % 2 == 0 and args
+        assert sum(a.u * b.u for a, b in zip(args[0::2], args[1::2])) <= COL_BOUND, "wsop bound"
+        lo, hi = self._val(1, True), self._val(1, True)
+        self.cur.items.append(Op("wsop", lo, list(args), dst2=hi))
+        return lo, hi
+
+    def wnorm(self, lo, hi):
+        """carry-propagate a wide value: every limb < 2^28 again (u = 1)"""
+        assert lo.half and hi.half
+        nlo, nhi = self._val(1, True), self._val(1, True)
+        self.cur.items.append(Op("wnorm", nlo, [lo, hi], dst2=nhi))
+        return nlo, nhi
+
+    def csub(self, a, b, climbs):
+        """a + C - b limb-wise with an explicit constant C (limbs >= b's)"""
+        ul = max(-(-c // MASK) for c in climbs)
+        return self._op("csub", [a, b], a.u + ul, imm=tuple(climbs))
+
+    def wred(self, lo, hi, u):
+        """Montgomery reduction (lo + hi 2^392) / 2^392 mod q of a wide value;
+        the caller proves the output bound u (checked by evaluate)."""
+        assert lo.half and hi.half
+        return self._op("wred", [lo, hi], u)
 
     def add(self, a, b):
         return self._op("add", [a, b], a.u + b.u)
@@ -132,14 +175,17 @@ class Prog:
         return self.add(a, a)
 
     def sub(self, a, b):
+        self._full(a, b)
         assert b.u in SUBCU, "sub subtrahend bound %d" % b.u
         return self._op("sub", [a, b], a.u + SUBCU[b.u], imm=b.u)
 
     def neg(self, b):
+        self._full(b)
         assert b.u in SUBCU, "neg bound %d" % b.u
         return self._cse("neg", [b], SUBCU[b.u], imm=b.u)
 
     def red(self, a):
+        self._full(a)
         if a.u == 1:
             return a
         return self._cse("red", [a], 1)
@@ -218,6 +264,8 @@ def check_scopes(prog):
                 mark(it.body)
             elif it.dst is not None:
                 owner[it.dst.id] = id(block)
+                if it.dst2 is not None:
+                    owner[it.dst2.id] = id(block)
 
     def check(block):
         for it in block.items:
@@ -254,9 +302,52 @@ class Stats:
         self.counts[k] = self.counts.get(k, 0) + n
 
 
-def _check(limbs, u, what):
+def _check(limbs, u, what, half=False):
     assert all(0 <= x <= u * MASK for x in limbs), "%s: limb bound u=%d violated" % (what, u)
-    assert val_of(limbs) < u * 2 * Q, "%s: value bound u=%d violated" % (what, u)
+    assert half or val_of(limbs) < u * 2 * Q, "%s: value bound u=%d violated" % (what, u)
+
+
+def wide_product(pairs):
+    """normalized 28 limbs of sum a*b (column accumulation, carries folded)"""
+    cols = [0] * (2 * NL)
+    for a, b in pairs:
+        for i in range(NL):
+            for j in range(NL):
+                cols[i + j] += a[i] * b[j]
+    out, acc = [], 0
+    for k in range(2 * NL - 1):
+        acc += cols[k]
+        assert acc < (1 << 64), "wide column %d overflows" % k
+        out.append(acc & MASK)
+        acc >>= LB
+    assert acc <= MASK
+    out.append(acc)
+    return tuple(out[:NL]), tuple(out[NL:])
+
+
+def wide_normalize(lo, hi):
+    w = val_of(lo) + (val_of(hi) << (LB * NL))
+    assert w < (1 << (LB * (2 * NL - 1) + LB)), "wide value exceeds 28 limbs"
+    ls = [(w >> (LB * i)) & MASK for i in range(2 * NL - 1)] + [w >> (LB * (2 * NL - 1))]
+    assert ls[-1] <= MASK
+    return tuple(ls[:NL]), tuple(ls[NL:])
+
+
+def mont_reduce_wide(lo, hi):
+    """exact result of the emitted column reduction of lo + hi 2^392"""
+    w = val_of(lo) + (val_of(hi) << (LB * NL))
+    m = (-w * pow(Q, -1, R)) % R
+    t = w + m * Q
+    ml = gen_fl.limbs(m)
+    acc = 0
+    for k in range(2 * NL - 1):
+        acc += (lo[k] if k < NL else hi[k - NL])
+        acc += sum(ml[i] * QL[k - i] for i in range(max(0, k - NL + 1), min(k, NL - 1) + 1))
+        assert acc < (1 << 64) - (1 << 36), "wred column %d overflows" % k
+        acc >>= LB
+    out = t // R
+    assert out < (1 << 388), "wred output too large"
+    return tuple(gen_fl.limbs(out))
 
 
 def mont_sop(pairs):
@@ -336,6 +427,10 @@ def evaluate(prog, inputs, stats=None, trace=None):
             return tuple(ci - b for ci, b in zip(c, s[0]))
         if k == "red":
             return red_limbs(s[0])
+        if k == "csub":
+            return tuple(a + ci - b for a, ci, b in zip(s[0], op.imm, s[1]))
+        if k == "wred":
+            return mont_reduce_wide(s[0], s[1])
         raise ValueError(k)
 
     def step(op):
@@ -365,10 +460,26 @@ def evaluate(prog, inputs, stats=None, trace=None):
             r = [s[0][1 - ln] for ln in range(L)]
         elif k == "sel":
             r = [s[ln][ln] for ln in range(L)]
+        elif k in ("wsop", "wnorm"):
+            if k == "wsop":
+                st.bump("wsop%d" % (len(op.srcs) // 2))
+                lh = [wide_product(list(zip([x[ln] for x in s][0::2], [x[ln] for x in s][1::2])))
+                      for ln in range(L)]
+            else:
+                lh = [wide_normalize(s[0][ln], s[1][ln]) for ln in range(L)]
+            for ln in range(L):
+                _check(lh[ln][0], op.dst.u, repr(op), True)
+                _check(lh[ln][1], op.dst2.u, repr(op), True)
+            env[op.dst.id] = [x[0] for x in lh]
+            env[op.dst2.id] = [x[1] for x in lh]
+            if trace is not None:
+                trace.append((op.dst.id, lh[0][0] if L == 1 else tuple(x[0] for x in lh), op))
+                trace.append((op.dst2.id, lh[0][1] if L == 1 else tuple(x[1] for x in lh), op))
+            return
         else:
             r = [lane_op(k, op, [x[ln] for x in s]) for ln in range(L)]
         for ln in range(L):
-            _check(r[ln], op.dst.u, repr(op))
+            _check(r[ln], op.dst.u, repr(op), op.dst.half)
         env[op.dst.id] = r
         if trace is not None:
             trace.append((op.dst.id, r[0] if L == 1 else tuple(r), op))

@@ -97,7 +97,8 @@ class Emitter:
         self.stats = {}
         self.recent_vwrite = {}             # VGPR -> instruction index of last VALU write
         self.recent_awrite = {}
-        self.mem_stores_pending = False
+        self.mem_stores_pending = False    # workspace stores whose completion is not tracked
+        self.mstore = {}                    # M slot -> vm count right after its last (tracked) store
         self.debug = False
         self.weight = 1
         self.ensuring = None
@@ -107,6 +108,7 @@ class Emitter:
         self.items = None            # the block being allocated (prefetch lookahead)
         self.defer_vm_wait = False   # batch the waits of one operation's HBM reloads
         self.vm_wait_owed = False
+        self.vm_owed_seq = 0
 
     # ---------------- emission helpers ----------------
     VMEM = ("global_load_dwordx2", "global_load_dword", "global_store_dwordx2", "global_store_byte",
@@ -121,6 +123,8 @@ class Emitter:
             self.lgkm_issued += 1
         elif m == "s_waitcnt_vm0":
             self.pending = {k: v for k, v in self.pending.items() if v[0] != "M"}
+            self.mstore = {}
+            self.mem_stores_pending = False
         elif m == "s_waitcnt_lgkm0":
             self.pending = {k: v for k, v in self.pending.items() if v[0] != "L"}
 
@@ -140,7 +144,7 @@ class Emitter:
     # ---------------- slot bookkeeping ----------------
     def free_vslot(self):
         for k in range(self.NV):
-            if self.vslot[k] is None:
+            if self.vslot[k] is None and k not in self.pinned:
                 return k
         return None
 
@@ -168,6 +172,19 @@ class Emitter:
             self.i("s_waitcnt_vm", n)
             for k in [k for k, v in self.pending.items() if v[0] == "M" and v[1] <= self.vm_issued - n]:
                 del self.pending[k]
+
+    def wait_vm_count(self, n):
+        """s_waitcnt vmcnt(n); retire the tracked stores / prefetches it completes"""
+        self.i("s_waitcnt_vm", n)
+        done = self.vm_issued - n
+        self.mstore = {k: q for k, q in self.mstore.items() if q > done}
+        self.pending = {k: v for k, v in self.pending.items() if v[0] != "M" or v[1] > done}
+
+    def untrack_stores(self):
+        """control-flow merge / loop back edge: the static issue counts no longer
+        describe what is in flight, so the next workspace load waits for all"""
+        self.mem_stores_pending = True
+        self.mstore = {}
 
     def get_vslot(self, pos, avoid=()):
         k = self.free_vslot()
@@ -248,7 +265,7 @@ class Emitter:
         self.i("s_addc_u32", S(S_TMP + 1), S(S_WS + 1), K(0))
         for j in range(7):
             self.i("global_store_dwordx2_s", LOFF, 2 * j, S(S_TMP), 512 * j)
-        self.mem_stores_pending = True
+        self.mstore[d] = self.vm_issued
 
     def own(self, loc, vs):
         kind, k = loc
@@ -316,11 +333,14 @@ class Emitter:
             self.i("s_addc_u32", S(S_TMP + 1), S(S_WS + 1), K(0))
             for j in range(7):
                 self.i("global_store_dwordx2_s", LOFF, self.vbase(s) + 2 * j, S(S_TMP), 512 * j)
-            self.mem_stores_pending = True
+            self.mstore[d] = self.vm_issued
         elif sk == "M" and dk == "V":
             if self.mem_stores_pending:
                 self.i("s_waitcnt_vm0")
-                self.mem_stores_pending = False
+            elif s in self.mstore:
+                # vector memory operations complete in issue order: wait only
+                # until this slot's store is done
+                self.wait_vm_count(min(63, self.vm_issued - self.mstore[s]))
             self.i("s_add_u32", S(S_TMP), S(S_WS), K(s * SLOT_BYTES))
             self.i("s_addc_u32", S(S_TMP + 1), S(S_WS + 1), K(0))
             for j in range(7):
@@ -329,6 +349,7 @@ class Emitter:
                 pass
             elif self.defer_vm_wait:
                 self.vm_wait_owed = True
+                self.vm_owed_seq = self.vm_issued
             else:
                 self.i("s_waitcnt_vm0")
         else:
@@ -409,6 +430,66 @@ class Emitter:
                 self.i("v_add_u32", d + i, K(c[i]), a + i)
                 self.i("v_sub_u32", d + i, d + i, b + i)
 
+    def emit_csub(self, a, b, d, c):
+        """a + C - b limb-wise, C given (wide-value halves)"""
+        if d == b:
+            assert a != b
+            for i in range(NL):
+                self.i("v_sub_u32", d + i, K(c[i]), b + i)
+                self.i("v_add_u32", d + i, a + i, d + i)
+        else:
+            for i in range(NL):
+                self.i("v_add_u32", d + i, K(c[i]), a + i)
+                self.i("v_sub_u32", d + i, d + i, b + i)
+
+    def emit_wsop(self, pairs, dlo, dhi):
+        """sum a*b as 28 normalized limbs, no reduction: column k -> limb k"""
+        first = True
+        for k in range(2 * NL - 1):
+            for a, b in pairs:
+                for i in range(max(0, k - NL + 1), min(k, NL - 1) + 1):
+                    self.i("v_mad_u64_u32", ACC, a + i, b + k - i, K(0) if first else ACC)
+                    first = False
+            self.i("v_and_b32", (dlo + k) if k < NL else (dhi + k - NL), K(MASK), ACC)
+            self.i("v_lshrrev_b64", ACC, K(28), ACC)
+        self.i("v_mov_b32", dhi + NL - 1, ACC)
+
+    def emit_wnorm(self, lo, hi, dlo, dhi):
+        """carry propagation over the 28 limbs (carry in v0, sum in v1)"""
+        for k in range(2 * NL):
+            src = (lo + k) if k < NL else (hi + k - NL)
+            dst = (dlo + k) if k < NL else (dhi + k - NL)
+            if k == 0:
+                self.i("v_lshrrev_b32", ACC, K(28), src)
+                self.i("v_and_b32", dst, K(MASK), src)
+            elif k < 2 * NL - 1:
+                self.i("v_add_u32", ACC + 1, src, ACC)
+                self.i("v_lshrrev_b32", ACC, K(28), ACC + 1)
+                self.i("v_and_b32", dst, K(MASK), ACC + 1)
+            else:
+                self.i("v_add_u32", dst, src, ACC)
+
+    def emit_wred(self, lo, hi, d):
+        """Montgomery reduction of lo + hi 2^392: the reduction half of a sop
+        with the column inputs taken from the wide value"""
+        for k in range(2 * NL - 1):
+            src = (lo + k) if k < NL else (hi + k - NL)
+            if k == 0:
+                self.i("v_mov_b32", ACC, src)
+                self.i("v_mov_b32", ACC + 1, K(0))
+            else:
+                self.i("v_mad_u64_u32", ACC, src, K(1), ACC)
+            for i in range(max(0, k - NL + 1), min(k - 1, NL - 1) + 1):
+                self.i("v_mad_u64_u32", ACC, M0 + i, S(SQ + k - i), ACC)
+            if k < NL:
+                self.i("v_mul_lo_u32", M0 + k, ACC, S(SQINV))
+                self.i("v_and_b32", M0 + k, K(MASK), M0 + k)
+                self.i("v_mad_u64_u32", ACC, M0 + k, S(SQ), ACC)
+            else:
+                self.i("v_and_b32", d + k - NL, K(MASK), ACC)
+            self.i("v_lshrrev_b64", ACC, K(28), ACC)
+        self.i("v_add_u32", d + NL - 1, hi + NL - 1, ACC)
+
     def emit_neg(self, b, d, ub):
         c = SUBC[ub]
         for i in range(NL):
@@ -436,6 +517,8 @@ class Emitter:
                     self.states[v.id].uses.append(pos)
                 if it.dst is not None:
                     self.states[it.dst.id] = ValState(it.dst)
+                if it.dst2 is not None:
+                    self.states[it.dst2.id] = ValState(it.dst2)
 
     def var_ranges(self, block):
         """for each var touched in `block` (at any depth): (first, last) item position"""
@@ -534,7 +617,8 @@ class Emitter:
         self.local_ids = saved_ids
 
     def block_vals(self, block):
-        return {it.dst.id for it in block.items if isinstance(it, Op) and it.dst is not None}
+        ids = {it.dst.id for it in block.items if isinstance(it, Op) and it.dst is not None}
+        return ids | {it.dst2.id for it in block.items if isinstance(it, Op) and it.dst2 is not None}
 
     def park(self, block, pos):
         """before a construct: values of this block live after it leave the V
@@ -570,6 +654,7 @@ class Emitter:
             top, done = self.label(), None
             self.i("s_mov_b32", S(it.sreg), K(it.trips - 1))
             self.i("label", top)
+            self.untrack_stores()      # the previous iteration's stores
             self.run_block(it.body)
             self.i("s_sub_u32", S(it.sreg), S(it.sreg), K(1))
             self.i("s_cmp_ge_i32", S(it.sreg), K(0))
@@ -585,6 +670,8 @@ class Emitter:
             self.i("long_cbranch_scc0", skip)
             self.run_block(it.body)
             self.i("label", skip)
+        if self.mstore:    # a skipped body: fewer operations in flight than counted
+            self.untrack_stores()
         self.weight = w0
         self.depth -= 1
 
@@ -612,16 +699,26 @@ class Emitter:
             sk.append(kk)
         self.defer_vm_wait = False
         if self.vm_wait_owed:
-            self.i("s_waitcnt_vm0")
+            # a demand reload stalls this operation: start the upcoming
+            # operations' reloads first, so they travel during the same wait
+            self.prefetch(pos, burst=True)
             self.vm_wait_owed = False
+            self.wait_vm_count(min(63, self.vm_issued - self.vm_owed_seq))
         dying = [vs for vs in srcs if self.next_use(vs, pos) == 1 << 30]
-        if op.dst is not None:
+        dk2 = None
+        if op.dst2 is not None:
+            # two-result ops (wsop, wnorm): fresh slots, no aliasing of sources
+            dk = self.get_vslot(pos, avoid=self.pinned)
+            self.pinned.add(dk)
+            dk2 = self.get_vslot(pos, avoid=self.pinned)
+            self.pinned.add(dk2)
+        elif op.dst is not None:
             dvs = self.states[op.dst.id]
             # in place over a dying source (safe for every op kind below)
             dk = None
             for vs, kk in zip(srcs, sk):
                 if (vs in dying and self.vslot[kk] is vs and k != "swap"
-                        and not (k == "sub" and op.srcs[0].id == op.srcs[1].id)):
+                        and not (k in ("sub", "csub") and op.srcs[0].id == op.srcs[1].id)):
                     dk = kk
                     break
             if dk is None:
@@ -630,6 +727,8 @@ class Emitter:
             dk = None
         if any(x in self.pending for x in sk):
             self.wait_pending(sk)
+        if dk2 is not None and dk2 in self.pending:
+            self.wait_pending([dk2])
         if dk is not None:
             self.pinned.add(dk)
         self.prefetch(pos)
@@ -645,6 +744,14 @@ class Emitter:
             self.emit_add(base[0], base[1], d)
         elif k == "sub":
             self.emit_sub(base[0], base[1], d, op.imm)
+        elif k == "csub":
+            self.emit_csub(base[0], base[1], d, op.imm)
+        elif k == "wsop":
+            self.emit_wsop(list(zip(base[0::2], base[1::2])), d, self.vbase(dk2))
+        elif k == "wnorm":
+            self.emit_wnorm(base[0], base[1], d, self.vbase(dk2))
+        elif k == "wred":
+            self.emit_wred(base[0], base[1], d)
         elif k == "neg":
             self.emit_neg(base[0], d, op.imm)
         elif k == "const":
@@ -663,17 +770,19 @@ class Emitter:
         for vs in dying:
             # the destination may have taken its V slot
             for loc in list(vs.locs):
-                if loc[0] == "V" and loc[1] == dk:
+                if loc[0] == "V" and loc[1] in (dk, dk2):
                     vs.locs.discard(loc)
                     continue
                 self.release_loc(loc, vs)
             vs.locs.clear()
-        if op.dst is not None:
-            dvs = self.states[op.dst.id]
-            self.vslot[dk] = dvs
-            dvs.locs = {("V", dk)}
+        for dst, kk in ((op.dst, dk), (op.dst2, dk2)):
+            if dst is None:
+                continue
+            dvs = self.states[dst.id]
+            self.vslot[kk] = dvs
+            dvs.locs = {("V", kk)}
             if self.debug:
-                self.i("mark", op.dst.id, d)
+                self.i("mark", dst.id, self.vbase(kk))
             if not dvs.uses:
                 self.kill(dvs)
 
@@ -686,11 +795,19 @@ class Emitter:
     def op_cost(self, op):
         if op.kind == "sop":
             return 196 * (len(op.srcs) // 2 + 1) + 70
+        if op.kind == "wsop":
+            return 196 * (len(op.srcs) // 2) + 60
+        if op.kind == "wred":
+            return 260
+        if op.kind in ("csub", "wnorm"):
+            return 28 if op.kind == "csub" else 84
         return self.COST.get(op.kind, 20)
 
-    def prefetch(self, pos):
+    def prefetch(self, pos, burst=False):
         """issue the LDS / HBM reloads of upcoming operations now, so their
-        latency hides behind the current operation's arithmetic"""
+        latency hides behind the current operation's arithmetic (burst: HBM
+        reloads of the next few operations however close, while this one
+        waits for its own)"""
         items = self.items
         work = 0
         for j in range(pos, min(len(items), pos + 40)):
@@ -703,7 +820,7 @@ class Emitter:
                     if vs is None or any(l[0] == "V" for l in vs.locs) or not vs.locs:
                         continue
                     src = self.best_src(vs)
-                    if src[0] == "A" or work < self.AHEAD[src[0]]:
+                    if src[0] == "A" or (work < self.AHEAD[src[0]] and not (burst and src[0] == "M")):
                         continue
                     k = self.prefetch_slot(pos, j)
                     if k is None:
@@ -714,7 +831,7 @@ class Emitter:
                     self.pending[k] = (src[0], self.lgkm_issued if src[0] == "L" else self.vm_issued)
                     self.bump("prefetch_" + src[0])
             work += self.op_cost(it)
-            if work > self.WINDOW:
+            if work > (self.AHEAD["M"] if burst else self.WINDOW):
                 break
 
     def prefetch_slot(self, pos, j):

@@ -10,7 +10,7 @@ Infinity inputs (miller loop -> one) and f == 0 (final exp -> None) are
 lane selects done by the emitted prologue/epilogue, outside the DSL.
 """
 from dsl import Prog
-from tower import Tower, X_ABS, declare12, get12, set12
+from tower import Tower, TowerLazy, X_ABS, declare12, get12, set12
 from tower2 import Tower2
 
 ML_MASK = (X_ABS >> 1) & ((1 << 62) - 1)  # bits 61..0 below the leading one of |x| >> 1
@@ -71,10 +71,10 @@ ML_HOMES = {"px": "L", "py": "L", "qx0": "M", "qx1": "M", "qy0": "M", "qy1": "M"
 # the Fq12 variable names f<i>_<c> carry the home of "f"
 
 
-def miller_loop_prog(homes=None, lanes=1):
+def miller_loop_prog(homes=None, lanes=1, lazy=False):
     homes = dict(ML_HOMES, **(homes or {}))
     p = Prog("miller_loop" if lanes == 1 else "miller_loop2", lanes)
-    T = Tower(p) if lanes == 1 else Tower2(p)
+    T = (TowerLazy(p) if lazy else Tower(p)) if lanes == 1 else Tower2(p)
     V = _Vars(p, lanes)
     for n in ("px", "py"):
         p.var(n, 1, homes.get(n))
@@ -186,9 +186,9 @@ def exp_by_x(p, T, V, f, x, tag):
     return T.conj12(V.get12(res))
 
 
-def final_exp_prog(lanes=1):
+def final_exp_prog(lanes=1, lazy=False):
     p = Prog("final_exp" if lanes == 1 else "final_exp2", lanes)
-    T = Tower(p) if lanes == 1 else Tower2(p)
+    T = (TowerLazy(p) if lazy else Tower(p)) if lanes == 1 else Tower2(p)
     V = _Vars(p, lanes)
     f = V.load12()
     # mod.rs:104-160

@@ -154,7 +154,7 @@ def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256):
 \t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1
 \t\t.amdhsa_system_sgpr_workgroup_id_x 1
 \t\t.amdhsa_system_vgpr_workitem_id 0
-\t\t.amdhsa_next_free_vgpr 512
+\t\t.amdhsa_next_free_vgpr {nfree}
 \t\t.amdhsa_next_free_sgpr 96
 \t\t.amdhsa_accum_offset {aoff}
 \t\t.amdhsa_reserve_vcc 1

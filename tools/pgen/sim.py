@@ -28,6 +28,7 @@ class Sim:
         self.lanes = lanes or [lane]
         self.inflight = {}   # (lane, vgpr) -> ("lgkm" | "vm", seq, value): loads not yet waited for
         self.seq = {"lgkm": 0, "vm": 0}
+        self.st_inflight = {}  # dword address -> vm seq of a workspace store not yet waited for
         self.vf = {ln: [0] * 256 for ln in self.lanes}
         self.af = {ln: [0] * 256 for ln in self.lanes}
         self.v = self.vf[self.lanes[0]]
@@ -106,6 +107,9 @@ class Sim:
     def complete(self, kind, keep=0):
         """s_waitcnt <kind>(keep): all but the `keep` youngest operations are done"""
         limit = self.seq[kind] - keep
+        if kind == "vm":
+            for ad in [ad for ad, sq in self.st_inflight.items() if sq <= limit]:
+                del self.st_inflight[ad]
         for key in [k for k, (kd, sq, _) in self.inflight.items() if kd == kind and sq <= limit]:
             ln, x = key
             self.vf[ln][x] = self.inflight.pop(key)[2]
@@ -238,8 +242,12 @@ class Sim:
             addr = rd64(a[2]) + rd(a[0]) + a[3]
             self.st32(addr, rd(a[1]))
             self.st32(addr + 4, rd(a[1] + 1))
+            self.st_inflight[addr] = self.st_inflight[addr + 4] = self.seq["vm"]
         elif m == "global_load_dwordx2_s":
             addr = rd64(a[2]) + rd(a[1]) + a[3]
+            if addr in self.st_inflight or addr + 4 in self.st_inflight:
+                raise AssertionError("workspace load of 0x%x before its store was waited for (instr %d)" % (
+                    addr, self.count))
             self.async_wr("vm", a[0], self.ld32(addr))
             self.async_wr("vm", a[0] + 1, self.ld32(addr + 4))
         elif m == "s_load_dwordx2":

@@ -35,7 +35,7 @@ def check(which, seed=5, lane=3, debug=True):
         sim_lane = 2 * lane
     else:
         sim_lane = lane
-    if which in ("small", "fe", "fe2"):
+    if which in ("small", "fe", "fe2", "fez"):
         ins = [rng.randrange(dsl.Q) for _ in range(12)]
         rec = [0] * (72 * lane) + words(ins)
         want = dsl.evaluate(prog, {k: ins[k] for k in range(12)}, trace=trace)
