@@ -7,6 +7,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <string>
 
@@ -44,7 +45,11 @@ const size_t kWaveBytes[kKernels] = {
     PA_GEN_MILLER_LOOP_LAZY_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_LAZY_MEM_SLOTS * 3584ull};
 const int kLanes[kKernels] = {1, 1, 2, 2, 1, 1};
 
+// PA_GEN_DIR (A/B experiments with alternative generated code objects) overrides
+// the directory of libpairing_amd.so; PA_GEN_WS_SLOTS raises the workspace size
+// to fit their spill slots.
 std::string lib_dir() {
+    if (const char* e = getenv("PA_GEN_DIR")) return e;
     Dl_info info;
     if (dladdr(reinterpret_cast<void*>(&lib_dir), &info) && info.dli_fname) {
         std::string p(info.dli_fname);
@@ -84,6 +89,10 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
     const size_t blocks = (n * kLanes[which] + 63) / 64;
     size_t wave_bytes = 0;
     for (int k = 0; k < kKernels; k++) wave_bytes = kWaveBytes[k] > wave_bytes ? kWaveBytes[k] : wave_bytes;
+    if (const char* e = getenv("PA_GEN_WS_SLOTS")) {
+        const size_t b = strtoull(e, nullptr, 10) * 3584ull;
+        wave_bytes = b > wave_bytes ? b : wave_bytes;
+    }
     const size_t need = blocks * wave_bytes;
     if (need > d.ws_bytes) {
         if (d.ws) (void)hipFree(d.ws);

@@ -52,7 +52,7 @@ def test_dsl_miller_loop_matches_oracle(ref_pair, lanes, lazy):
     assert [out[k] for k in range(12)] == ml
 
 
-@pytest.mark.parametrize("lanes,lazy", [(1, False), (2, False), (1, True)])
+@pytest.mark.parametrize("lanes,lazy", [(1, False), (2, False), (1, True), (1, "sq")])
 def test_dsl_final_exp_matches_oracle(ref_pair, lanes, lazy):
     _, ml, fe = ref_pair
     out = dsl.evaluate(kernels.final_exp_prog(lanes=lanes, lazy=lazy), {k: ml[k] for k in range(12)})

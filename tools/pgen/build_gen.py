@@ -56,7 +56,10 @@ def _mk(progf, cfgc, kname):
 PROGRAMS = {
     "small": _mk(small_prog, kcfg.FinalExpCfg, "pa_gen_small"),
     "ml": _mk(kernels.miller_loop_prog, kcfg.MillerLoopCfg, "pa_gen_miller_loop"),
-    "fe": _mk(kernels.final_exp_prog, kcfg.FinalExpCfg, "pa_gen_final_exp"),
+    # default final exponentiation: lazy Fq4 squarings only (tower.TowerLazySq, -1.5 % time);
+    # PGEN_FE_LAZY=0 / 1 builds the plain / fully lazy tower instead (A/B experiments)
+    "fe": _mk(lambda: kernels.final_exp_prog(lazy={"sq": "sq", "0": False, "1": True}[os.environ.get("PGEN_FE_LAZY", "sq")]),
+              kcfg.FinalExpCfg, "pa_gen_final_exp"),
     "ml2": _mk(lambda: kernels.miller_loop_prog(lanes=2), kcfg.MillerLoopCfg2, "pa_gen_miller_loop2"),
     "fe2": _mk(lambda: kernels.final_exp_prog(lanes=2), kcfg.FinalExpCfg2, "pa_gen_final_exp2"),
     # lazy reduction (tower.TowerLazy): wide products, one reduction per output Fq
@@ -89,12 +92,15 @@ def macs(counts):
     """28x28-bit limb multiply-accumulates (v_mad_u64_u32 / v_mad_i64_i32) of
     one pairing, from the DSL's dynamic op counts: a K-term product leaf is
     196 (K + 1) (K products + one Montgomery reduction), a square 392 (it is
-    emitted as a one-term product), red() 30."""
+    emitted as a one-term product), red() 30; lazy reduction: a K-term wide
+    product 196 K, its reduction wred() 222 (196 + 26 column additions)."""
     n = 0
     for k, v in counts.items():
         if k.startswith("sop") and k[3:].isdigit():
             n += 196 * (int(k[3:]) + 1) * v
-    return n + 392 * counts.get("sqr", 0) + 30 * counts.get("red", 0)
+        elif k.startswith("wsop") and k[4:].isdigit():
+            n += 196 * int(k[4:]) * v
+    return n + 392 * counts.get("sqr", 0) + 30 * counts.get("red", 0) + 222 * counts.get("wred", 0)
 
 
 def write_work_json(outdir):

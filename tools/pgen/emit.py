@@ -24,6 +24,8 @@ Output: a list of instruction tuples (mnemonic, operands...) where
 operands are ints (VGPR n: n, AGPR n: 256+n, SGPR n: 512+n), ("k", value)
 for constants, or label strings; see render.py / sim.py.
 """
+import os
+
 from dsl import Loop, If, Op, SUBC, NL, MASK, QL, QINV28, KQ
 
 A_BASE, S_BASE = 256, 512
@@ -75,7 +77,7 @@ class ValState:
 S_ODD = 40          # s[40:41] lane mask of the odd lanes (lane pairs: role 1)
 
 # storage configurations: (V slots, A slots, L slots)
-STORAGE = {1: (17, 18, 11),     # one wave per SIMD: 256 VGPR + 256 AGPR, 40 KB LDS
+STORAGE = {1: (17, 18, int(os.environ.get("PGEN_NL", 11))),  # one wave per SIMD: 256 VGPR + 256 AGPR, 40 KB LDS
            2: (17, 0, 5)}       # two waves per SIMD: 256 VGPR, no AGPR, 20 KB LDS
 
 
@@ -789,7 +791,8 @@ class Emitter:
     # ---------------- prefetch ----------------
     COST = {"sop": None, "sqr": 460, "red": 62, "add": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
             "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14}
-    AHEAD = {"L": 40, "M": 500}   # instructions of other work that hide the load latency
+    # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
+    AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}
     WINDOW = 2500
 
     def op_cost(self, op):

@@ -10,7 +10,7 @@ Infinity inputs (miller loop -> one) and f == 0 (final exp -> None) are
 lane selects done by the emitted prologue/epilogue, outside the DSL.
 """
 from dsl import Prog
-from tower import Tower, TowerLazy, X_ABS, declare12, get12, set12
+from tower import Tower, TowerLazy, TowerLazySq, X_ABS, declare12, get12, set12
 from tower2 import Tower2
 
 ML_MASK = (X_ABS >> 1) & ((1 << 62) - 1)  # bits 61..0 below the leading one of |x| >> 1
@@ -187,8 +187,12 @@ def exp_by_x(p, T, V, f, x, tag):
 
 
 def final_exp_prog(lanes=1, lazy=False):
+    """lazy: False (Tower), True (TowerLazy) or "sq" (TowerLazySq)"""
     p = Prog("final_exp" if lanes == 1 else "final_exp2", lanes)
-    T = (TowerLazy(p) if lazy else Tower(p)) if lanes == 1 else Tower2(p)
+    if lanes == 2:
+        T = Tower2(p)
+    else:
+        T = {False: Tower, True: TowerLazy, "sq": TowerLazySq}[lazy](p)
     V = _Vars(p, lanes)
     f = V.load12()
     # mod.rs:104-160

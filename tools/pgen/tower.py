@@ -414,3 +414,13 @@ class TowerLazy(Tower):
         t2 = t.w_sqr2(t.lim1(t.add2(a, b)))
         r1 = t.w_red2(t.w_sub2(t2, t.w_add2(t0, t1)))
         return t.lim1(r0), t.lim1(r1)
+
+
+class TowerLazySq(TowerLazy):
+    """Only the Fq4 squaring of the cyclotomic square is lazy: its three Fq2
+    squares stay wide and each output Fq is reduced once -- the one override
+    that lowers the final exponentiation's instruction count
+    (tools/pgen/lazy_explore.py); every other product as in Tower."""
+    mul2 = Tower.mul2
+    mul6 = Tower.mul6
+    mul_by_01 = Tower.mul_by_01
