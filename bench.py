@@ -140,6 +140,24 @@ def cpu_baseline_wnaf(base, scalars, seconds):
                       "restatement, OpenMP over scalars, %.1f s wall" % (n, wall)}
 
 
+def measure_copy_gbs(nbytes, dev, stream, reps=20):
+    """Device-to-device copy of nbytes/2 (nbytes moved: half read, half
+    written) timed with HIP events: the achievable streaming rate on this box."""
+    import torch
+    half = max(1, nbytes // 2 // 8)
+    src = torch.empty(half, dtype=torch.int64, device=dev)
+    dst = torch.empty_like(src)
+    src.fill_(1)
+    dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return 2 * half * 8 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+
 def cpu_baseline_fq_mul(a, b, seconds):
     from oracle import binding as oracle
     n = min(len(a), 1 << 20)
@@ -353,15 +371,18 @@ def main():
         step(False)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    # per-kernel durations from HIP events on the launch stream: one event set
+    # per step, read after the closing synchronize (no host sync between steps)
+    step_ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    for s in range(args.steps):
+        ev[:] = step_ev[s]
         step(True)
-        # per-kernel durations from HIP events on the launch stream
-        torch.cuda.synchronize()
-        k_ms["a"].append(ev[0].elapsed_time(ev[1]))
-        if args.workload in ("pairing", "wnaf", "decode"):
-            k_ms["b"].append(ev[1].elapsed_time(ev[2]))
     barrier()
     elapsed = time.perf_counter() - t0
+    for e in step_ev:
+        k_ms["a"].append(e[0].elapsed_time(e[1]))
+        if args.workload in ("pairing", "wnaf", "decode"):
+            k_ms["b"].append(e[1].elapsed_time(e[2]))
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if ws > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -429,6 +450,13 @@ def main():
         roof = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "bytes_per_unit": dom_bytes, "avg_launch_ms": round(dom_ms, 4)}
+        if args.workload in ("fq_mul", "fr_mul"):
+            # what a plain device copy of the same byte count reaches on this
+            # box (read a,b / write out = 2 reads + 1 write; the copy moves
+            # 1 read + 1 write per byte pair), for context next to the spec peak
+            copy_gbs = measure_copy_gbs(dom_bytes * n, dev, stream)
+            roof["copy_GBs"] = round(copy_gbs, 1)
+            roof["frac_of_copy"] = achieved / copy_gbs
         work_path = os.path.join(ROOT, "pairing_amd", "lib", "pa_gen_work.json")
         if args.workload == "pairing" and os.path.exists(work_path):
             # the pairing kernels are VALU-issue bound (multiply-accumulate

@@ -10,17 +10,44 @@
 namespace pa {
 
 // Fq::mul_assign over a batch, fq.rs:909-960.  Grid-stride so one launch
-// covers any n with a chip-filling grid.
+// covers any n with a chip-filling grid; PF = 1 software-pipelines the loop:
+// the next element's operands are loaded before the current multiply, so a
+// wave's loads overlap its own ~600-instruction multiply instead of every
+// wave alternating a memory phase and a compute phase in lockstep.
+template <int PF>
 __global__ void __launch_bounds__(256) k_fq_mul_batch(const uint64_t* __restrict__ a,
                                                        const uint64_t* __restrict__ b,
                                                        uint64_t* __restrict__ out, size_t n) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        Fq x, y, z;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if constexpr (PF) {
+        if (i >= n) return;
+        Fq x, y;
         fq_load(x, a + 6 * i);
         fq_load(y, b + 6 * i);
-        fq_mul(z, x, y);
-        fq_store(out + 6 * i, z);
+        for (;;) {
+            const size_t j = i + stride;
+            Fq xn, yn;
+            if (j < n) {
+                fq_load(xn, a + 6 * j);
+                fq_load(yn, b + 6 * j);
+            }
+            Fq z;
+            fq_mul(z, x, y);
+            fq_store(out + 6 * i, z);
+            if (j >= n) break;
+            x = xn;
+            y = yn;
+            i = j;
+        }
+    } else {
+        for (; i < n; i += stride) {
+            Fq x, y, z;
+            fq_load(x, a + 6 * i);
+            fq_load(y, b + 6 * i);
+            fq_mul(z, x, y);
+            fq_store(out + 6 * i, z);
+        }
     }
 }
 
@@ -108,10 +135,13 @@ static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n 
 hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
                                hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    // 256 CUs x 8 blocks of 256 threads, grid-stride beyond that
     size_t blocks = (n + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(k_fq_mul_batch, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
+    const StreamCfg c = stream_cfg();
+    if (blocks > c.max_blocks) blocks = c.max_blocks;
+    if (c.prefetch)
+        hipLaunchKernelGGL(k_fq_mul_batch<1>, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
+    else
+        hipLaunchKernelGGL(k_fq_mul_batch<0>, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
     return hipGetLastError();
 }
 

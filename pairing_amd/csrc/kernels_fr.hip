@@ -9,16 +9,42 @@
 
 namespace pa {
 
-// Field::mul_assign over a batch (fr.rs:438-465), grid-stride.
+// Field::mul_assign over a batch (fr.rs:438-465), grid-stride; PF = 1
+// prefetches the next element's operands before the current multiply (see
+// k_fq_mul_batch).
+template <int PF>
 __global__ void __launch_bounds__(256) k_fr_mul_batch(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
                                                        uint64_t* __restrict__ out, size_t n) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        Fr x, y, z;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if constexpr (PF) {
+        if (i >= n) return;
+        Fr x, y;
         fr_load(x, a + 4 * i);
         fr_load(y, b + 4 * i);
-        fr_mul(z, x, y);
-        fr_store(out + 4 * i, z);
+        for (;;) {
+            const size_t j = i + stride;
+            Fr xn, yn;
+            if (j < n) {
+                fr_load(xn, a + 4 * j);
+                fr_load(yn, b + 4 * j);
+            }
+            Fr z;
+            fr_mul(z, x, y);
+            fr_store(out + 4 * i, z);
+            if (j >= n) break;
+            x = xn;
+            y = yn;
+            i = j;
+        }
+    } else {
+        for (; i < n; i += stride) {
+            Fr x, y, z;
+            fr_load(x, a + 4 * i);
+            fr_load(y, b + 4 * i);
+            fr_mul(z, x, y);
+            fr_store(out + 4 * i, z);
+        }
     }
 }
 
@@ -66,8 +92,12 @@ static inline unsigned fr_blocks_for(size_t n, unsigned bs) { return (unsigned)(
 hipError_t launch_fr_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     size_t blocks = (n + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(k_fr_mul_batch, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
+    const StreamCfg c = stream_cfg();
+    if (blocks > c.max_blocks) blocks = c.max_blocks;
+    if (c.prefetch)
+        hipLaunchKernelGGL(k_fr_mul_batch<1>, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
+    else
+        hipLaunchKernelGGL(k_fr_mul_batch<0>, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
     return hipGetLastError();
 }
 

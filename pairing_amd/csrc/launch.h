@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace pa {
 
@@ -30,6 +31,26 @@ hipError_t launch_field_op(int op, const uint64_t* a, const uint64_t* b, uint64_
                            size_t n, int param, hipStream_t stream);
 hipError_t launch_fq12_mul_by_014(const uint64_t* a, const uint64_t* c0, const uint64_t* c1,
                                   const uint64_t* c4, uint64_t* out, size_t n, hipStream_t stream);
+// Launch shape of the HBM-streaming batch multiplies (Fq, Fr): grid cap in
+// 256-thread blocks and whether the grid-stride loop prefetches.  Read once;
+// PA_STREAM_BLOCKS / PA_STREAM_PREFETCH override for A/B measurements.
+struct StreamCfg {
+    size_t max_blocks;
+    int prefetch;
+};
+inline StreamCfg stream_cfg() {
+    static const StreamCfg c = [] {
+        StreamCfg r{1024, 1};
+        if (const char* e = getenv("PA_STREAM_BLOCKS")) {
+            const long v = strtol(e, nullptr, 10);
+            if (v > 0) r.max_blocks = (size_t)v;
+        }
+        if (const char* e = getenv("PA_STREAM_PREFETCH")) r.prefetch = atoi(e) != 0;
+        return r;
+    }();
+    return c;
+}
+
 // Fq::mul_assign batch, 6 x u64 AoS in and out (config 2 kernel)
 hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
                                hipStream_t stream);
