@@ -9,8 +9,9 @@
 //
 // One lane per record.  Every output is canonical (affine coordinates, status
 // codes, bytes), so the only freedom used is in how the subgroup membership
-// r*P == 0 (ec.rs:142-144) is evaluated: MSB-first double-and-add from the top
-// set bit of r with the reference's Jacobian formulas (curve.h).  Records are
+// r*P == 0 (ec.rs:142-144) is evaluated: by the equivalent endomorphism
+// identities phi(P) == -[x^2]P (G1) and psi(P) == [x]P (G2), see
+// in_subgroup below.  Records are
 // read as 32-bit words and byte-swapped (the wire format is big-endian).
 #include <type_traits>
 
@@ -25,9 +26,6 @@ __constant__ const uint64_t kQm3Div4[6] = {0xee7fbfffffffeaaaULL, 0x07aaffffac54
                                            0xd91dd2e13ce144afULL, 0x92c6e9ed90d2eb35ULL, 0x0680447a8e5ff9a6ULL};
 __constant__ const uint64_t kQm1Div2[6] = {0xdcff7fffffffd555ULL, 0x0f55ffff58a9ffffULL, 0xb39869507b587b12ULL,
                                            0xb23ba5c279c2895fULL, 0x258dd3db21a5d66bULL, 0x0d0088f51cbff34dULL};
-// Fr::char() = r, fr.rs:5-10
-__constant__ const uint64_t kFrModulus[4] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL,
-                                             0x73eda753299d7d48ULL};
 // R^2 mod q (fq.rs:33-40) and -1 (fq.rs:501-508), Montgomery
 __constant__ const uint64_t kR2[6] = {0xf4df1f341c341746ULL, 0x0a76e6a609d104f1ULL, 0x8de5476c4c95b6d5ULL,
                                       0x67eb88a9939d83c0ULL, 0x9a793e85b519952dULL, 0x11988fe592cae3aaULL};
@@ -170,18 +168,87 @@ PA_DEV bool on_curve(const Aff<F>& a) {
     return eq(y2, rhs);
 }
 
-// is_in_correct_subgroup_assuming_on_curve, ec.rs:142-144: r * P == 0
+// is_in_correct_subgroup_assuming_on_curve, ec.rs:142-144: r * P == 0.
+// The reference multiplies by r (255 doublings + ~128 additions).  For a point
+// already on the curve the same yes/no answer comes from an endomorphism
+// identity (Scott, "A note on group membership tests for G1, G2 and GT on BLS
+// pairing-friendly curves", eprint 2021/1130, sections 4 and 6; the tests the
+// zkcrypto bls12_381 crate uses):
+//   G1: P in G1  <=>  phi(P) == -[x^2] P,  phi(x, y) = (beta x, y)
+//   G2: P in G2  <=>  psi(P) == [x] P = -[|x|] P,
+//       psi(x, y) = (conj(x) cx, conj(y) cy), cx = (u+1)^-((q-1)/3), cy = (u+1)^-((q-1)/2)
+// with x = -0xd201000000010000 the BLS parameter (mod.rs:23-25): 126 (G1) or
+// 63 (G2) doublings instead of 255.  tests/test_decode.py pins the answers to
+// the oracle's r * P on the reference's invalid-vector suites plus random
+// on-curve points with and without small-order components.
+__constant__ const uint64_t kBeta[6] = {0x30f1361b798a64e8ULL, 0xf3b8ddab7ece5a2aULL, 0x16a8ca3ac61577f7ULL,
+                                        0xc26a2ff874fd029bULL, 0x3636b76660701c6eULL, 0x051ba4ab241b6160ULL};
+__constant__ const uint64_t kPsiX1[6] = {0x890dc9e4867545c3ULL, 0x2af322533285a5d5ULL, 0x50880866309b7e2cULL,
+                                         0xa20d1b8c7e881024ULL, 0x14e4f04fe2db9068ULL, 0x14e56d3f1564853aULL};
+__constant__ const uint64_t kPsiY0[6] = {0x3e2f585da55c9ad1ULL, 0x4294213d86c18183ULL, 0x382844c88b623732ULL,
+                                         0x92ad2afd19103e18ULL, 0x1d794e4fac7cf0b9ULL, 0x0bd592fc7d825ec8ULL};
+__constant__ const uint64_t kPsiY1[6] = {0x7bcfa7a25aa30fdaULL, 0xdc17dec12a927e7cULL, 0x2f088dd86b4ebef1ULL,
+                                         0xd1ca2087da74d4a7ULL, 0x2da2596696cebc1dULL, 0x0e2b7eedbbfd87d2ULL};
+constexpr uint64_t kAbsX = 0xd201000000010000ULL;
+
+// r = [|x|] p: MSB-first double-and-add (63 doublings, 5 additions)
+template <class F>
+__device__ __noinline__ void mul_abs_x(Jac<F>& r, const Jac<F>& p) {
+    r = p;  // bit 63
+#pragma unroll 1
+    for (int bit = 62; bit >= 0; bit--) {
+        jac_double(r);
+        if ((kAbsX >> bit) & 1) jac_add(r, p);
+    }
+}
+
+// affine e == -q (q Jacobian): e.x z^2 == X and e.y z^3 == -Y, q not zero
+template <class F>
+PA_DEV bool aff_eq_neg_jac(const F& ex, const F& ey, const Jac<F>& q) {
+    if (jac_is_zero(q)) return false;
+    F zz, t, u;
+    sqr(zz, q.z);
+    mul(t, ex, zz);
+    if (!eq(t, q.x)) return false;
+    mul(zz, zz, q.z);
+    mul(t, ey, zz);
+    add(u, t, q.y);
+    return is_zero(u);
+}
+
+PA_DEV bool in_subgroup_endo(const Aff<Fq>& a) {
+    Jac<Fq> p, t, q;
+    jac_from_affine(p, a);
+    mul_abs_x(t, p);
+    mul_abs_x(q, t);  // [x^2] P
+    Fq beta, ex;
+    fq_const(beta, kBeta);
+    mul(ex, a.x, beta);
+    return aff_eq_neg_jac(ex, a.y, q);
+}
+PA_DEV bool in_subgroup_endo(const Aff<Fq2>& a) {
+    Jac<Fq2> p, q;
+    jac_from_affine(p, a);
+    mul_abs_x(q, p);  // [|x|] P = -[x] P
+    Fq2 c, ex, ey, yc;
+    yc.c0 = a.y.c0;
+    neg(yc.c1, a.y.c1);
+    // cx = (0, kPsiX1): conj(x) * cx = (x1 cx1, x0 cx1)
+    Fq cx1;
+    fq_const(cx1, kPsiX1);
+    mul(ex.c0, a.x.c1, cx1);
+    mul(ex.c1, a.x.c0, cx1);
+    fq_const(c.c0, kPsiY0);
+    fq_const(c.c1, kPsiY1);
+    mul(ey, yc, c);
+    // psi(P) == [x] P == -[|x|] P
+    return aff_eq_neg_jac(ex, ey, q);
+}
+
 template <class F>
 __device__ __noinline__ bool in_subgroup(const Aff<F>& a) {
     if (a.inf) return true;
-    Jac<F> acc;
-    jac_from_affine(acc, a);  // bit 254, the top set bit of r
-#pragma unroll 1
-    for (int bit = 253; bit >= 0; bit--) {
-        jac_double(acc);
-        if ((kFrModulus[bit >> 6] >> (bit & 63)) & 1) jac_add_mixed(acc, a);
-    }
-    return jac_is_zero(acc);
+    return in_subgroup_endo(a);
 }
 
 // 48 big-endian bytes (word-aligned) -> 12 little-endian u32 words

@@ -209,3 +209,92 @@ def as_array(cases, size):
     enc = np.frombuffer(b"".join(c[0] for c in cases), np.uint8).reshape(-1, size)
     want = np.array([c[1] for c in cases], np.uint8)
     return enc.copy(), want
+
+
+# ---------------- subgroup-membership cases ----------------
+# On-curve points in and out of the prime-order subgroups, including points
+# with small-order components, to pin the GPU's endomorphism membership test
+# (kernels_decode.hip in_subgroup) to the reference's r * P == 0
+# (ec.rs:142-144) as evaluated by the oracle.  Affine Python-int arithmetic.
+R_ORDER = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+_X = -0xd201000000010000
+H1 = 0x396c8c005555e1568c00aaab0000aaab
+H2 = (_X ** 8 - 4 * _X ** 7 + 5 * _X ** 6 - 4 * _X ** 4 + 6 * _X ** 3 - 4 * _X ** 2 - 4 * _X + 13) // 9
+
+
+def _f1():
+    inv = lambda a: pow(a, -1, Q)
+    return dict(add=lambda a, b: (a + b) % Q, sub=lambda a, b: (a - b) % Q, mul=lambda a, b: a * b % Q,
+                inv=inv, zero=0, small=lambda k: k % Q)
+
+
+def _f2():
+    from pymodel import f2inv, f2sub
+    return dict(add=f2add, sub=f2sub, mul=f2mul, inv=f2inv, zero=(0, 0), small=lambda k: (k % Q, 0))
+
+
+def _ec_add(F, P, R):
+    if P is None:
+        return R
+    if R is None:
+        return P
+    (x1, y1), (x2, y2) = P, R
+    if x1 == x2:
+        if F["add"](y1, y2) == F["zero"]:
+            return None
+        lam = F["mul"](F["mul"](F["small"](3), F["mul"](x1, x1)), F["inv"](F["add"](y1, y1)))
+    else:
+        lam = F["mul"](F["sub"](y2, y1), F["inv"](F["sub"](x2, x1)))
+    x3 = F["sub"](F["sub"](F["mul"](lam, lam), x1), x2)
+    return (x3, F["sub"](F["mul"](lam, F["sub"](x1, x3)), y1))
+
+
+def _ec_mul(F, P, k):
+    acc = None
+    for bit in bin(k)[2:]:
+        acc = _ec_add(F, acc, acc)
+        if bit == "1":
+            acc = _ec_add(F, acc, P)
+    return acc
+
+
+def _random_point(group, g):
+    while True:
+        if group == 1:
+            x = int(g.integers(0, 1 << 62)) * (1 << 300) % Q + int(g.integers(0, 1 << 62))
+            if is_square_fq(rhs1(x)):
+                return (x, sqrt_fq(rhs1(x)))
+        else:
+            x = (int(g.integers(0, 1 << 62)) << 200, int(g.integers(0, 1 << 62)) + 7)
+            if is_square_fq2(rhs2(x)):
+                return (x, sqrt_fq2(rhs2(x)))
+
+
+def subgroup_points(group, seed, n=6):
+    """(points, in_subgroup) for uncompressed encoding: random curve points,
+    their cofactor-cleared and r-multiplied images (small-order only), order-3
+    and order-13 (G2) torsion points, and sums of subgroup and torsion points."""
+    F = _f1() if group == 1 else _f2()
+    h = H1 if group == 1 else H2
+    small = 3 if group == 1 else 13
+    g = np.random.default_rng(seed)
+    pts = []
+    for _ in range(n):
+        R = _random_point(group, g)
+        S = _ec_mul(F, R, h)             # in the subgroup
+        T = _ec_mul(F, R, R_ORDER)       # order divides h: outside
+        Ts = _ec_mul(F, T, h // small)   # order `small` or trivial
+        pts += [R, S, T, _ec_add(F, S, T)]
+        if Ts is not None:
+            pts += [Ts, _ec_add(F, S, Ts)]
+    pts = [P for P in pts if P is not None]
+    truth = [_ec_mul(F, P, R_ORDER) is None for P in pts]
+    return pts, truth
+
+
+def subgroup_records(group, seed, n=6):
+    pts, truth = subgroup_points(group, seed, n)
+    enc = enc_g1 if group == 1 else enc_g2
+    recs = [enc(P[0], P[1], False) for P in pts]
+    size = 96 if group == 1 else 192
+    return np.frombuffer(b"".join(recs), np.uint8).reshape(-1, size).copy(), np.array(truth)

@@ -167,3 +167,26 @@ def test_gpu_fq2_sqrt_matches_oracle(gpu, oracle):
     assert ok.tolist() == want_ok.astype(bool).tolist()
     assert np.array_equal(got[ok], want[ok])
     assert ok[3:400].all()
+
+
+# ---------------- subgroup membership: r * P == 0 vs the GPU's endomorphism test ----------------
+@pytest.fixture(scope="module", params=[1, 2])
+def subgroup_case(request):
+    enc, truth = D.subgroup_records(request.param, seed=40 + request.param, n=3)
+    return request.param, enc, truth
+
+
+def test_oracle_subgroup_check_matches_integer_model(oracle, subgroup_case):
+    group, enc, truth = subgroup_case
+    _, st = oracle.decode(group, enc, False, checked=True, nthreads=4)
+    assert st.tolist() == [D.OK if t else D.NOT_IN_SUBGROUP for t in truth]
+    assert truth.any() and not truth.all()
+
+
+@pytest.mark.gpu
+def test_gpu_subgroup_check_matches_oracle(gpu, oracle, subgroup_case):
+    group, enc, truth = subgroup_case
+    want_pts, want_st = oracle.decode(group, enc, False, checked=True, nthreads=4)
+    pts, st = (gpu.g1_decode if group == 1 else gpu.g2_decode)(enc, False, True)
+    assert st.tolist() == want_st.tolist()
+    assert np.array_equal(pts, want_pts)
