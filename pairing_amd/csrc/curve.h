@@ -197,6 +197,59 @@ PA_DEV void jac_add_mixed(Jac<F>& s, const Aff<F>& o) {
     sub(s.z, s.z, hh);
 }
 
+// ---- cooperative doubling (three lanes of one wave) ----
+// Broadcast lane `src`'s value to every lane (v_readlane into SGPRs).
+PA_DEV Fq from_lane(const Fq& x, int src) {
+    Fq r;
+#pragma unroll
+    for (int i = 0; i < 12; i++) r.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.w[i], src);
+    return r;
+}
+PA_DEV Fq2 from_lane(const Fq2& x, int src) {
+    Fq2 r;
+    r.c0 = from_lane(x.c0, src);
+    r.c1 = from_lane(x.c1, src);
+    return r;
+}
+
+// dbl-2009-l (ec.rs:296-354) with its seven products spread over three lanes
+// of one wave: the products form three dependent levels
+//   (A = X^2, B = Y^2, T = Y Z) -> (C = B^2, (X + B)^2, F = (3A)^2) -> E (D - X3)
+// so a doubling costs three product latencies instead of seven -- for the
+// one-lane serial chains (comb bases, MSM Horner step).  Every lane of the
+// wave must call it with the same point; every lane ends with the result,
+// the same field values as jac_double.
+template <class F>
+PA_DEV void jac_double_3lane(Jac<F>& p, int lane) {
+    if (is_zero(p.z)) return;  // uniform
+    F s1, s2, m;
+    s1 = lane == 0 ? p.x : p.y;
+    s2 = lane == 0 ? p.x : (lane == 1 ? p.y : p.z);
+    mul(m, s1, s2);
+    const F a = from_lane(m, 0), b = from_lane(m, 1), t = from_lane(m, 2);
+    F e, xb;
+    dbl(e, a);
+    add(e, e, a);
+    add(xb, p.x, b);
+    s1 = lane == 0 ? b : (lane == 1 ? xb : e);
+    sqr(m, s1);
+    const F c = from_lane(m, 0), dd = from_lane(m, 1), f = from_lane(m, 2);
+    F d;
+    sub(d, dd, a);
+    sub(d, d, c);
+    dbl(d, d);
+    dbl(p.z, t);
+    sub(p.x, f, d);
+    sub(p.x, p.x, d);
+    sub(p.y, d, p.x);
+    mul(p.y, p.y, e);
+    F c8;
+    dbl(c8, c);
+    dbl(c8, c8);
+    dbl(c8, c8);
+    sub(p.y, p.y, c8);
+}
+
 template <class F>
 PA_DEV void jac_negate(Jac<F>& p) {  // ec.rs:528-532
     if (!jac_is_zero(p)) neg(p.y, p.y);

@@ -86,49 +86,6 @@ __global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict_
 }
 
 // ---------------- fixed-base comb ----------------
-// Broadcast lane `src`'s Fq to every lane (v_readlane into SGPRs).
-PA_DEV Fq fq_from_lane(const Fq& x, int src) {
-    Fq r;
-#pragma unroll
-    for (int i = 0; i < 12; i++) r.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.w[i], src);
-    return r;
-}
-
-// dbl-2009-l (ec.rs:296-354) with its seven products spread over three lanes
-// of one wave: the products form three dependent levels
-//   (A = X^2, B = Y^2, T = Y Z) -> (C = B^2, (X + B)^2, F = (3A)^2) -> E (D - X3)
-// so a doubling costs three product latencies instead of seven.  Every lane
-// ends with the same point; the field values are the reference's.
-PA_DEV void jac_double_3lane(Jac<Fq>& p, int lane) {
-    if (fq_is_zero(p.z)) return;  // uniform
-    Fq s1, s2, m;
-    s1 = lane == 0 ? p.x : p.y;
-    s2 = lane == 0 ? p.x : (lane == 1 ? p.y : p.z);
-    fq_mul(m, s1, s2);
-    const Fq a = fq_from_lane(m, 0), b = fq_from_lane(m, 1), t = fq_from_lane(m, 2);
-    Fq e, xb;
-    fq_dbl(e, a);
-    fq_add(e, e, a);
-    fq_add(xb, p.x, b);
-    s1 = lane == 0 ? b : (lane == 1 ? xb : e);
-    fq_sqr(m, s1);
-    const Fq c = fq_from_lane(m, 0), dd = fq_from_lane(m, 1), f = fq_from_lane(m, 2);
-    Fq d;
-    fq_sub(d, dd, a);
-    fq_sub(d, d, c);
-    fq_dbl(d, d);
-    fq_dbl(p.z, t);
-    fq_sub(p.x, f, d);
-    fq_sub(p.x, p.x, d);
-    fq_sub(p.y, d, p.x);
-    fq_mul(p.y, p.y, e);
-    Fq c8;
-    fq_dbl(c8, c);
-    fq_dbl(c8, c8);
-    fq_dbl(c8, c8);
-    fq_sub(p.y, p.y, c8);
-}
-
 // B_i = 2^(8i) g for i = 0..32 (Jacobian): one wave, 256 sequential
 // doublings, three lanes per doubling.
 __global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases) {

@@ -24,7 +24,7 @@
 //   5. k_msm_segments: per window, sum_m m*B_m by running sums over segments of
 //      L buckets (T += B_m; S += T, top down), plus a*T for the segment offset.
 //   6. k_msm_group_sum (repeated): segment results -> one sum per window.
-//   7. k_msm_horner: one lane, sum_w 2^(c*w) S_w.
+//   7. k_msm_horner: one wave, sum_w 2^(c*w) S_w (doublings over three lanes).
 // Work: n*W mixed additions + ~2*W*2^(c-1) additions + ~256 doublings.
 #include <hipcub/hipcub.hpp>
 
@@ -283,18 +283,21 @@ __global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ 
                                                    uint64_t* __restrict__ out) {
     using F = typename Grp<G>::F;
     constexpr int JW = Grp<G>::JW;
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    // one wave; the doublings use three lanes (jac_double_3lane), every lane
+    // holds the same accumulator
+    if (blockIdx.x != 0) return;
+    const int lane = threadIdx.x;
     Jac<F> acc;
     load_jac(acc, wsum + (size_t)JW * (W - 1));
 #pragma unroll 1
     for (int w = (int)W - 2; w >= 0; w--) {
 #pragma unroll 1
-        for (uint32_t k = 0; k < c; k++) jac_double(acc);
+        for (uint32_t k = 0; k < c; k++) jac_double_3lane(acc, lane);
         Jac<F> x;
         load_jac(x, wsum + (size_t)JW * w);
         jac_add(acc, x);
     }
-    store_jac(out, acc);
+    if (lane == 0) store_jac(out, acc);
 }
 
 template <int G>

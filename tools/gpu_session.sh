@@ -36,6 +36,7 @@ for step in "$@"; do
         decbench) run bench_decode 300 python bench.py --workload decode --steps 5 --warmup 1 ;;
         newtests) run pytest_new 600 python -u -m pytest tests/test_fr.py tests/test_msm.py -m gpu -v --timeout 300 --timeout-method thread ;;
         frbench) run bench_fr 300 python bench.py --workload fr_mul --steps 20 --warmup 3 ;;
+        msmtests) run pytest_msm 600 python -u -m pytest tests/test_msm.py tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         msmbench) run bench_msm 400 python bench.py --workload msm --steps 5 --warmup 1 ;;
         profmsm) run prof_msm 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_msm -o run -- python bench.py --workload msm --steps 3 --warmup 1 --no-cpu-baseline ;;
         profwnaf) run prof_wnaf 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_wnaf -o run -- python bench.py --workload wnaf --steps 3 --warmup 1 --no-cpu-baseline ;;
