@@ -115,7 +115,7 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.c = msm_window_bits(n);
     p.W = (257 + p.c - 1) / p.c;
     p.B = 1u << (p.c - 1);
-    p.L = p.B < 32 ? p.B : 32;
+    p.L = p.B < 8 ? p.B : 8;  // short segments: the running sums are a latency chain per lane
     p.items = (size_t)p.W * n;
     const uint64_t sentinel = (uint64_t)p.W * p.B;
     p.key_bits = 1;
@@ -359,12 +359,12 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     const size_t nseg = (size_t)p.W * spw;
     hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(nseg, 64)), dim3(64), 0, s, buckets, p.B, p.L, nseg,
                        segs);
-    // segment sums -> one per window, 32 at a time (ping-pong segs <-> tmp)
+    // segment sums -> one per window, 4 at a time (ping-pong segs <-> tmp)
     uint32_t count = spw;
     uint64_t* src = segs;
     uint64_t* dst = tmp;
     while (count > 1) {
-        const uint32_t group = 32;
+        const uint32_t group = 4;  // shallow chains: 4 additions per level
         const uint32_t gpw = (count + group - 1) / group;
         hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks((size_t)p.W * gpw, 64)), dim3(64), 0, s, src, count,
                            group, gpw, p.W, dst);
