@@ -40,7 +40,7 @@ struct StreamCfg {
 };
 inline StreamCfg stream_cfg() {
     static const StreamCfg c = [] {
-        StreamCfg r{1024, 1};
+        StreamCfg r{4096, 1};
         if (const char* e = getenv("PA_STREAM_BLOCKS")) {
             const long v = strtol(e, nullptr, 10);
             if (v > 0) r.max_blocks = (size_t)v;

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 out=gpurun_out/stream_ab.txt
 : > $out
 for wl in fq_mul fr_mul; do
-  for cfg in "0 2048" "1 1024" "1 1536" "1 2048" "1 4096" "0 4096"; do
+  for cfg in "0 2048" "1 1024" "1 2048" "1 4096" "0 4096"; do
     set -- $cfg
     echo "=== $wl prefetch=$1 blocks=$2" >> $out
     PA_STREAM_PREFETCH=$1 PA_STREAM_BLOCKS=$2 timeout -k 10 120 python bench.py --workload $wl --steps 200 --warmup 10 --no-cpu-baseline >> $out 2>&1 || exit $?
