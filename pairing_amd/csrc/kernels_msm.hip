@@ -19,8 +19,10 @@
 //   2. hipcub radix sort of the W*n (key, value) pairs: each bucket's points
 //      become contiguous (stable, so the result is deterministic).
 //   3. k_msm_bucket_bounds: [start, end) per bucket from the sorted keys.
-//   4. k_msm_bucket_acc: one lane per bucket, mixed additions (madd-2007-bl)
-//      of the affine bases gathered from HBM (y negated for negative digits).
+//   4. k_msm_chunk_acc: one lane per 32 sorted items, mixed additions
+//      (madd-2007-bl) of the affine bases gathered from HBM (y negated for
+//      negative digits), run by run; k_msm_bucket_fix folds the pieces of
+//      buckets that span chunks and zeroes empty buckets.
 //   5. k_msm_segments: per window, sum_m m*B_m by running sums over segments of
 //      L buckets (T += B_m; S += T, top down), plus a*T for the segment offset.
 //   6. k_msm_group_sum (repeated): segment results -> one sum per window.
@@ -96,7 +98,7 @@ struct MsmPlan {
     uint32_t key_bits;          // radix-sort key width
     size_t items;               // W * n
     size_t off_keys_in, off_keys_out, off_vals_in, off_vals_out, off_start, off_end;
-    size_t off_buckets, off_segs, off_tmp, off_sort;
+    size_t off_buckets, off_segs, off_tmp, off_sort, off_cont;
     size_t sort_bytes, total;
 };
 
@@ -108,6 +110,9 @@ static inline uint32_t msm_window_bits(size_t n) {
     if (c > 16) c = 16;
     return (uint32_t)c;
 }
+
+// items (sorted (bucket, term) pairs) per lane of the bucket accumulation
+constexpr uint32_t kMsmChunk = 32;
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -133,6 +138,7 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.off_buckets = off; off = align256(off + jw * nb);
     p.off_segs = off; off = align256(off + jw * nseg);
     p.off_tmp = off; off = align256(off + jw * nseg);
+    p.off_cont = off; off = align256(off + jw * ((p.items + kMsmChunk - 1) / kMsmChunk));
     p.sort_bytes = 0;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, p.sort_bytes, (const uint32_t*)nullptr,
                                                       (uint32_t*)nullptr, (const uint32_t*)nullptr,
@@ -195,27 +201,86 @@ __global__ void __launch_bounds__(256) k_msm_bucket_bounds(const uint32_t* __res
     if (j + 1 == items || keys[j + 1] != k) end[k] = (uint32_t)(j + 1);
 }
 
+// Bucket accumulation, load-balanced: lane k owns the sorted items
+// [k T, (k+1) T) (T = kMsmChunk) and adds their bases run by run.  A run whose
+// bucket starts inside the chunk is written to the bucket; the chunk's first
+// run, when its bucket started in an earlier chunk, goes to cont[k] and is
+// folded in by k_msm_bucket_fix.  Every lane does at most T mixed additions
+// whatever the digit distribution (a window whose digits crowd into few
+// buckets -- the top window of scalars < r -- no longer makes a few lanes
+// walk hundreds of terms).
 template <int G>
-__global__ void __launch_bounds__(64) k_msm_bucket_acc(const uint64_t* __restrict__ bases,
-                                                       const uint32_t* __restrict__ vals,
-                                                       const uint32_t* __restrict__ start,
-                                                       const uint32_t* __restrict__ end, size_t nb,
-                                                       uint64_t* __restrict__ buckets) {
+PA_DEV void msm_flush(uint32_t key, const Jac<typename Grp<G>::F>& acc, size_t j0, size_t k,
+                      const uint32_t* __restrict__ start, uint64_t* __restrict__ buckets,
+                      uint64_t* __restrict__ cont) {
+    constexpr int JW = Grp<G>::JW;
+    if (start[key] >= j0) store_jac(buckets + (size_t)JW * key, acc);
+    else store_jac(cont + (size_t)JW * k, acc);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_msm_chunk_acc(const uint64_t* __restrict__ bases,
+                                                      const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ vals,
+                                                      const uint32_t* __restrict__ start, size_t items,
+                                                      uint32_t sentinel, uint64_t* __restrict__ buckets,
+                                                      uint64_t* __restrict__ cont) {
     using F = typename Grp<G>::F;
-    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t j0 = k * kMsmChunk;
+    if (j0 >= items) return;
+    const size_t j1 = (j0 + kMsmChunk < items) ? j0 + kMsmChunk : items;
+    uint32_t cur = keys[j0];
+    if (cur >= sentinel) return;  // zero digits sort last
     Jac<F> acc;
     jac_zero(acc);
-    const uint32_t e = end[b];
 #pragma unroll 1
-    for (uint32_t j = start[b]; j < e; j++) {
+    for (size_t j = j0; j < j1; j++) {
+        const uint32_t key = keys[j];
+        if (key >= sentinel) break;
+        if (key != cur) {
+            msm_flush<G>(cur, acc, j0, k, start, buckets, cont);
+            jac_zero(acc);
+            cur = key;
+        }
         const uint32_t v = vals[j];
         Aff<F> p;
         load_aff(p, bases + (size_t)Grp<G>::AW * (v & 0x7fffffffu));
         if (v >> 31) neg(p.y, p.y);
         jac_add_mixed(acc, p);
     }
-    store_jac(buckets + (size_t)Grp<G>::JW * b, acc);
+    msm_flush<G>(cur, acc, j0, k, start, buckets, cont);
+}
+
+// One lane per bucket: empty buckets become the identity; a bucket spanning
+// several chunks adds the continuation pieces of the chunks after its first.
+template <int G>
+__global__ void __launch_bounds__(64) k_msm_bucket_fix(const uint32_t* __restrict__ start,
+                                                       const uint32_t* __restrict__ end, size_t nb,
+                                                       const uint64_t* __restrict__ cont,
+                                                       uint64_t* __restrict__ buckets) {
+    using F = typename Grp<G>::F;
+    constexpr int JW = Grp<G>::JW;
+    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const uint32_t s = start[b], e = end[b];
+    if (s == e) {
+        Jac<F> z;
+        jac_zero(z);
+        store_jac(buckets + (size_t)JW * b, z);
+        return;
+    }
+    const size_t first = s / kMsmChunk, last = (e - 1) / kMsmChunk;
+    if (first == last) return;
+    Jac<F> acc;
+    load_jac(acc, buckets + (size_t)JW * b);
+#pragma unroll 1
+    for (size_t k = first + 1; k <= last; k++) {
+        Jac<F> x;
+        load_jac(x, cont + (size_t)JW * k);
+        jac_add(acc, x);
+    }
+    store_jac(buckets + (size_t)JW * b, acc);
 }
 
 // One lane per segment of L buckets of one window: sum_m m * B_m over the segment.
@@ -353,8 +418,11 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     if ((e = hipMemsetAsync(end, 0, 4 * nb, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_msm_bucket_bounds, dim3(msm_blocks(p.items, 256)), dim3(256), 0, s, keys_out, p.items,
                        p.W * p.B, start, end);
-    hipLaunchKernelGGL(k_msm_bucket_acc<G>, dim3(msm_blocks(nb, 64)), dim3(64), 0, s, bases, vals_out, start, end,
-                       nb, buckets);
+    uint64_t* cont = reinterpret_cast<uint64_t*>(base + p.off_cont);
+    const size_t nchunks = (p.items + kMsmChunk - 1) / kMsmChunk;
+    hipLaunchKernelGGL(k_msm_chunk_acc<G>, dim3(msm_blocks(nchunks, 64)), dim3(64), 0, s, bases, keys_out, vals_out,
+                       start, p.items, p.W * p.B, buckets, cont);
+    hipLaunchKernelGGL(k_msm_bucket_fix<G>, dim3(msm_blocks(nb, 64)), dim3(64), 0, s, start, end, nb, cont, buckets);
     const uint32_t spw = p.B / p.L;
     const size_t nseg = (size_t)p.W * spw;
     hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(nseg, 64)), dim3(64), 0, s, buckets, p.B, p.L, nseg,
