@@ -18,6 +18,7 @@
 // batch_normalization.  Montgomery's trick over chunks of CHUNK points per
 // lane with one Fermat inversion per chunk; zero and already-normalized points
 // are left bit-for-bit untouched, as in the reference (ec.rs:255-257, 271, 285).
+#include "fl.h"
 #include "launch.h"
 #include "pairing.h"
 
@@ -26,7 +27,7 @@ namespace pa {
 constexpr int kCombWindows = 33;      // 8-bit digits of a 255-bit scalar + final carry
 constexpr int kCombEntries = 128;     // |d| in 1..128
 constexpr int kG1Jac = 18;            // u64 words per Jacobian G1
-constexpr int kAffPair = 12;          // u64 words per table entry (x, y)
+constexpr int kFlPair = 14;           // u64 words per table entry: x, y as 14 x 28-bit limbs (lazy core)
 constexpr int kNormChunk = 8;         // points per lane in batch_normalization
 
 // ---------------- batch_normalization ----------------
@@ -86,21 +87,6 @@ __global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict_
 }
 
 // ---------------- fixed-base comb ----------------
-// B_i = 2^(8i) g for i = 0..32 (Jacobian): one wave, 256 sequential
-// doublings, three lanes per doubling.
-__global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases) {
-    if (blockIdx.x != 0) return;
-    const int lane = threadIdx.x;
-    Jac<Fq> p;
-    load_jac(p, base);
-#pragma unroll 1
-    for (int i = 0; i < kCombWindows; i++) {
-        if (lane == 0) store_jac(bases + kG1Jac * i, p);
-#pragma unroll 1
-        for (int k = 0; k < 8; k++) jac_double_3lane(p, lane);
-    }
-}
-
 // T[i][d-1] = d * B_i (Jacobian), one lane per entry: double-and-add over d's 8 bits.
 __global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict__ bases, uint64_t* __restrict__ table_jac) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -117,15 +103,129 @@ __global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict_
     store_jac(table_jac + (size_t)kG1Jac * e, acc);
 }
 
-// normalized Jacobian table -> packed affine (x, y)
-__global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table_aff) {
+// normalized Jacobian table -> affine (x, y) in the lazy 28-bit core's
+// representation (fl.h: 14 limbs, R = 2^392), 28 u32 per entry
+__global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table_fl) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= kCombWindows * kCombEntries) return;
-    for (int w = 0; w < kAffPair; w++) table_aff[(size_t)kAffPair * e + w] = table_jac[(size_t)kG1Jac * e + w];
+    const F<1> x = fl_load(table_jac + (size_t)kG1Jac * e);
+    const F<1> y = fl_load(table_jac + (size_t)kG1Jac * e + 6);
+    uint32_t* d = reinterpret_cast<uint32_t*>(table_fl + (size_t)kFlPair * e);
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+        d[i] = x.w[i];
+        d[14 + i] = y.w[i];
+    }
 }
 
-// s*g for n scalars (FrRepr, 4 x u64 canonical): out Jacobian.
-__global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__ table_aff,
+// ---- G1 Jacobian arithmetic on the lazy core (same field values as curve.h) ----
+struct FlJac {
+    F<1> x, y, z;
+};
+PA_DEV bool fl_eq(const F<1>& a, const F<1>& b) { return fl_is_zero(sub(a, b)); }
+
+// dbl-2009-l, ec.rs:296-354 (caller: z != 0)
+PA_DEV void fl_jac_double(FlJac& p) {
+    const F<1> a = sqr(p.x);
+    const F<1> b = sqr(p.y);
+    const F<1> c = sqr(b);
+    const F<1> d = red(dbl(sub(sqr(add(p.x, b)), add(a, c))));
+    const F<3> e = add(dbl(a), a);
+    const F<1> f = sqr(e);
+    p.z = red(dbl(mul(p.z, p.y)));
+    p.x = red(sub(f, dbl(d)));
+    p.y = red(sub(mul(e, sub(d, p.x)), dbl(dbl(dbl(c)))));
+}
+
+// madd-2007-bl, ec.rs:446-526: s += (ox, oy), (ox, oy) a nonzero affine point;
+// `untouched` marks the initial identity (the reference's zero()), a Jacobian
+// zero produced on the way (z == 0) is detected as jac_is_zero does
+PA_DEV void fl_jac_add_mixed(FlJac& s, bool& untouched, const F<1>& ox, const F<2>& oy) {
+    if (untouched || fl_is_zero(s.z)) {
+        s.x = ox;
+        s.y = red(oy);
+        s.z = fl_one();
+        untouched = false;
+        return;
+    }
+    const F<1> z1z1 = sqr(s.z);
+    const F<1> u2 = mul(ox, z1z1);
+    const F<1> s2 = mul(mul(oy, s.z), z1z1);
+    if (fl_eq(s.x, u2) && fl_eq(s.y, s2)) {
+        fl_jac_double(s);
+        return;
+    }
+    const F<3> h = sub(u2, s.x);
+    const F<1> hh = sqr(h);
+    const F<4> i = dbl(dbl(hh));
+    const F<1> j = mul(h, i);
+    const F<1> r = red(dbl(sub(s2, s.y)));
+    const F<1> v = mul(s.x, i);
+    const F<1> x3 = red(sub(sub(sub(sqr(r), j), v), v));
+    const F<1> y3 = red(sub(mul(r, sub(v, x3)), dbl(mul(j, s.y))));
+    const F<1> z3 = red(sub(sub(sqr(add(s.z, red(h))), z1z1), hh));
+    s.x = x3;
+    s.y = y3;
+    s.z = z3;
+}
+
+PA_DEV F<1> fl_from_lane(const F<1>& x, int src) {
+    F<1> r;
+#pragma unroll
+    for (int i = 0; i < 14; i++) r.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.w[i], src);
+    return r;
+}
+
+// jac_double_3lane (curve.h) on the lazy core: dbl-2009-l's seven products
+// in three dependent levels over lanes 0..2; every lane ends with the point.
+// Caller: z != 0.
+PA_DEV void fl_jac_double_3lane(FlJac& p, int lane) {
+    F<1> m = mul(lane == 0 ? p.x : p.y, lane == 0 ? p.x : (lane == 1 ? p.y : p.z));
+    const F<1> a = fl_from_lane(m, 0), b = fl_from_lane(m, 1), t = fl_from_lane(m, 2);
+    const F<3> e = add(dbl(a), a);
+    const F<3> s = lane == 0 ? relax<3>(b) : (lane == 1 ? relax<3>(add(p.x, b)) : e);
+    m = sqr(s);
+    const F<1> c = fl_from_lane(m, 0), dd = fl_from_lane(m, 1), f = fl_from_lane(m, 2);
+    const F<1> d = red(dbl(sub(dd, add(a, c))));
+    p.z = red(dbl(t));
+    p.x = red(sub(f, dbl(d)));
+    p.y = red(sub(mul(e, sub(d, p.x)), dbl(dbl(dbl(c)))));
+}
+
+// B_i = 2^(8i) g for i = 0..32 (Jacobian): one wave, 256 sequential
+// doublings on the lazy core, three lanes per doubling.  A zero base stays
+// zero (ec.rs:299-301); a nonzero point never doubles to zero (#E(Fq) is odd).
+__global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases) {
+    if (blockIdx.x != 0) return;
+    const int lane = threadIdx.x;
+    Jac<Fq> p0;
+    load_jac(p0, base);
+    if (fq_is_zero(p0.z)) {
+        if (lane == 0)
+            for (int i = 0; i < kCombWindows; i++) store_jac(bases + kG1Jac * i, p0);
+        return;
+    }
+    FlJac p;
+    p.x = fl_from_abi(p0.x);
+    p.y = fl_from_abi(p0.y);
+    p.z = fl_from_abi(p0.z);
+#pragma unroll 1
+    for (int i = 0; i < kCombWindows; i++) {
+        if (lane == 0) {
+            uint64_t* o = bases + kG1Jac * i;
+            fl_store(o, p.x);
+            fl_store(o + 6, p.y);
+            fl_store(o + 12, p.z);
+        }
+#pragma unroll 1
+        for (int k = 0; k < 8; k++) fl_jac_double_3lane(p, lane);
+    }
+}
+
+// s*g for n scalars (FrRepr, 4 x u64 canonical): out Jacobian.  Runs on the
+// lazy 28-bit core (fl.h): the mixed additions are the reference's formulas,
+// so the stored coordinates are the bits the 12-word core would produce.
+__global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__ table_fl,
                                                     const uint64_t* __restrict__ scalars,
                                                     uint64_t* __restrict__ out, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -133,8 +233,11 @@ __global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__
     uint64_t s[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
-    Jac<Fq> acc;
-    jac_zero(acc);
+    FlJac acc;
+    acc.x = fl_zero();
+    acc.y = fl_one();
+    acc.z = fl_zero();
+    bool untouched = true;
     int carry = 0;
 #pragma unroll 1
     for (int win = 0; win < kCombWindows; win++) {
@@ -144,16 +247,30 @@ __global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__
         if (d > 128) d -= 256;
         if (d != 0) {
             const int ad = d < 0 ? -d : d;
-            Aff<Fq> t;
-            const uint64_t* src = table_aff + (size_t)kAffPair * (win * kCombEntries + ad - 1);
-            fq_load(t.x, src);
-            fq_load(t.y, src + 6);
-            t.inf = false;
-            if (d < 0) fq_neg(t.y, t.y);
-            jac_add_mixed(acc, t);
+            const uint2* src = reinterpret_cast<const uint2*>(table_fl + (size_t)kFlPair * (win * kCombEntries + ad - 1));
+            F<1> tx, ty;
+#pragma unroll
+            for (int k = 0; k < 7; k++) {
+                const uint2 a = src[k], b = src[7 + k];
+                tx.w[2 * k] = a.x;
+                tx.w[2 * k + 1] = a.y;
+                ty.w[2 * k] = b.x;
+                ty.w[2 * k + 1] = b.y;
+            }
+            const F<2> oy = d < 0 ? neg(ty) : relax<2>(ty);
+            fl_jac_add_mixed(acc, untouched, tx, oy);
         }
     }
-    store_jac(out + (size_t)kG1Jac * i, acc);
+    uint64_t* o = out + (size_t)kG1Jac * i;
+    if (untouched) {
+        Jac<Fq> z;
+        jac_zero(z);
+        store_jac(o, z);
+    } else {
+        fl_store(o, acc.x);
+        fl_store(o + 6, acc.y);
+        fl_store(o + 12, acc.z);
+    }
 }
 
 static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -168,7 +285,7 @@ hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream) 
 size_t g1_comb_workspace_words() {
     return (size_t)kG1Jac * kCombWindows + (size_t)kG1Jac * kCombWindows * kCombEntries;
 }
-size_t g1_comb_table_words() { return (size_t)kAffPair * kCombWindows * kCombEntries; }
+size_t g1_comb_table_words() { return (size_t)kFlPair * kCombWindows * kCombEntries; }
 
 hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_aff, uint64_t* workspace, hipStream_t stream) {
     uint64_t* bases = workspace;
