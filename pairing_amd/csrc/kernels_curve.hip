@@ -18,7 +18,7 @@
 // batch_normalization.  Montgomery's trick over chunks of CHUNK points per
 // lane with one Fermat inversion per chunk; zero and already-normalized points
 // are left bit-for-bit untouched, as in the reference (ec.rs:255-257, 271, 285).
-#include "fl.h"
+#include "curve_fl.h"
 #include "launch.h"
 #include "pairing.h"
 
@@ -116,80 +116,6 @@ __global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict_
         d[i] = x.w[i];
         d[14 + i] = y.w[i];
     }
-}
-
-// ---- G1 Jacobian arithmetic on the lazy core (same field values as curve.h) ----
-struct FlJac {
-    F<1> x, y, z;
-};
-PA_DEV bool fl_eq(const F<1>& a, const F<1>& b) { return fl_is_zero(sub(a, b)); }
-
-// dbl-2009-l, ec.rs:296-354 (caller: z != 0)
-PA_DEV void fl_jac_double(FlJac& p) {
-    const F<1> a = sqr(p.x);
-    const F<1> b = sqr(p.y);
-    const F<1> c = sqr(b);
-    const F<1> d = red(dbl(sub(sqr(add(p.x, b)), add(a, c))));
-    const F<3> e = add(dbl(a), a);
-    const F<1> f = sqr(e);
-    p.z = red(dbl(mul(p.z, p.y)));
-    p.x = red(sub(f, dbl(d)));
-    p.y = red(sub(mul(e, sub(d, p.x)), dbl(dbl(dbl(c)))));
-}
-
-// madd-2007-bl, ec.rs:446-526: s += (ox, oy), (ox, oy) a nonzero affine point;
-// `untouched` marks the initial identity (the reference's zero()), a Jacobian
-// zero produced on the way (z == 0) is detected as jac_is_zero does
-PA_DEV void fl_jac_add_mixed(FlJac& s, bool& untouched, const F<1>& ox, const F<2>& oy) {
-    if (untouched || fl_is_zero(s.z)) {
-        s.x = ox;
-        s.y = red(oy);
-        s.z = fl_one();
-        untouched = false;
-        return;
-    }
-    const F<1> z1z1 = sqr(s.z);
-    const F<1> u2 = mul(ox, z1z1);
-    const F<1> s2 = mul(mul(oy, s.z), z1z1);
-    if (fl_eq(s.x, u2) && fl_eq(s.y, s2)) {
-        fl_jac_double(s);
-        return;
-    }
-    const F<3> h = sub(u2, s.x);
-    const F<1> hh = sqr(h);
-    const F<4> i = dbl(dbl(hh));
-    const F<1> j = mul(h, i);
-    const F<1> r = red(dbl(sub(s2, s.y)));
-    const F<1> v = mul(s.x, i);
-    const F<1> x3 = red(sub(sub(sub(sqr(r), j), v), v));
-    const F<1> y3 = red(sub(mul(r, sub(v, x3)), dbl(mul(j, s.y))));
-    const F<1> z3 = red(sub(sub(sqr(add(s.z, red(h))), z1z1), hh));
-    s.x = x3;
-    s.y = y3;
-    s.z = z3;
-}
-
-PA_DEV F<1> fl_from_lane(const F<1>& x, int src) {
-    F<1> r;
-#pragma unroll
-    for (int i = 0; i < 14; i++) r.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.w[i], src);
-    return r;
-}
-
-// jac_double_3lane (curve.h) on the lazy core: dbl-2009-l's seven products
-// in three dependent levels over lanes 0..2; every lane ends with the point.
-// Caller: z != 0.
-PA_DEV void fl_jac_double_3lane(FlJac& p, int lane) {
-    F<1> m = mul(lane == 0 ? p.x : p.y, lane == 0 ? p.x : (lane == 1 ? p.y : p.z));
-    const F<1> a = fl_from_lane(m, 0), b = fl_from_lane(m, 1), t = fl_from_lane(m, 2);
-    const F<3> e = add(dbl(a), a);
-    const F<3> s = lane == 0 ? relax<3>(b) : (lane == 1 ? relax<3>(add(p.x, b)) : e);
-    m = sqr(s);
-    const F<1> c = fl_from_lane(m, 0), dd = fl_from_lane(m, 1), f = fl_from_lane(m, 2);
-    const F<1> d = red(dbl(sub(dd, add(a, c))));
-    p.z = red(dbl(t));
-    p.x = red(sub(f, dbl(d)));
-    p.y = red(sub(mul(e, sub(d, p.x)), dbl(dbl(dbl(c)))));
 }
 
 // B_i = 2^(8i) g for i = 0..32 (Jacobian): one wave, 256 sequential

@@ -30,7 +30,7 @@
 // Work: n*W mixed additions + ~2*W*2^(c-1) additions + ~256 doublings.
 #include <hipcub/hipcub.hpp>
 
-#include "curve.h"
+#include "curve_fl.h"
 #include "launch_msm.h"
 
 namespace pa {
@@ -98,7 +98,7 @@ struct MsmPlan {
     uint32_t key_bits;          // radix-sort key width
     size_t items;               // W * n
     size_t off_keys_in, off_keys_out, off_vals_in, off_vals_out, off_start, off_end;
-    size_t off_buckets, off_segs, off_tmp, off_sort, off_cont;
+    size_t off_buckets, off_segs, off_tmp, off_sort, off_cont, off_basefl;
     size_t sort_bytes, total;
 };
 
@@ -139,6 +139,7 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.off_segs = off; off = align256(off + jw * nseg);
     p.off_tmp = off; off = align256(off + jw * nseg);
     p.off_cont = off; off = align256(off + jw * ((p.items + kMsmChunk - 1) / kMsmChunk));
+    p.off_basefl = off; off = align256(off + (group == 1 ? 4 * 28 * n : 0));
     p.sort_bytes = 0;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, p.sort_bytes, (const uint32_t*)nullptr,
                                                       (uint32_t*)nullptr, (const uint32_t*)nullptr,
@@ -250,6 +251,120 @@ __global__ void __launch_bounds__(64) k_msm_chunk_acc(const uint64_t* __restrict
         jac_add_mixed(acc, p);
     }
     msm_flush<G>(cur, acc, j0, k, start, buckets, cont);
+}
+
+// G1 on the lazy 28-bit core: the affine bases converted once per MSM
+// (x, y -> 28 u32; infinity stays in the ABI record) ...
+__global__ void __launch_bounds__(256) k_msm_bases_fl(const uint64_t* __restrict__ bases, size_t n,
+                                                      uint32_t* __restrict__ fl) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Aff<Fq> a;
+    load_aff(a, bases + (size_t)Grp<1>::AW * i);
+    const F<1> x = fl_from_abi(a.x), y = fl_from_abi(a.y);
+    uint32_t* d = fl + 28 * i;
+#pragma unroll
+    for (int k = 0; k < 14; k++) {
+        d[k] = x.w[k];
+        d[14 + k] = y.w[k];
+    }
+}
+
+PA_DEV void msm_flush_fl(uint32_t key, const FlJac& acc, bool untouched, size_t j0, size_t k,
+                         const uint32_t* __restrict__ start, uint64_t* __restrict__ buckets,
+                         uint64_t* __restrict__ cont) {
+    constexpr int JW = Grp<1>::JW;
+    uint64_t* o = start[key] >= j0 ? buckets + (size_t)JW * key : cont + (size_t)JW * k;
+    if (untouched) {
+        Jac<Fq> z;
+        jac_zero(z);
+        store_jac(o, z);
+    } else {
+        fl_store(o, acc.x);
+        fl_store(o + 6, acc.y);
+        fl_store(o + 12, acc.z);
+    }
+}
+
+// ... and k_msm_chunk_acc<1> with the lazy mixed addition (curve_fl.h);
+// bucket pieces leave in the ABI form the later phases read.
+__global__ void __launch_bounds__(64) k_msm_chunk_acc_fl(const uint64_t* __restrict__ bases,
+                                                         const uint32_t* __restrict__ basefl,
+                                                         const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ vals,
+                                                         const uint32_t* __restrict__ start, size_t items,
+                                                         uint32_t sentinel, uint64_t* __restrict__ buckets,
+                                                         uint64_t* __restrict__ cont) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t j0 = k * kMsmChunk;
+    if (j0 >= items) return;
+    const size_t j1 = (j0 + kMsmChunk < items) ? j0 + kMsmChunk : items;
+    uint32_t cur = keys[j0];
+    if (cur >= sentinel) return;
+    FlJac acc;
+    acc.x = fl_zero();
+    acc.y = fl_one();
+    acc.z = fl_zero();
+    bool untouched = true;
+    // software pipeline: the (key, value) pair two items ahead and the base
+    // of the next item are in flight while the current mixed addition runs
+    // (the bucket phase is bound by these dependent random gathers)
+    auto fetch = [&](size_t jj, uint32_t& kk, uint32_t& vv) {
+        kk = sentinel;
+        vv = 0;
+        if (jj < j1) {
+            kk = keys[jj];
+            vv = vals[jj];
+        }
+    };
+    auto gather = [&](uint32_t kk, uint32_t vv, F<1>& x, F<1>& y, bool& inf) {
+        inf = true;
+        if (kk < sentinel) {
+            const uint32_t idx = vv & 0x7fffffffu;
+            inf = (bases[(size_t)Grp<1>::AW * idx + 12] & 0xff) != 0;
+            const uint2* src = reinterpret_cast<const uint2*>(basefl + 28 * (size_t)idx);
+#pragma unroll
+            for (int q = 0; q < 7; q++) {
+                const uint2 a = src[q], b = src[7 + q];
+                x.w[2 * q] = a.x;
+                x.w[2 * q + 1] = a.y;
+                y.w[2 * q] = b.x;
+                y.w[2 * q + 1] = b.y;
+            }
+        }
+    };
+    uint32_t key0, v0, key1, v1;
+    fetch(j0, key0, v0);
+    fetch(j0 + 1, key1, v1);
+    F<1> tx, ty;
+    bool inf;
+    gather(key0, v0, tx, ty, inf);
+#pragma unroll 1
+    for (size_t j = j0; j < j1; j++) {
+        if (key0 >= sentinel) break;
+        uint32_t key2, v2;
+        fetch(j + 2, key2, v2);
+        F<1> nx, ny;
+        bool ninf;
+        gather(key1, v1, nx, ny, ninf);
+        if (key0 != cur) {
+            msm_flush_fl(cur, acc, untouched, j0, k, start, buckets, cont);
+            untouched = true;
+            cur = key0;
+        }
+        if (!inf) {  // an infinity base is add_assign_mixed's no-op
+            const F<2> oy = (v0 >> 31) ? neg(ty) : relax<2>(ty);
+            fl_jac_add_mixed(acc, untouched, tx, oy);
+        }
+        key0 = key1;
+        v0 = v1;
+        key1 = key2;
+        v1 = v2;
+        tx = nx;
+        ty = ny;
+        inf = ninf;
+    }
+    msm_flush_fl(cur, acc, untouched, j0, k, start, buckets, cont);
 }
 
 // One lane per bucket: empty buckets become the identity; a bucket spanning
@@ -420,8 +535,15 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
                        p.W * p.B, start, end);
     uint64_t* cont = reinterpret_cast<uint64_t*>(base + p.off_cont);
     const size_t nchunks = (p.items + kMsmChunk - 1) / kMsmChunk;
-    hipLaunchKernelGGL(k_msm_chunk_acc<G>, dim3(msm_blocks(nchunks, 64)), dim3(64), 0, s, bases, keys_out, vals_out,
-                       start, p.items, p.W * p.B, buckets, cont);
+    if constexpr (G == 1) {
+        uint32_t* basefl = reinterpret_cast<uint32_t*>(base + p.off_basefl);
+        hipLaunchKernelGGL(k_msm_bases_fl, dim3(msm_blocks(n, 256)), dim3(256), 0, s, bases, n, basefl);
+        hipLaunchKernelGGL(k_msm_chunk_acc_fl, dim3(msm_blocks(nchunks, 64)), dim3(64), 0, s, bases, basefl,
+                           keys_out, vals_out, start, p.items, p.W * p.B, buckets, cont);
+    } else {
+        hipLaunchKernelGGL(k_msm_chunk_acc<G>, dim3(msm_blocks(nchunks, 64)), dim3(64), 0, s, bases, keys_out,
+                           vals_out, start, p.items, p.W * p.B, buckets, cont);
+    }
     hipLaunchKernelGGL(k_msm_bucket_fix<G>, dim3(msm_blocks(nb, 64)), dim3(64), 0, s, start, end, nb, cont, buckets);
     const uint32_t spw = p.B / p.L;
     const size_t nseg = (size_t)p.W * spw;
