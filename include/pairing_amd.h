@@ -231,6 +231,11 @@ size_t pa_g1_fixed_base_workspace_words(void);
 int pa_g1_fixed_base_table_device(const pa_g1 *base, uint64_t *table, uint64_t *workspace, void *stream);
 int pa_g1_fixed_base_mul_device(const uint64_t *table, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
                                 void *stream);
+/* Wnaf::new().base(base, n).scalar(s_i) for every i (wnaf.rs:93-107, 169-178) in one call: table build and
+ * multiply with the table's serial base chain overlapped (a per-device side stream, ordered after `stream` by an
+ * event); the same output bits as pa_g1_fixed_base_table_device + pa_g1_fixed_base_mul_device. */
+int pa_g1_wnaf_fixed_base_device(const pa_g1 *base, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
+                                 uint64_t *table, uint64_t *workspace, void *stream);
 int pa_fq_mul_batch_device(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n, void *stream);
 int pa_fr_mul_batch_device(const pa_fr *a, const pa_fr *b, pa_fr *out, size_t n, void *stream);
 int pa_g1_multiexp_device(const pa_g1_affine *bases, const pa_fr_repr *s, size_t n, pa_g1 *out, void *workspace,

@@ -429,9 +429,8 @@ int pa_g1_wnaf_fixed_base(const pa_g1* base, const pa_fr_repr* scalars, size_t n
     PA_TRY(dt.alloc(8 * pa::g1_comb_table_words()), "hipMalloc");
     PA_TRY(dw.alloc(8 * pa::g1_comb_workspace_words()), "hipMalloc");
     PA_TRY(dout.alloc(sizeof(pa_g1) * n), "hipMalloc");
-    PA_TRY(pa::launch_g1_comb_table(db.as<uint64_t>(), dt.as<uint64_t>(), dw.as<uint64_t>(), nullptr),
-           "kernel launch");
-    PA_TRY(pa::launch_g1_comb_mul(dt.as<uint64_t>(), ds.as<uint64_t>(), dout.as<uint64_t>(), n, nullptr),
+    PA_TRY(pa::launch_g1_fixed_base(db.as<uint64_t>(), ds.as<uint64_t>(), dout.as<uint64_t>(), n, dt.as<uint64_t>(),
+                                    dw.as<uint64_t>(), nullptr),
            "kernel launch");
     PA_TRY(hipDeviceSynchronize(), "kernel execution");
     return download(out, dout, sizeof(pa_g1) * n);
@@ -468,6 +467,14 @@ int pa_g1_fixed_base_mul_device(const uint64_t* table, const pa_fr_repr* scalars
                                 void* stream) {
     if (n && (!table || !scalars || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     PA_TRY(pa::launch_g1_comb_mul(table, (const uint64_t*)scalars, (uint64_t*)out, n, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+int pa_g1_wnaf_fixed_base_device(const pa_g1* base, const pa_fr_repr* scalars, pa_g1* out, size_t n,
+                                 uint64_t* table, uint64_t* workspace, void* stream) {
+    if (n && (!base || !scalars || !out || !table || !workspace)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g1_fixed_base((const uint64_t*)base, (const uint64_t*)scalars, (uint64_t*)out, n, table,
+                                    workspace, (hipStream_t)stream),
            "kernel launch");
     return PA_OK;
 }

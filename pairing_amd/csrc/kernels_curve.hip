@@ -18,6 +18,8 @@
 // batch_normalization.  Montgomery's trick over chunks of CHUNK points per
 // lane with one Fermat inversion per chunk; zero and already-normalized points
 // are left bit-for-bit untouched, as in the reference (ec.rs:255-257, 271, 285).
+#include <mutex>
+
 #include "curve_fl.h"
 #include "launch.h"
 #include "pairing.h"
@@ -27,6 +29,7 @@ namespace pa {
 constexpr int kCombWindows = 33;      // 8-bit digits of a 255-bit scalar + final carry
 constexpr int kCombEntries = 128;     // |d| in 1..128
 constexpr int kG1Jac = 18;            // u64 words per Jacobian G1
+constexpr uint32_t kFlInfinity = 0xffffffffu;  // table entry marker: no lazy limb has all 32 bits set
 constexpr int kFlPair = 14;           // u64 words per table entry: x, y as 14 x 28-bit limbs (lazy core)
 constexpr int kNormChunk = 8;         // points per lane in batch_normalization
 
@@ -88,9 +91,10 @@ __global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict_
 
 // ---------------- fixed-base comb ----------------
 // T[i][d-1] = d * B_i (Jacobian), one lane per entry: double-and-add over d's 8 bits.
-__global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict__ bases, uint64_t* __restrict__ table_jac) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= kCombWindows * kCombEntries) return;
+__global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict__ bases, uint64_t* __restrict__ table_jac,
+                                                     int e0, int e1) {
+    const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= e1) return;
     const int i = e / kCombEntries, d = e % kCombEntries + 1;
     Jac<Fq> b, acc;
     load_jac(b, bases + kG1Jac * i);
@@ -105,30 +109,36 @@ __global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict_
 
 // normalized Jacobian table -> affine (x, y) in the lazy 28-bit core's
 // representation (fl.h: 14 limbs, R = 2^392), 28 u32 per entry
-__global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table_fl) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= kCombWindows * kCombEntries) return;
+__global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table_fl,
+                                                     int e0, int e1) {
+    const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= e1) return;
     const F<1> x = fl_load(table_jac + (size_t)kG1Jac * e);
     const F<1> y = fl_load(table_jac + (size_t)kG1Jac * e + 6);
+    Fq z;
+    fq_load(z, table_jac + (size_t)kG1Jac * e + 12);
+    const bool zero = fq_is_zero(z);  // e.g. every entry of a zero base: marked, skipped by the multiply
     uint32_t* d = reinterpret_cast<uint32_t*>(table_fl + (size_t)kFlPair * e);
 #pragma unroll
     for (int i = 0; i < 14; i++) {
-        d[i] = x.w[i];
-        d[14 + i] = y.w[i];
+        d[i] = zero ? kFlInfinity : x.w[i];
+        d[14 + i] = zero ? kFlInfinity : y.w[i];
     }
 }
 
-// B_i = 2^(8i) g for i = 0..32 (Jacobian): one wave, 256 sequential
-// doublings on the lazy core, three lanes per doubling.  A zero base stays
-// zero (ec.rs:299-301); a nonzero point never doubles to zero (#E(Fq) is odd).
-__global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases) {
+// B_i = 2^(8i) g for i in [w0, w1) (Jacobian): one wave, 8 sequential
+// doublings per base on the lazy core, three lanes per doubling, starting from
+// g (w0 = 0) or from B_(w0-1) already in `bases`.  A zero point stays zero
+// (ec.rs:299-301); a nonzero point never doubles to zero (#E(Fq) is odd).
+__global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases,
+                                                      int w0, int w1) {
     if (blockIdx.x != 0) return;
     const int lane = threadIdx.x;
     Jac<Fq> p0;
-    load_jac(p0, base);
+    load_jac(p0, w0 == 0 ? base : bases + kG1Jac * (w0 - 1));
     if (fq_is_zero(p0.z)) {
         if (lane == 0)
-            for (int i = 0; i < kCombWindows; i++) store_jac(bases + kG1Jac * i, p0);
+            for (int i = w0; i < w1; i++) store_jac(bases + kG1Jac * i, p0);
         return;
     }
     FlJac p;
@@ -136,42 +146,56 @@ __global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict
     p.y = fl_from_abi(p0.y);
     p.z = fl_from_abi(p0.z);
 #pragma unroll 1
-    for (int i = 0; i < kCombWindows; i++) {
+    for (int i = w0; i < w1; i++) {
+        if (i > 0) {
+#pragma unroll 1
+            for (int k = 0; k < 8; k++) fl_jac_double_3lane(p, lane);
+        }
         if (lane == 0) {
             uint64_t* o = bases + kG1Jac * i;
             fl_store(o, p.x);
             fl_store(o + 6, p.y);
             fl_store(o + 12, p.z);
         }
-#pragma unroll 1
-        for (int k = 0; k < 8; k++) fl_jac_double_3lane(p, lane);
     }
 }
 
 // s*g for n scalars (FrRepr, 4 x u64 canonical): out Jacobian.  Runs on the
 // lazy 28-bit core (fl.h): the mixed additions are the reference's formulas,
 // so the stored coordinates are the bits the 12-word core would produce.
+// Windows [w0, w1) only; `first` = the accumulator starts at zero, else it
+// continues from `out` (the previous window range's result, stored only if
+// this range added something -- so the bits match one full-range pass).
 __global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__ table_fl,
                                                     const uint64_t* __restrict__ scalars,
-                                                    uint64_t* __restrict__ out, size_t n) {
+                                                    uint64_t* __restrict__ out, size_t n, int w0, int w1,
+                                                    int first) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t s[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
+    uint64_t* o = out + (size_t)kG1Jac * i;
     FlJac acc;
-    acc.x = fl_zero();
-    acc.y = fl_one();
-    acc.z = fl_zero();
-    bool untouched = true;
+    bool untouched = true, changed = false;
+    if (first) {
+        acc.x = fl_zero();
+        acc.y = fl_one();
+        acc.z = fl_zero();
+    } else {
+        acc.x = fl_load(o);
+        acc.y = fl_load(o + 6);
+        acc.z = fl_load(o + 12);
+        untouched = false;  // a zero (z == 0) is caught by fl_jac_add_mixed
+    }
     int carry = 0;
 #pragma unroll 1
-    for (int win = 0; win < kCombWindows; win++) {
+    for (int win = 0; win < w1; win++) {
         int d = carry;
         if (win < 32) d += (int)((s[win >> 3] >> (8 * (win & 7))) & 0xff);
         carry = d > 128 ? 1 : 0;
         if (d > 128) d -= 256;
-        if (d != 0) {
+        if (d != 0 && win >= w0) {
             const int ad = d < 0 ? -d : d;
             const uint2* src = reinterpret_cast<const uint2*>(table_fl + (size_t)kFlPair * (win * kCombEntries + ad - 1));
             F<1> tx, ty;
@@ -183,11 +207,14 @@ __global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__
                 ty.w[2 * k] = b.x;
                 ty.w[2 * k + 1] = b.y;
             }
-            const F<2> oy = d < 0 ? neg(ty) : relax<2>(ty);
-            fl_jac_add_mixed(acc, untouched, tx, oy);
+            if (tx.w[0] != kFlInfinity) {  // adding the identity is add_assign_mixed's no-op
+                const F<2> oy = d < 0 ? neg(ty) : relax<2>(ty);
+                fl_jac_add_mixed(acc, untouched, tx, oy);
+                changed = true;
+            }
         }
     }
-    uint64_t* o = out + (size_t)kG1Jac * i;
+    if (!first && !changed) return;
     if (untouched) {
         Jac<Fq> z;
         jac_zero(z);
@@ -213,23 +240,87 @@ size_t g1_comb_workspace_words() {
 }
 size_t g1_comb_table_words() { return (size_t)kFlPair * kCombWindows * kCombEntries; }
 
-hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_aff, uint64_t* workspace, hipStream_t stream) {
+static hipError_t comb_table_range(const uint64_t* base, uint64_t* table_fl, uint64_t* workspace, int w0, int w1,
+                                   hipStream_t stream) {
     uint64_t* bases = workspace;
     uint64_t* table_jac = workspace + (size_t)kG1Jac * kCombWindows;
-    const int entries = kCombWindows * kCombEntries;
-    hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, stream, base, bases);
-    hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(entries, 64)), dim3(64), 0, stream, bases, table_jac);
-    hipError_t e = launch_g1_batch_normalize(table_jac, entries, stream);
+    const int e0 = w0 * kCombEntries, e1 = w1 * kCombEntries;
+    hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, stream, base, bases, w0, w1);
+    hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, stream, bases, table_jac, e0, e1);
+    const hipError_t e = launch_g1_batch_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(entries, 64)), dim3(64), 0, stream, table_jac, table_aff);
+    hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, stream, table_jac, table_fl, e0,
+                       e1);
     return hipGetLastError();
 }
 
-hipError_t launch_g1_comb_mul(const uint64_t* table_aff, const uint64_t* scalars, uint64_t* out, size_t n,
+hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_fl, uint64_t* workspace, hipStream_t stream) {
+    return comb_table_range(base, table_fl, workspace, 0, kCombWindows, stream);
+}
+
+hipError_t launch_g1_comb_mul(const uint64_t* table_fl, const uint64_t* scalars, uint64_t* out, size_t n,
                               hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_aff, scalars, out, n);
+    hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_fl, scalars, out, n, 0,
+                       kCombWindows, 1);
     return hipGetLastError();
+}
+
+// Table + multiply with the serial base chain overlapped: the table is built
+// in two window halves on a side stream; the multiply over the low half runs
+// on `stream` while the side stream is still doubling toward the high half's
+// bases.  Same result bits as launch_g1_comb_table + launch_g1_comb_mul.
+hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
+                                uint64_t* table_fl, uint64_t* workspace, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    static std::mutex mu;
+    static hipStream_t side[64] = {};
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!side[dev] && (e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking)) != hipSuccess) return e;
+    }
+    hipStream_t aux = side[dev];
+    constexpr int kSplit = 17;  // windows [0, 17) need 128 doublings, [17, 33) another 128
+    hipEvent_t ev[3] = {};
+    int made = 0;
+    hipError_t err = hipSuccess;
+    auto ck = [&](hipError_t x) {
+        if (err == hipSuccess) err = x;
+        return err == hipSuccess;
+    };
+    for (; made < 3; made++)
+        if (!ck(hipEventCreateWithFlags(&ev[made], hipEventDisableTiming))) break;
+    uint64_t* bases = workspace;
+    uint64_t* table_jac = workspace + (size_t)kG1Jac * kCombWindows;
+    const int e1 = kSplit * kCombEntries;
+    if (ck(hipEventRecord(ev[0], stream)) && ck(hipStreamWaitEvent(aux, ev[0], 0))) {
+        // side stream: the low half's bases, then the whole high half of the table
+        hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, aux, base, bases, 0, kSplit);
+        if (ck(hipGetLastError()) && ck(hipEventRecord(ev[1], aux)) &&
+            ck(comb_table_range(base, table_fl, workspace, kSplit, kCombWindows, aux)) &&
+            ck(hipEventRecord(ev[2], aux)) && ck(hipStreamWaitEvent(stream, ev[1], 0))) {
+            // caller's stream: low half of the table, low-half multiply, then the high half
+            hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(e1, 64)), dim3(64), 0, stream, bases, table_jac, 0,
+                               e1);
+            if (ck(hipGetLastError()) && ck(launch_g1_batch_normalize(table_jac, e1, stream))) {
+                hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1, 64)), dim3(64), 0, stream, table_jac,
+                                   table_fl, 0, e1);
+                hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_fl, scalars,
+                                   out, n, 0, kSplit, 1);
+                if (ck(hipGetLastError()) && ck(hipStreamWaitEvent(stream, ev[2], 0))) {
+                    hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_fl,
+                                       scalars, out, n, kSplit, kCombWindows, 0);
+                    ck(hipGetLastError());
+                }
+            }
+        }
+    }
+    for (int k = 0; k < made; k++) (void)hipEventDestroy(ev[k]);
+    return err;
 }
 
 }  // namespace pa

@@ -103,6 +103,10 @@ size_t g1_comb_workspace_words();
 hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_aff, uint64_t* workspace, hipStream_t stream);
 hipError_t launch_g1_comb_mul(const uint64_t* table_aff, const uint64_t* scalars, uint64_t* out, size_t n,
                               hipStream_t stream);
+// both in one call, the table's serial base chain overlapped with the multiply
+// (a side stream per device; same result bits)
+hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
+                                uint64_t* table, uint64_t* workspace, hipStream_t stream);
 
 // Scalar field Fr (kernels_fr.hip).  `flag` receives the Option / Result byte
 // (inverse, from_repr, sqrt) or the LegendreSymbol as int8 (0, 1, -1);

@@ -70,6 +70,22 @@ def g1_fixed_base_mul(table, scalars, out, stream=None):
          _dptr(out, W_G1, "out"), scalars.shape[0], _stream_ptr(stream))
 
 
+def g1_wnaf_fixed_base(base, scalars, out, table, ws, stream=None):
+    """out[i] = scalars[i] * base with the table built in the same call (its
+    serial base chain overlapped with the multiply); table / ws as returned by
+    fixed_base_buffers()."""
+    call("pa_g1_wnaf_fixed_base_device", _dptr(base, W_G1, "base"), _dptr(scalars, 4, "scalars"),
+         _dptr(out, W_G1, "out"), scalars.shape[0], ctypes.c_void_p(table.data_ptr()),
+         ctypes.c_void_p(ws.data_ptr()), _stream_ptr(stream))
+
+
+def fixed_base_buffers(dev):
+    """(table, workspace) device buffers for g1_wnaf_fixed_base."""
+    table = torch.empty(int(_lib.pa_g1_fixed_base_table_words()), dtype=torch.int64, device=dev)
+    ws = torch.empty(int(_lib.pa_g1_fixed_base_workspace_words()), dtype=torch.int64, device=dev)
+    return table, ws
+
+
 def g1_batch_normalization(v, stream=None):
     call("pa_g1_batch_normalization_device", _dptr(v, W_G1, "v"), v.shape[0], _stream_ptr(stream))
 

@@ -295,3 +295,33 @@ def test_g1_config3_full_size_properties(gpu, oracle):
     lhs = oracle.g1_add(np.ascontiguousarray(got[i]), np.ascontiguousarray(got[j]))
     rhs = oracle.g1_wnaf_fixed_base(base, ssum, NT)
     assert oracle.g1_eq(lhs, rhs).all()
+
+
+@pytest.mark.parametrize("zero_base", [False, True])
+def test_g1_fixed_base_overlapped_halves(gpu, oracle, zero_base):
+    """pa_g1_wnaf_fixed_base runs the table build overlapped with the multiply
+    (side stream, window halves [0, 17) and [17, 33)): equal as points to the
+    reference's wNAF for scalars whose nonzero digits sit in one half only,
+    digit/carry edges at the split, and the zero base (ec.rs:299-301)."""
+    g = rng(53)
+    base = oracle.g1_mul_generator_jacobian(random_scalars(g, 1))
+    if zero_base:
+        base[0, 12:18] = 0
+    s = random_scalars(g, 3000)
+    s[0] = 0
+    s[1] = limbs(1, 4)
+    s[2] = limbs(R_ORDER - 1, 4)
+    # (not 2^256 - 1: the reference's wnaf_form adds 2^w to the repr with
+    # add_nocarry, which wraps for reprs this close to 2^256 -- a value no
+    # Fr::into_repr produces; the GPU computes s * base there)
+    s[3] = limbs((1 << 255) - 1, 4)
+    s[4] = limbs(1 << 200, 4)          # only the high half
+    s[5] = limbs((1 << 130) - 1, 4)    # low half + carry into window 17
+    s[6] = limbs(0x80 << 128, 4)       # digit 128 at window 16, no carry
+    s[7] = limbs(0x81 << 128, 4)       # digit -127 at window 16, carry into window 17
+    got = gpu.g1_wnaf_fixed_base(base, s)
+    k = 256
+    exp = oracle.g1_wnaf_fixed_base(base, np.ascontiguousarray(s[:k]), NT)
+    assert oracle.g1_eq(got[:k], exp).all()
+    if not zero_base:  # a zero base gives zeros whose (x, y) bits are whatever the add chain copied (ec.rs:398)
+        np.testing.assert_array_equal(gpu.g1_batch_normalization(got[:k]), oracle.g1_batch_normalization(exp))
