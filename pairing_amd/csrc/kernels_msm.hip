@@ -480,6 +480,37 @@ __global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ 
     if (lane == 0) store_jac(out, acc);
 }
 
+// G1 Horner with the doublings on the lazy core (fl_jac_double_3lane); the
+// window sums are added with the 12-word jac_add, so the accumulator crosses
+// between the representations once per window.  #E(Fq) is odd, so a nonzero
+// accumulator never doubles to zero and a zero one stays zero.
+__global__ void __launch_bounds__(64) k_msm_horner_fl(const uint64_t* __restrict__ wsum, uint32_t W, uint32_t c,
+                                                      uint64_t* __restrict__ out) {
+    constexpr int JW = Grp<1>::JW;
+    if (blockIdx.x != 0) return;
+    const int lane = threadIdx.x;
+    Jac<Fq> acc;
+    load_jac(acc, wsum + (size_t)JW * (W - 1));
+#pragma unroll 1
+    for (int w = (int)W - 2; w >= 0; w--) {
+        if (!jac_is_zero(acc)) {
+            FlJac p;
+            p.x = fl_from_abi(acc.x);
+            p.y = fl_from_abi(acc.y);
+            p.z = fl_from_abi(acc.z);
+#pragma unroll 1
+            for (uint32_t k = 0; k < c; k++) fl_jac_double_3lane(p, lane);
+            acc.x = fl_to_abi(p.x);
+            acc.y = fl_to_abi(p.y);
+            acc.z = fl_to_abi(p.z);
+        }
+        Jac<Fq> x;
+        load_jac(x, wsum + (size_t)JW * w);
+        jac_add(acc, x);
+    }
+    if (lane == 0) store_jac(out, acc);
+}
+
 template <int G>
 __global__ void __launch_bounds__(64) k_jac_zero_out(uint64_t* __restrict__ out) {
     using F = typename Grp<G>::F;
@@ -563,7 +594,10 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
         src = dst;
         dst = t;
     }
-    hipLaunchKernelGGL(k_msm_horner<G>, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
+    if constexpr (G == 1)
+        hipLaunchKernelGGL(k_msm_horner_fl, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
+    else
+        hipLaunchKernelGGL(k_msm_horner<G>, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
     (void)JW;
     return hipGetLastError();
 }
