@@ -203,14 +203,47 @@ __constant__ const uint64_t kPsiY1[6] = {0x7bcfa7a25aa30fdaULL, 0xdc17dec12a927e
                                          0xd1ca2087da74d4a7ULL, 0x2da2596696cebc1dULL, 0x0e2b7eedbbfd87d2ULL};
 constexpr uint64_t kAbsX = 0xd201000000010000ULL;
 
-// r = [|x|] p: MSB-first double-and-add (63 doublings, 5 additions)
+// dbl-2009-l (ec.rs:296-354) on the lazy core for G1 (E = F<1>) and G2
+// (E = F2<1>): the same field values as jac_double for a nonzero point
+template <class E>
+struct FlJacE {
+    E x, y, z;
+};
+template <class E>
+PA_DEV void fl_double_any(FlJacE<E>& p) {
+    const auto a = sqr(p.x);
+    const auto b = sqr(p.y);
+    const auto c = sqr(b);
+    const auto d = red(dbl(sub(sqr(add(p.x, b)), add(a, c))));
+    const auto e = red(add(dbl(a), a));
+    const auto f = sqr(e);
+    p.z = red(dbl(mul(p.z, p.y)));
+    p.x = red(sub(f, dbl(d)));
+    p.y = red(sub(mul(e, sub(d, p.x)), dbl(dbl(dbl(c)))));
+}
+
+// r = [|x|] p: MSB-first double-and-add (63 doublings, 5 additions).  The runs
+// of doublings between set bits go through the lazy core; the 5 additions use
+// the 12-word jac_add.  A zero point (z = 0) stays zero under either doubling
+// and is all the callers look at, so the yes/no result is the 12-word one.
 template <class F>
 __device__ __noinline__ void mul_abs_x(Jac<F>& r, const Jac<F>& p) {
     r = p;  // bit 63
+    int bit = 62;
 #pragma unroll 1
-    for (int bit = 62; bit >= 0; bit--) {
-        jac_double(r);
-        if ((kAbsX >> bit) & 1) jac_add(r, p);
+    while (bit >= 0) {
+        int stop = bit;  // the run ends at the next set bit (or bit 0)
+        while (stop > 0 && !((kAbsX >> stop) & 1)) stop--;
+        if (!jac_is_zero(r)) {
+            FlJacE<decltype(to_fl(r.x))> t{to_fl(r.x), to_fl(r.y), to_fl(r.z)};
+#pragma unroll 1
+            for (int k = bit; k >= stop; k--) fl_double_any(t);
+            from_fl(r.x, t.x);
+            from_fl(r.y, t.y);
+            from_fl(r.z, t.z);
+        }
+        if ((kAbsX >> stop) & 1) jac_add(r, p);
+        bit = stop - 1;
     }
 }
 
