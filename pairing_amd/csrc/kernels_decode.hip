@@ -62,7 +62,7 @@ PA_DEV void from_fl(Fq2& r, const F2<1>& a) {
     r.c1 = fl_to_abi(a.c1);
 }
 template <class F>
-__device__ __noinline__ void pow_fixed(F& r, const F& a, const uint64_t* e, int top) {
+__device__ __forceinline__ void pow_fixed(F& r, const F& a, const uint64_t* e, int top) {
     const auto x = to_fl(a);
     auto acc = x;
 #pragma unroll 1
@@ -227,7 +227,7 @@ PA_DEV void fl_double_any(FlJacE<E>& p) {
 // the 12-word jac_add.  A zero point (z = 0) stays zero under either doubling
 // and is all the callers look at, so the yes/no result is the 12-word one.
 template <class F>
-__device__ __noinline__ void mul_abs_x(Jac<F>& r, const Jac<F>& p) {
+__device__ __forceinline__ void mul_abs_x(Jac<F>& r, const Jac<F>& p) {
     r = p;  // bit 63
     int bit = 62;
 #pragma unroll 1
@@ -291,7 +291,7 @@ PA_DEV bool in_subgroup_endo(const Aff<Fq2>& a) {
 }
 
 template <class F>
-__device__ __noinline__ bool in_subgroup(const Aff<F>& a) {
+__device__ __forceinline__ bool in_subgroup(const Aff<F>& a) {
     if (a.inf) return true;
     return in_subgroup_endo(a);
 }
