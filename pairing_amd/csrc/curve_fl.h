@@ -61,6 +61,47 @@ PA_DEV void fl_jac_add_mixed(FlJac& s, bool& untouched, const F<1>& ox, const F<
     s.z = z3;
 }
 
+// add-2007-bl, ec.rs:356-444 (doubles when the points are equal); zero is
+// z == 0, as jac_is_zero
+PA_DEV void fl_jac_add(FlJac& s, const FlJac& o) {
+    if (fl_is_zero(s.z)) {
+        s = o;
+        return;
+    }
+    if (fl_is_zero(o.z)) return;
+    const F<1> z1z1 = sqr(s.z), z2z2 = sqr(o.z);
+    const F<1> u1 = mul(s.x, z2z2), u2 = mul(o.x, z1z1);
+    const F<1> s1 = mul(mul(s.y, o.z), z2z2), s2 = mul(mul(o.y, s.z), z1z1);
+    if (fl_eq(u1, u2) && fl_eq(s1, s2)) {
+        fl_jac_double(s);
+        return;
+    }
+    const F<3> h = sub(u2, u1);
+    const F<1> i = sqr(red(dbl(h)));
+    const F<1> j = mul(h, i);
+    const F<1> r = red(dbl(sub(s2, s1)));
+    const F<1> v = mul(u1, i);
+    const F<1> x3 = red(sub(sub(sub(sqr(r), j), v), v));
+    const F<1> y3 = red(sub(mul(r, sub(v, x3)), dbl(mul(s1, j))));
+    const F<1> z3 = mul(red(sub(sub(sqr(add(s.z, o.z)), z1z1), z2z2)), h);
+    s.x = x3;
+    s.y = y3;
+    s.z = z3;
+}
+
+PA_DEV FlJac fl_load_jac(const uint64_t* p) {
+    FlJac r;
+    r.x = fl_load(p);
+    r.y = fl_load(p + 6);
+    r.z = fl_load(p + 12);
+    return r;
+}
+PA_DEV void fl_store_jac(uint64_t* p, const FlJac& a) {
+    fl_store(p, a.x);
+    fl_store(p + 6, a.y);
+    fl_store(p + 12, a.z);
+}
+
 PA_DEV F<1> fl_from_lane(const F<1>& x, int src) {
     F<1> r;
 #pragma unroll

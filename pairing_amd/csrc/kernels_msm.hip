@@ -480,35 +480,58 @@ __global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ 
     if (lane == 0) store_jac(out, acc);
 }
 
-// G1 Horner with the doublings on the lazy core (fl_jac_double_3lane); the
-// window sums are added with the 12-word jac_add, so the accumulator crosses
-// between the representations once per window.  #E(Fq) is odd, so a nonzero
-// accumulator never doubles to zero and a zero one stays zero.
+// G1 Horner entirely on the lazy core: doublings over three lanes
+// (fl_jac_double_3lane), window sums added with fl_jac_add.  #E(Fq) is odd,
+// so a nonzero accumulator never doubles to zero and a zero one is skipped.
 __global__ void __launch_bounds__(64) k_msm_horner_fl(const uint64_t* __restrict__ wsum, uint32_t W, uint32_t c,
                                                       uint64_t* __restrict__ out) {
     constexpr int JW = Grp<1>::JW;
     if (blockIdx.x != 0) return;
     const int lane = threadIdx.x;
-    Jac<Fq> acc;
-    load_jac(acc, wsum + (size_t)JW * (W - 1));
+    FlJac acc = fl_load_jac(wsum + (size_t)JW * (W - 1));
 #pragma unroll 1
     for (int w = (int)W - 2; w >= 0; w--) {
-        if (!jac_is_zero(acc)) {
-            FlJac p;
-            p.x = fl_from_abi(acc.x);
-            p.y = fl_from_abi(acc.y);
-            p.z = fl_from_abi(acc.z);
+        if (!fl_is_zero(acc.z)) {
 #pragma unroll 1
-            for (uint32_t k = 0; k < c; k++) fl_jac_double_3lane(p, lane);
-            acc.x = fl_to_abi(p.x);
-            acc.y = fl_to_abi(p.y);
-            acc.z = fl_to_abi(p.z);
+            for (uint32_t k = 0; k < c; k++) fl_jac_double_3lane(acc, lane);
         }
-        Jac<Fq> x;
-        load_jac(x, wsum + (size_t)JW * w);
-        jac_add(acc, x);
+        fl_jac_add(acc, fl_load_jac(wsum + (size_t)JW * w));
     }
-    if (lane == 0) store_jac(out, acc);
+    if (lane == 0) fl_store_jac(out, acc);
+}
+
+// k_msm_segments<1> on the lazy core (same sums, same formulas)
+__global__ void __launch_bounds__(64) k_msm_segments_fl(const uint64_t* __restrict__ buckets, uint32_t B, uint32_t L,
+                                                        size_t nseg, uint64_t* __restrict__ segs) {
+    constexpr int JW = Grp<1>::JW;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg) return;
+    const uint32_t spw = B / L;
+    const size_t w = t / spw;
+    const uint32_t j = (uint32_t)(t % spw);
+    const uint64_t* bw = buckets + (size_t)JW * (w * B);
+    FlJac T, S;
+    T.x = fl_zero();
+    T.y = fl_one();
+    T.z = fl_zero();
+    S = T;
+#pragma unroll 1
+    for (uint32_t m = (j + 1) * L; m > j * L; m--) {  // magnitudes (j*L, (j+1)*L], top down
+        fl_jac_add(T, fl_load_jac(bw + (size_t)JW * (m - 1)));
+        fl_jac_add(S, T);
+    }
+    const uint32_t a = j * L;  // S = sum (m - a) B_m; add a * T
+    if (a && !fl_is_zero(T.z)) {
+        FlJac aT = T;  // top set bit of a
+        const int top = 31 - __clz(a);
+#pragma unroll 1
+        for (int bit = top - 1; bit >= 0; bit--) {
+            fl_jac_double(aT);
+            if ((a >> bit) & 1) fl_jac_add(aT, T);
+        }
+        fl_jac_add(S, aT);
+    }
+    fl_store_jac(segs + (size_t)JW * t, S);
 }
 
 template <int G>
@@ -578,8 +601,12 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     hipLaunchKernelGGL(k_msm_bucket_fix<G>, dim3(msm_blocks(nb, 64)), dim3(64), 0, s, start, end, nb, cont, buckets);
     const uint32_t spw = p.B / p.L;
     const size_t nseg = (size_t)p.W * spw;
-    hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(nseg, 64)), dim3(64), 0, s, buckets, p.B, p.L, nseg,
-                       segs);
+    if constexpr (G == 1)
+        hipLaunchKernelGGL(k_msm_segments_fl, dim3(msm_blocks(nseg, 64)), dim3(64), 0, s, buckets, p.B, p.L, nseg,
+                           segs);
+    else
+        hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(nseg, 64)), dim3(64), 0, s, buckets, p.B, p.L, nseg,
+                           segs);
     // segment sums -> one per window, 4 at a time (ping-pong segs <-> tmp)
     uint32_t count = spw;
     uint64_t* src = segs;
