@@ -387,6 +387,13 @@ __global__ void __launch_bounds__(64) k_msm_bucket_fix(const uint32_t* __restric
     }
     const size_t first = s / kMsmChunk, last = (e - 1) / kMsmChunk;
     if (first == last) return;
+    if constexpr (G == 1) {  // lazy core, same formulas and values
+        FlJac acc = fl_load_jac(buckets + (size_t)JW * b);
+#pragma unroll 1
+        for (size_t k = first + 1; k <= last; k++) fl_jac_add(acc, fl_load_jac(cont + (size_t)JW * k));
+        fl_store_jac(buckets + (size_t)JW * b, acc);
+        return;
+    }
     Jac<F> acc;
     load_jac(acc, buckets + (size_t)JW * b);
 #pragma unroll 1
