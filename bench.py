@@ -2,7 +2,10 @@
 """Benchmark: BLS12-381 pairings/sec at batch 2^16 per GPU (BASELINE.json).
 
   python bench.py --gpus N --steps K --warmup W
-  (N > 1: launched by torch.distributed.run, one rank per GPU over RCCL)
+  (N > 1: one rank per GPU over RCCL.  Under torch.distributed.run the ranks
+  come from WORLD_SIZE/RANK/LOCAL_RANK; run directly with N > 1, bench.py
+  first checks that N devices are visible and then starts the N ranks itself
+  as a torch.distributed.run child, before anything touches the GPU.)
 
 A step = one batch of 2^16 independent pairings e(P_i, Q_i) per GPU, inputs
 (G1Affine, G2Affine records) already resident in HBM: the fused
@@ -51,7 +54,39 @@ def parse():
     ap.add_argument("--workload", choices=["pairing", "fq_mul", "fr_mul", "wnaf", "decode", "msm"], default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-stub", action="store_true",
+                    help="launcher test only: gloo ranks on the CPU, the oracle as the per-rank compute "
+                         "(tests/test_bench_launcher.py); not a measurement")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 without a torch.distributed.run environment: start the N
+    ranks as a child torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1) and return its exit code.  Nothing here touches the GPU:
+    torch.cuda.device_count() does not initialise it on this image.  Returns
+    None when this process is itself a rank (or N == 1)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    if not args.cpu_stub:
+        import torch
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print("bench.py: --gpus %d but only %d device(s) visible" % (args.gpus, visible), file=sys.stderr)
+            return 2
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    return subprocess.call(cmd)
 
 
 def dist_env():
@@ -78,36 +113,53 @@ def make_pairs(n, rank, seed=0):
     return p, q
 
 
-def cpu_baseline_pairing(p, q, seconds):
-    """Time the oracle (C restatement of the reference) on this host."""
-    from oracle import binding as oracle
+def host_threads():
+    """(host cores this process may run on, threads the CPU baseline uses):
+    the affinity mask, capped by OMP_NUM_THREADS when the environment sets it
+    (the GPU box sets 16, its CPU share per GPU)."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        host = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
-    # calibrate on a small sample, then size the sample to ~`seconds` of CPU work
+        host = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(host, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else host
+    return host, max(1, threads)
+
+
+def _timed_pairings(oracle, p, q, threads, seconds):
+    """pairings/s of the oracle on `threads` threads over a prefix of (p, q)
+    sized from a calibration run to about `seconds` of wall time"""
+    k = min(len(p), max(threads, 2 * threads))
     t0 = time.perf_counter()
-    oracle.pairing(p[:threads], q[:threads], threads)
-    dt = time.perf_counter() - t0
-    per_pair_cpu = dt * threads / threads  # wall per pair-per-thread
-    n = int(max(threads, min(len(p), seconds / max(per_pair_cpu, 1e-4))))
+    oracle.pairing(p[:k], q[:k], threads)
+    per = max(time.perf_counter() - t0, 1e-4) / k           # wall per pairing at this thread count
+    n = int(max(k, min(len(p), seconds / per)))
     t0 = time.perf_counter()
     oracle.pairing(p[:n], q[:n], threads)
     wall = time.perf_counter() - t0
-    return {"value": n / wall, "unit": "pairings/s", "cores": threads, "kind": "port",
-            "sample": "%d pairings of the same synthetic batch, C restatement of the reference "
-                      "(oracle/), OpenMP over pairs, %.1f s wall" % (n, wall)}
+    return n / wall, n, wall
+
+
+def cpu_baseline_pairing(p, q, seconds):
+    """The oracle (C restatement of the reference's pairing, OpenMP over
+    pairs) on this host: one core, then every thread the host gives us."""
+    from oracle import binding as oracle
+    host, threads = host_threads()
+    v1, n1, w1 = _timed_pairings(oracle, p, q, 1, max(5.0, seconds / 2))
+    vt, nt, wt = (v1, n1, w1) if threads == 1 else _timed_pairings(oracle, p, q, threads, max(5.0, seconds / 2))
+    return {"value": vt, "unit": "pairings/s", "cores": threads, "kind": "port", "host_cores": host,
+            "value_1core": v1,
+            "sample": "C restatement of the reference (oracle/) over a prefix of the same synthetic batch: "
+                      "%d pairings on 1 core in %.1f s; %d pairings on %d threads (OpenMP over pairs) in %.1f s; "
+                      "host affinity %d cores%s" % (n1, w1, nt, threads, wt, host,
+                                                    ", OMP_NUM_THREADS=%s" % os.environ["OMP_NUM_THREADS"]
+                                                    if os.environ.get("OMP_NUM_THREADS") else "")}
 
 
 def cpu_baseline_decode(enc1, enc2, seconds):
     """The reference's into_affine for compressed G2 + G1 records, restated in C (OpenMP over records)."""
     from oracle import binding as oracle
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
+    _, threads = host_threads()
     t0 = time.perf_counter()
     oracle.decode(2, enc2[:threads], True, True, threads)
     oracle.decode(1, enc1[:threads], True, True, threads)
@@ -125,11 +177,7 @@ def cpu_baseline_decode(enc1, enc2, seconds):
 def cpu_baseline_wnaf(base, scalars, seconds):
     """The reference's Wnaf (window 16 at 2^18 scalars) + batch_normalization, restated in C."""
     from oracle import binding as oracle
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
+    _, threads = host_threads()
     n = min(len(scalars), 131072)
     t0 = time.perf_counter()
     out = oracle.g1_wnaf_fixed_base(base, np.ascontiguousarray(scalars[:n]), threads)
@@ -182,11 +230,7 @@ def cpu_baseline_msm(base, k, s, seconds):
     """The reference-style sum of CurveAffine::mul terms (C restatement), OpenMP over terms,
     on a bounded prefix of the same bases (k_i * G, made by the oracle)."""
     from oracle import binding as oracle
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
+    _, threads = host_threads()
     m = 64 * threads
     pts = oracle.g1_mul_generator(np.ascontiguousarray(k[:m]), threads)
     t0 = time.perf_counter()
@@ -204,9 +248,57 @@ def cpu_baseline_msm(base, k, s, seconds):
                       "OpenMP over terms, %.1f s wall" % (m, wall)}
 
 
+def main_cpu_stub(args, ws, rank):
+    """Launcher test: the same rank/shard/gather/timing structure on gloo with
+    the oracle as each rank's compute (no GPU).  Not a measurement."""
+    import torch
+    import torch.distributed as dist
+    from oracle import binding as oracle
+    from pairing_amd.shard import gather_rows_to_root
+    if ws > 1:
+        dist.init_process_group("gloo")
+    n = args.batch
+    p_np, q_np = make_pairs(n, rank)
+
+    def step():
+        out = torch.from_numpy(oracle.pairing(p_np, q_np, 1).view(np.int64))
+        if ws > 1:
+            gather_rows_to_root(out, ws * n)
+
+    for _ in range(args.warmup):
+        step()
+    if ws > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if ws > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if ws > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "launcher test (cpu stub)", "value": ws * n * args.steps / elapsed,
+                          "unit": "pairings/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "u64", "data": "cpu stub: oracle per rank, gloo gather",
+                          "config": {"workload": "cpu stub", "batch_per_gpu": n, "global_batch": n * ws,
+                                     "parallelism": "shard%d+gather" % ws if ws > 1 else "single"}}), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d; timing %d ranks" % (ws, args.gpus, ws), file=sys.stderr)
+    if args.cpu_stub:
+        return main_cpu_stub(args, ws, rank)
     import torch
     import torch.distributed as dist
     import pairing_amd
@@ -417,7 +509,7 @@ def main():
             value = ws * n * args.steps / elapsed
             metric, unit = "BLS12-381 pairings/sec at batch 2^16", "pairings/s"
             config = {"workload": "bls12_381 e(P_i,Q_i) batch (fused G2 prepare + Miller loop + final exp)",
-                      "kernel_variant": ["lazy28", "word32", "word32x2", "gen", "gen2", "gen_lazyred"][int(os.environ.get("PA_PAIRING_KERNEL", "3"))],
+                      "kernel_variant": ["gen", "gen2"][int(os.environ.get("PA_PAIRING_KERNEL", "0"))],
                       "batch_per_gpu": n, "global_batch": n * ws, "parallelism": "shard%d+rccl_gather" % ws
                       if ws > 1 else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}

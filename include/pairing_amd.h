@@ -77,17 +77,12 @@ const char *pa_last_error(void);
 int pa_device_count(int *count);
 int pa_set_device(int device);
 int pa_synchronize(void);
-/* Tuning knob: which kernel family runs the Miller loop / final
- * exponentiation (identical results):
- *   0 = lazy 28-bit-limb core, one pairing per lane
- *   1 = 32-bit-word core, one pairing per lane
- *   2 = 32-bit-word core, two lanes per pairing
- *   3 = generated kernels (tools/pgen: own register allocation, code objects
- *       lib/pa_gen_*.hsaco loaded at first use), one lane per pairing (default)
- *   4 = generated kernels, a lane pair per pairing (two waves per SIMD)
- *   5 = generated kernels with lazy reduction (Fq2 products kept double-width
- *       and reduced once per output, pa_gen_*_lazy.hsaco), one lane per pairing
- * Not part of the reference interface; for A/B measurement. */
+/* Tuning knob: how the generated Miller-loop / final-exponentiation kernels
+ * (tools/pgen: own register allocation, code objects lib/pa_gen_*.hsaco
+ * loaded at first use) lay a pairing out (identical results):
+ *   0 = one pairing per lane (default)
+ *   1 = a lane pair per pairing (twice the waves; A/B alternative)
+ * Process-wide; not part of the reference interface. */
 int pa_set_pairing_kernel(int variant);
 
 /* ---- Fq (src/bls12_381/fq.rs, Field trait src/lib.rs:267-325) ---- */

@@ -142,9 +142,8 @@ def device_count():
 
 
 def set_pairing_kernel(variant):
-    """Pairing kernel family: 0 lazy 28-bit core, 1 32-bit one lane, 2 32-bit
-    two lanes per pairing, 3 generated (tools/pgen, default), 4 generated on
-    lane pairs.  Identical results."""
+    """Layout of the generated pairing kernels: 0 one pairing per lane
+    (default), 1 a lane pair per pairing.  Identical results."""
     call("pa_set_pairing_kernel", int(variant))
 
 

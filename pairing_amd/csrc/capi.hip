@@ -17,28 +17,15 @@
 namespace {
 
 thread_local std::string g_last_error;
-// kernel family for the Miller loop / final exponentiation (pa_set_pairing_kernel)
-int g_pairing_kernel = 3;
+// lanes per pairing of the generated Miller-loop / final-exponentiation
+// kernels (pa_set_pairing_kernel: 0 -> 1 lane, the default; 1 -> 2 lanes)
+int g_pairing_lanes = 1;
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
-    switch (g_pairing_kernel) {
-        case 1: return pa::launch_miller_loop_fused(p, q, out, n, s);
-        case 2: return pa::launch_miller_loop_fused2(p, q, out, n, s);
-        case 3: return pa::launch_miller_loop_gen(p, q, out, n, s);
-        case 4: return pa::launch_miller_loop_gen2(p, q, out, n, s);
-        case 5: return pa::launch_miller_loop_gen_lazy(p, q, out, n, s);
-        default: return pa::launch_miller_loop_fl(p, q, out, n, s);
-    }
+    return pa::launch_miller_loop_gen(g_pairing_lanes, p, q, out, n, s);
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
-    switch (g_pairing_kernel) {
-        case 1: return pa::launch_final_exponentiation(in, out, ok, n, s);
-        case 2: return pa::launch_final_exponentiation2(in, out, ok, n, s);
-        case 3: return pa::launch_final_exp_gen(in, out, ok, n, s);
-        case 4: return pa::launch_final_exp_gen2(in, out, ok, n, s);
-        case 5: return pa::launch_final_exp_gen_lazy(in, out, ok, n, s);
-        default: return pa::launch_final_exp_fl(in, out, ok, n, s);
-    }
+    return pa::launch_final_exp_gen(g_pairing_lanes, in, out, ok, n, s);
 }
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
@@ -134,8 +121,8 @@ int pa_set_device(int device) {
     return PA_OK;
 }
 int pa_set_pairing_kernel(int variant) {
-    if (variant < 0 || variant > 5) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..5");
-    g_pairing_kernel = variant;
+    if (variant < 0 || variant > 1) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0 or 1");
+    g_pairing_lanes = variant + 1;
     return PA_OK;
 }
 int pa_synchronize(void) {

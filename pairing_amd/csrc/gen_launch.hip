@@ -4,12 +4,23 @@
 // five kernel arguments of tools/pgen/kcfg.py and a per-wave spill
 // workspace (pa_gen_meta.h gives its size).  A missing code object is an
 // error, never a fallback.
+//
+// Spill workspaces.  A launch's waves index their workspace from its base by
+// block, so two launches that run at the same time must not share one.  Each
+// device keeps a pool of workspaces; a workspace records the stream and an
+// event of its last launch and is handed to a new launch only if that launch
+// is on the same stream (stream order serializes them) or the event has
+// completed.  Otherwise a new workspace is allocated, so concurrent callers
+// on different streams (pairing_amd.h: every entry point is reentrant) each
+// get their own.  The pool only grows to the number of launches in flight at
+// once.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "launch.h"
 #include "pa_gen_meta.h"
@@ -17,33 +28,36 @@
 namespace pa {
 namespace {
 
-constexpr int kKernels = 6;
+constexpr int kKernels = 4;
+constexpr size_t kSlotBytes = 3584;  // one 14-limb spill slot for a 64-lane wave
+
+struct Workspace {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipStream_t last = nullptr;
+    hipEvent_t done = nullptr;
+};
 
 struct GenDevice {
     bool loaded = false;
-    hipError_t err = hipSuccess;
     hipModule_t mod[kKernels] = {};
     hipFunction_t fn[kKernels] = {};
-    void* ws = nullptr;
-    size_t ws_bytes = 0;
+    std::vector<Workspace> pool;
 };
 
 std::mutex g_mu;
 GenDevice g_dev[64];
 thread_local std::string g_detail;   // the code object that failed to load, for pa_last_error
 
-// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing; 4, 5: one lane,
-// lazy reduction (tower.TowerLazy)
+// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing
 const char* const kFile[kKernels] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco",
-                                     "pa_gen_miller_loop2.hsaco", "pa_gen_final_exp2.hsaco",
-                                     "pa_gen_miller_loop_lazy.hsaco", "pa_gen_final_exp_lazy.hsaco"};
+                                     "pa_gen_miller_loop2.hsaco", "pa_gen_final_exp2.hsaco"};
 const char* const kName[kKernels] = {"pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2",
-                                     "pa_gen_final_exp2", "pa_gen_miller_loop_lazy", "pa_gen_final_exp_lazy"};
-const size_t kWaveBytes[kKernels] = {
-    PA_GEN_MILLER_LOOP_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_MEM_SLOTS * 3584ull,
-    PA_GEN_MILLER_LOOP2_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP2_MEM_SLOTS * 3584ull,
-    PA_GEN_MILLER_LOOP_LAZY_MEM_SLOTS * 3584ull, PA_GEN_FINAL_EXP_LAZY_MEM_SLOTS * 3584ull};
-const int kLanes[kKernels] = {1, 1, 2, 2, 1, 1};
+                                     "pa_gen_final_exp2"};
+const size_t kWaveBytes[kKernels] = {PA_GEN_MILLER_LOOP_MEM_SLOTS * kSlotBytes, PA_GEN_FINAL_EXP_MEM_SLOTS * kSlotBytes,
+                                     PA_GEN_MILLER_LOOP2_MEM_SLOTS * kSlotBytes,
+                                     PA_GEN_FINAL_EXP2_MEM_SLOTS * kSlotBytes};
+const int kLanes[kKernels] = {1, 1, 2, 2};
 
 // PA_GEN_DIR (A/B experiments with alternative generated code objects) overrides
 // the directory of libpairing_amd.so; PA_GEN_WS_SLOTS raises the workspace size
@@ -59,22 +73,86 @@ std::string lib_dir() {
     return ".";
 }
 
+// Loads every code object or none: on a failure the modules already loaded
+// are unloaded and the next launch tries again.
 hipError_t load(GenDevice& d) {
-    if (d.loaded) return d.err;
-    d.loaded = true;
+    if (d.loaded) return hipSuccess;
     const std::string dir = lib_dir();
-    for (int k = 0; k < kKernels; k++) {
+    hipError_t e = hipSuccess;
+    int k = 0;
+    for (; k < kKernels; k++) {
         const std::string path = dir + "/" + kFile[k];
-        if ((d.err = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess ||
-            (d.err = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) {
+        if ((e = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess) {
+            d.mod[k] = nullptr;
             g_detail = "generated kernel " + path;
-            return d.err;
+            break;
+        }
+        if ((e = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) {
+            g_detail = "kernel " + std::string(kName[k]) + " in " + path;
+            k++;  // this module did load
+            break;
         }
     }
+    if (e != hipSuccess) {
+        for (int j = 0; j < k; j++)
+            if (d.mod[j]) (void)hipModuleUnload(d.mod[j]);
+        for (int j = 0; j < kKernels; j++) {
+            d.mod[j] = nullptr;
+            d.fn[j] = nullptr;
+        }
+        return e;
+    }
+    d.loaded = true;
+    return hipSuccess;
+}
+
+size_t wave_bytes() {
+    size_t b = 0;
+    for (int k = 0; k < kKernels; k++) b = kWaveBytes[k] > b ? kWaveBytes[k] : b;
+    if (const char* e = getenv("PA_GEN_WS_SLOTS")) {
+        const size_t x = strtoull(e, nullptr, 10) * kSlotBytes;
+        b = x > b ? x : b;
+    }
+    return b;
+}
+
+// A workspace of at least `need` bytes that no unfinished launch on another
+// stream uses (caller holds g_mu).
+hipError_t acquire(GenDevice& d, size_t need, hipStream_t stream, Workspace** out) {
+    Workspace* idle_small = nullptr;
+    for (auto& w : d.pool) {
+        const bool free_now = w.last == stream || hipEventQuery(w.done) == hipSuccess;
+        if (!free_now) continue;
+        if (w.bytes >= need) {
+            *out = &w;
+            return hipSuccess;
+        }
+        if (!idle_small && w.last != stream) idle_small = &w;
+    }
+    hipError_t e;
+    if (idle_small) {  // its last launch has finished: grow it in place
+        if ((e = hipFree(idle_small->p)) != hipSuccess) return e;
+        idle_small->p = nullptr;
+        idle_small->bytes = 0;
+        if ((e = hipMalloc(&idle_small->p, need)) != hipSuccess) return e;
+        idle_small->bytes = need;
+        *out = idle_small;
+        return hipSuccess;
+    }
+    Workspace w;
+    if ((e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipMalloc(&w.p, need)) != hipSuccess) {
+        (void)hipEventDestroy(w.done);
+        return e;
+    }
+    w.bytes = need;
+    d.pool.push_back(w);
+    *out = &d.pool.back();
     return hipSuccess;
 }
 
 hipError_t launch(int which, const void* a0, const void* a1, const void* a2, size_t n, hipStream_t stream) {
+    g_detail.clear();
     if (n == 0) return hipSuccess;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -87,58 +165,37 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
         return e;
     }
     const size_t blocks = (n * kLanes[which] + 63) / 64;
-    size_t wave_bytes = 0;
-    for (int k = 0; k < kKernels; k++) wave_bytes = kWaveBytes[k] > wave_bytes ? kWaveBytes[k] : wave_bytes;
-    if (const char* e = getenv("PA_GEN_WS_SLOTS")) {
-        const size_t b = strtoull(e, nullptr, 10) * 3584ull;
-        wave_bytes = b > wave_bytes ? b : wave_bytes;
-    }
-    const size_t need = blocks * wave_bytes;
-    if (need > d.ws_bytes) {
-        if (d.ws) (void)hipFree(d.ws);
-        d.ws = nullptr;
-        d.ws_bytes = 0;
-        if ((e = hipMalloc(&d.ws, need)) != hipSuccess) return e;
-        d.ws_bytes = need;
-    }
+    if (blocks > 0xffffffffull) return hipErrorInvalidValue;
+    Workspace* ws = nullptr;
+    if ((e = acquire(d, blocks * wave_bytes(), stream, &ws)) != hipSuccess) return e;
     struct {
         const void* a0;
         const void* a1;
         const void* a2;
         uint64_t n;
         void* ws;
-    } args{a0, a1, a2, (uint64_t)n, d.ws};
+    } args{a0, a1, a2, (uint64_t)n, ws->p};
     size_t size = sizeof(args);
     void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                       HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(d.fn[which], (unsigned)blocks, 1, 1, 64, 1, 1, 0, stream, nullptr, config);
+    if ((e = hipModuleLaunchKernel(d.fn[which], (unsigned)blocks, 1, 1, 64, 1, 1, 0, stream, nullptr, config)) !=
+        hipSuccess)
+        return e;
+    ws->last = stream;
+    return hipEventRecord(ws->done, stream);
 }
 
 }  // namespace
 
 const char* gen_error_detail() { return g_detail.c_str(); }
 
-hipError_t launch_miller_loop_gen(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+hipError_t launch_miller_loop_gen(int lanes, const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                   hipStream_t stream) {
-    return launch(0, p_aff, q_aff, out, n, stream);
+    return launch(lanes == 2 ? 2 : 0, p_aff, q_aff, out, n, stream);
 }
-hipError_t launch_final_exp_gen(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream) {
-    return launch(1, in, out, ok, n, stream);
-}
-hipError_t launch_miller_loop_gen2(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                   hipStream_t stream) {
-    return launch(2, p_aff, q_aff, out, n, stream);
-}
-hipError_t launch_final_exp_gen2(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream) {
-    return launch(3, in, out, ok, n, stream);
-}
-hipError_t launch_miller_loop_gen_lazy(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                       hipStream_t stream) {
-    return launch(4, p_aff, q_aff, out, n, stream);
-}
-hipError_t launch_final_exp_gen_lazy(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
-                                     hipStream_t stream) {
-    return launch(5, in, out, ok, n, stream);
+hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
+                                hipStream_t stream) {
+    return launch(lanes == 2 ? 3 : 1, in, out, ok, n, stream);
 }
 
 }  // namespace pa

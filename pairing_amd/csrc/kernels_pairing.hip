@@ -1,15 +1,14 @@
-// Pairing kernels, one pairing per lane (BASELINE config 4 / 5 hot path).
+// Materialized-G2Prepared pairing kernels, one pairing per lane (the
+// fused Miller loop and final exponentiation of the hot path are the
+// generated code objects of tools/pgen, gen_launch.hip).
 //
 //   k_g2_prepare             G2Prepared::from_affine  (mod.rs:168-358)
 //   k_miller_loop_prepared   miller_loop([(p, q_prepared)])  (mod.rs:40-102)
-//   k_miller_loop_fused      the same with prepare fused in: no 19.6 KB
-//                            G2Prepared round trip through HBM per pair
-//   k_final_exponentiation   mod.rs:104-160
 //   k_fq12_product           Fq12 tree product (multi-pair miller_loop)
 //
 // HBM records use the reference's in-memory order (include/pairing_amd.h).
 #include "launch.h"
-#include "pairing2.h"
+#include "pairing.h"
 
 namespace pa {
 
@@ -82,65 +81,6 @@ __global__ void __launch_bounds__(64) k_miller_loop_prepared(const uint64_t* __r
     store(out + 72 * i, f);
 }
 
-__global__ void __launch_bounds__(64) k_miller_loop_fused(const uint64_t* __restrict__ p_aff,
-                                                          const uint64_t* __restrict__ q_aff,
-                                                          uint64_t* __restrict__ out, size_t n) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Aff<Fq> p;
-    Aff<Fq2> q;
-    load_aff(p, p_aff + kAffG1Words * i);
-    load_aff(q, q_aff + kAffG2Words * i);
-    Fq12 f;
-    miller_loop_fused(f, p, q);
-    store(out + 72 * i, f);
-}
-
-__global__ void __launch_bounds__(64) k_final_exponentiation(const uint64_t* __restrict__ in,
-                                                             uint64_t* __restrict__ out,
-                                                             uint8_t* __restrict__ ok, size_t n) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Fq12 f, r;
-    load(f, in + 72 * i);
-    const bool k = final_exponentiation(r, f);
-    if (!k) { zero(r.c0); zero(r.c1); }
-    store(out + 72 * i, r);
-    if (ok) ok[i] = k ? 1 : 0;
-}
-
-// ---- two lanes per pairing (pairing2.h): lane 2i+r holds half r of pairing i ----
-__global__ void __launch_bounds__(64) k_miller_loop_fused2(const uint64_t* __restrict__ p_aff,
-                                                           const uint64_t* __restrict__ q_aff,
-                                                           uint64_t* __restrict__ out, size_t n) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t i = t >> 1;
-    if (i >= n) return;  // both lanes of a pair leave together
-    const bool r = (threadIdx.x & 1) != 0;
-    Aff<Fq> p;
-    Aff<Fq2> q;
-    load_aff(p, p_aff + kAffG1Words * i);
-    load_aff(q, q_aff + kAffG2Words * i);
-    Fq6 f;
-    miller_loop2(f, p, q, r);
-    store(out + 72 * i + (r ? 36 : 0), f);
-}
-
-__global__ void __launch_bounds__(64) k_final_exponentiation2(const uint64_t* __restrict__ in,
-                                                              uint64_t* __restrict__ out,
-                                                              uint8_t* __restrict__ ok, size_t n) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t i = t >> 1;
-    if (i >= n) return;
-    const bool r = (threadIdx.x & 1) != 0;
-    Fq6 f, z;
-    load(f, in + 72 * i + (r ? 36 : 0));
-    const bool k = final_exponentiation2(z, f, r);
-    if (!k) zero(z);
-    store(out + 72 * i + (r ? 36 : 0), z);
-    if (ok && !r) ok[i] = k ? 1 : 0;
-}
-
 // one tree level: work[i] *= work[i + half] for i < cnt - half
 __global__ void __launch_bounds__(64) k_fq12_product_level(uint64_t* __restrict__ work, size_t cnt, size_t half) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,30 +104,6 @@ hipError_t launch_miller_loop_prepared(const uint64_t* p_aff, const uint64_t* pr
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_miller_loop_prepared, dim3(blocks_for(n, 64)), dim3(64), 0, stream, p_aff, prepared,
                        out, n);
-    return hipGetLastError();
-}
-hipError_t launch_miller_loop_fused(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                    hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_miller_loop_fused, dim3(blocks_for(n, 64)), dim3(64), 0, stream, p_aff, q_aff, out, n);
-    return hipGetLastError();
-}
-hipError_t launch_final_exponentiation(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
-                                       hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_final_exponentiation, dim3(blocks_for(n, 64)), dim3(64), 0, stream, in, out, ok, n);
-    return hipGetLastError();
-}
-hipError_t launch_miller_loop_fused2(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                     hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_miller_loop_fused2, dim3(blocks_for(2 * n, 64)), dim3(64), 0, stream, p_aff, q_aff, out, n);
-    return hipGetLastError();
-}
-hipError_t launch_final_exponentiation2(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
-                                        hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_final_exponentiation2, dim3(blocks_for(2 * n, 64)), dim3(64), 0, stream, in, out, ok, n);
     return hipGetLastError();
 }
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream) {

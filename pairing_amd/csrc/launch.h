@@ -58,32 +58,17 @@ hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* o
 hipError_t launch_g2_prepare(const uint64_t* q_aff, uint64_t* prepared, size_t n, hipStream_t stream);
 hipError_t launch_miller_loop_prepared(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out,
                                        size_t n, hipStream_t stream);
-hipError_t launch_miller_loop_fused(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                    hipStream_t stream);
-hipError_t launch_final_exponentiation(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
-                                       hipStream_t stream);
-// two lanes per pairing (pairing2.h); same results as the one-lane kernels
-hipError_t launch_miller_loop_fused2(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                     hipStream_t stream);
-hipError_t launch_final_exponentiation2(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
-                                        hipStream_t stream);
-// lazy 28-bit-limb core (kernels_pairing_fl.hip); same results
-hipError_t launch_miller_loop_fl(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                 hipStream_t stream);
-hipError_t launch_final_exp_fl(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream);
 // non-empty after a generated code object failed to load (names the file)
 const char* gen_error_detail();
-// generated kernels (tools/pgen, gen_launch.hip); same results
-hipError_t launch_miller_loop_gen(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+// The generated Miller-loop / final-exponentiation kernels (tools/pgen,
+// gen_launch.hip).  `lanes` = 1: one pairing per lane (default); 2: a lane
+// pair per pairing (A/B alternative, same results).  Each launch draws its
+// spill workspace from a per-device pool keyed by stream and completion
+// event, so concurrent launches on different streams never share one.
+hipError_t launch_miller_loop_gen(int lanes, const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                   hipStream_t stream);
-hipError_t launch_final_exp_gen(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream);
-hipError_t launch_miller_loop_gen2(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                   hipStream_t stream);
-hipError_t launch_final_exp_gen2(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream);
-// generated, lazy reduction (tools/pgen tower.TowerLazy); same results
-hipError_t launch_miller_loop_gen_lazy(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                       hipStream_t stream);
-hipError_t launch_final_exp_gen_lazy(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream);
+hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
+                                hipStream_t stream);
 // out[0] = prod_i in[i] (Fq12), in-place tree reduction over `work` (n entries, clobbered)
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
 

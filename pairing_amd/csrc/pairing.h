@@ -130,35 +130,6 @@ PA_DEV void ell(Fq12& f, const EllCoeff& c, const Fq& px, const Fq& py) {
     mul_by_014(f, f, c.c2, b, a);
 }
 
-// Single-pair Miller loop with the line precomputation fused in (no
-// G2Prepared round trip through HBM).  Equals
-// miller_loop([(P.prepare(), Q.prepare())]) of mod.rs:40-102; pairs with an
-// infinity side give one (mod.rs:50-54).  Infinity lanes run the same
-// instruction stream on the generator-free dummy data and are selected out.
-PA_NOINLINE void miller_loop_fused(Fq12& f, const Aff<Fq>& p, const Aff<Fq2>& q) {
-    Jac<Fq2> r;
-    r.x = q.x;
-    r.y = q.y;
-    one(r.z);
-    one(f);
-    EllCoeff c;
-    // bits of |x| >> 1 below its leading one: 62 iterations, 5 of them set
-#pragma unroll 1
-    for (int bit = 61; bit >= 0; bit--) {
-        doubling_step(c, r);
-        ell(f, c, p.x, p.y);
-        if (((kBlsX >> 1) >> bit) & 1) {  // wave-uniform
-            addition_step(c, r, q.x, q.y);
-            ell(f, c, p.x, p.y);
-        }
-        sqr(f, f);
-    }
-    doubling_step(c, r);
-    ell(f, c, p.x, p.y);
-    conjugate(f, f);
-    if (p.inf || q.inf) one(f);
-}
-
 // ---- final exponentiation ----
 // Granger-Scott squaring in the cyclotomic subgroup (f^(q^6+1)(q^2+1) = ...
 // lies there after the easy part).  Same value as Fq12::square for such f.
@@ -199,57 +170,6 @@ PA_NOINLINE void cyclotomic_sqr(Fq12& r, const Fq12& f) {
     // c1.c2 = 3 t3 + 2 b2
     add(tmp, t3, b2); dbl(tmp, tmp); add(o.c1.c2, tmp, t3);
     r = o;
-}
-
-// exp_by_x, mod.rs:116-121: f^|x| (Field::pow square-and-multiply, lib.rs:306-324)
-// followed by conjugation (x < 0).  Squarings are cyclotomic.
-PA_NOINLINE void exp_by_x(Fq12& r, const Fq12& f, uint64_t x) {
-    Fq12 res = f;  // the leading one bit
-    const int top = 63 - __builtin_clzll(x);
-#pragma unroll 1
-    for (int bit = top - 1; bit >= 0; bit--) {
-        cyclotomic_sqr(res, res);
-        if ((x >> bit) & 1) mul(res, res, f);  // wave-uniform
-    }
-    conjugate(r, res);
-}
-
-// mod.rs:104-160.  Returns false (reference: None) iff f == 0.
-PA_NOINLINE bool final_exponentiation(Fq12& out, const Fq12& f) {
-    Fq12 f1, f2, r, y0, y1, y2, y3;
-    conjugate(f1, f);
-    const bool ok = inverse(f2, f);
-    mul(r, f1, f2);
-    f2 = r;
-    frobenius_map(r, r, 2);
-    mul(r, r, f2);
-
-    uint64_t x = kBlsX;
-    cyclotomic_sqr(y0, r);
-    exp_by_x(y1, y0, x);
-    x >>= 1;
-    exp_by_x(y2, y1, x);
-    x <<= 1;
-    conjugate(y3, r);
-    mul(y1, y1, y3);
-    conjugate(y1, y1);
-    mul(y1, y1, y2);
-    exp_by_x(y2, y1, x);
-    exp_by_x(y3, y2, x);
-    conjugate(y1, y1);
-    mul(y3, y3, y1);
-    conjugate(y1, y1);
-    frobenius_map(y1, y1, 3);
-    frobenius_map(y2, y2, 2);
-    mul(y1, y1, y2);
-    exp_by_x(y2, y3, x);
-    mul(y2, y2, y0);
-    mul(y2, y2, r);
-    mul(y1, y1, y2);
-    frobenius_map(y2, y3, 1);
-    mul(y1, y1, y2);
-    out = y1;
-    return ok;
 }
 
 }  // namespace pa

@@ -1,0 +1,51 @@
+"""bench.py --gpus N run directly (no WORLD_SIZE): it must start N ranks
+itself through torch.distributed.run and report n_gpus = N with the shard +
+gather parallelism.  Exercised on the CPU with --cpu-stub (gloo ranks, the
+oracle as each rank's compute); the GPU path shares launch_ranks, dist_env
+and the rank/shard/gather structure."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "1"
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def test_bench_gpus2_launches_two_ranks():
+    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "6", "--cpu-stub"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout          # rank 0 prints one line
+    line = lines[0]
+    assert line["n_gpus"] == 2
+    assert line["config"]["parallelism"] == "shard2+gather"
+    assert line["config"]["global_batch"] == 12
+    assert line["value"] > 0 and line["steps"] == 2
+
+
+def test_bench_gpus1_runs_in_process():
+    r = _run(["--gpus", "1", "--steps", "1", "--warmup", "0", "--batch", "4", "--cpu-stub"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_lines(r.stdout)[0]
+    assert line["n_gpus"] == 1 and line["config"]["parallelism"] == "single"
+
+
+def test_bench_fails_when_fewer_devices_than_gpus():
+    import torch
+    n = torch.cuda.device_count() + 1
+    r = _run(["--gpus", str(max(n, 2)), "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 2
+    assert "visible" in r.stderr

@@ -1,0 +1,131 @@
+"""Parity of the exact kernels bench.py times, at the sizes it times them.
+
+bench.py measures the `_device` entry points (HBM-resident tensors through
+pairing_amd.device): config 2 is `pa_fq_mul_batch_device` at 2^20 elements
+(k_fq_mul_batch: grid-stride loop with register prefetch and a 4096-block
+grid cap), the Fr leg `pa_fr_mul_batch_device` at 2^20, config 4
+`pa_pairing_batch_device` at 2^16 pairs on bench.make_pairs' inputs.  Each is
+compared here bit for bit with the oracle (fq.rs:909-960, fr.rs:438-465,
+mod.rs:40-160), at the benched size and at a ragged size that leaves a
+partial tail for the grid-stride loop.  A last test runs two pairing batches
+on two streams at the same time (each launch must get its own spill
+workspace, gen_launch.hip)."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import Q, R_ORDER, limbs, rng
+
+pytestmark = pytest.mark.gpu
+
+FQ_TOP = Q >> 320            # top limb of q
+FR_TOP = R_ORDER >> 192
+
+
+def _threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+
+
+def _field_rows(seed, n, words, top, edges):
+    """n values < modulus (top limb drawn below the modulus' top limb), the
+    edge values first."""
+    g = rng(seed)
+    a = g.integers(0, 1 << 64, size=(n, words), dtype=np.uint64)
+    a[:, words - 1] = g.integers(0, top, size=n, dtype=np.uint64)
+    e = np.array([limbs(v, words) for v in edges], np.uint64)
+    a[:len(e)] = e
+    return a
+
+
+def _fq_rows(seed, n):
+    return _field_rows(seed, n, 6, FQ_TOP, [0, 1, 2, Q - 1, Q - 2, (Q - 1) // 2, (1 << 380) - 1])
+
+
+def _fr_rows(seed, n):
+    return _field_rows(seed, n, 4, FR_TOP, [0, 1, 2, R_ORDER - 1, R_ORDER - 2, (R_ORDER - 1) // 2])
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(a.view(np.int64)).to("cuda:0")
+
+
+def _host(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("n", [1 << 20, (1 << 20) + 37, 4096 * 256 * 2 + 5])
+def test_fq_mul_device_bit_exact_at_bench_size(gpu, oracle, n):
+    """config 2: the benched kernel, every element against Fq::mul_assign"""
+    import torch
+    import pairing_amd.device as pdev
+    a, b = _fq_rows(100 + n % 97, n), _fq_rows(200 + n % 89, n)[::-1].copy()
+    out = pdev.empty_records(n, 6, "cuda:0")
+    pdev.fq_mul(_dev(a), _dev(b), out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(out), oracle.fq_mul(a, b))
+
+
+@pytest.mark.parametrize("n", [1 << 20, (1 << 20) + 37])
+def test_fr_mul_device_bit_exact_at_bench_size(gpu, oracle, n):
+    import torch
+    import pairing_amd.device as pdev
+    a, b = _fr_rows(300 + n % 97, n), _fr_rows(400 + n % 89, n)[::-1].copy()
+    out = pdev.empty_records(n, 4, "cuda:0")
+    pdev.fr_mul(_dev(a), _dev(b), out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(out), oracle.fr_mul(a, b))
+
+
+def test_pairing_device_bit_exact_at_bench_size(gpu, oracle):
+    """config 4: 2^16 pairings (1024 waves, every wave with its own spill
+    workspace) on the bench's own inputs, every pairing against the oracle"""
+    import torch
+    import bench
+    import pairing_amd.device as pdev
+    n = 1 << 16
+    p_np, q_np = bench.make_pairs(n, 0)
+    out = pdev.empty_records(n, 72, "cuda:0")
+    scratch = pdev.empty_records(n, 72, "cuda:0")
+    pdev.pairing(_dev(p_np), _dev(q_np), out, scratch)
+    torch.cuda.synchronize()
+    got = _host(out)
+    exp = oracle.pairing(p_np, q_np, _threads())
+    np.testing.assert_array_equal(got, exp)
+    # infinity pairs (1/128 of P) give one
+    inf = np.nonzero(p_np[:, 12] != 0)[0]
+    assert len(inf) == n // 128
+    one = np.zeros(72, np.uint64)
+    one[:6] = limbs(pow(2, 384, Q))
+    assert (got[inf] == one).all()
+
+
+def test_pairing_two_streams_concurrently(gpu, oracle):
+    """Two pairing batches enqueued on two streams before either finishes:
+    both bit-exact (each launch draws its own spill workspace)"""
+    import torch
+    import bench
+    import pairing_amd.device as pdev
+    n = 4096
+    p0, q0 = bench.make_pairs(n, 0, seed=11)
+    p1, q1 = bench.make_pairs(n, 1, seed=57)
+    s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for (p, q), s in (((p0, q0), s0), ((p1, q1), s1)):
+        with torch.cuda.stream(s):
+            dp, dq = _dev(p), _dev(q)
+            out = pdev.empty_records(n, 72, "cuda:0")
+            scratch = pdev.empty_records(n, 72, "cuda:0")
+        s.synchronize()
+        outs.append((dp, dq, out, scratch, s))
+    for dp, dq, out, scratch, s in outs:       # both enqueued back to back
+        pdev.pairing(dp, dq, out, scratch, s)
+    torch.cuda.synchronize()
+    t = _threads()
+    np.testing.assert_array_equal(_host(outs[0][2]), oracle.pairing(p0, q0, t))
+    np.testing.assert_array_equal(_host(outs[1][2]), oracle.pairing(p1, q1, t))

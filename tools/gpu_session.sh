@@ -25,13 +25,10 @@ for step in "$@"; do
         valu) run valu 120 ./tools/valu_rates ;;
         tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
         alltests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
+        sizetests) run pytest_sizes 600 python -u -m pytest tests/test_bench_sizes.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
-        bench1) run bench_word32 600 env PA_PAIRING_KERNEL=1 python bench.py --no-cpu-baseline ;;
-        benchgen) run bench_gen 600 env PA_PAIRING_KERNEL=3 python bench.py --no-cpu-baseline ;;
-        benchlazy) run bench_lazy 600 env PA_PAIRING_KERNEL=5 python bench.py --no-cpu-baseline ;;
-        proflazy) run prof_lazy 600 env PA_PAIRING_KERNEL=5 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lazy -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-        benchgen2) run bench_gen2 600 env PA_PAIRING_KERNEL=4 python bench.py --no-cpu-baseline ;;
+        benchgen2) run bench_gen2 600 env PA_PAIRING_KERNEL=1 python bench.py --no-cpu-baseline ;;
         wnafbench) run bench_wnaf 300 python bench.py --workload wnaf --steps 5 --warmup 1 ;;
         decbench) run bench_decode 300 python bench.py --workload decode --steps 5 --warmup 1 ;;
         newtests) run pytest_new 600 python -u -m pytest tests/test_fr.py tests/test_msm.py -m gpu -v --timeout 300 --timeout-method thread ;;
@@ -49,9 +46,8 @@ for step in "$@"; do
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         pmcsq) run pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES -d gpurun_out/pmc_sq1 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline &&
                run pmc_sq2 600 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR -d gpurun_out/pmc_sq2 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
-        pmcsq4) run pmc4_sq1 300 env PA_PAIRING_KERNEL=4 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES -d gpurun_out/pmc4_sq1 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline &&
-                run pmc4_sq2 300 env PA_PAIRING_KERNEL=4 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR -d gpurun_out/pmc4_sq2 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
-        pmcsq5) run pmc5_sq2 300 env PA_PAIRING_KERNEL=5 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR -d gpurun_out/pmc5_sq2 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+        pmcsq4) run pmc4_sq1 300 env PA_PAIRING_KERNEL=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES -d gpurun_out/pmc4_sq1 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline &&
+                run pmc4_sq2 300 env PA_PAIRING_KERNEL=1 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR -d gpurun_out/pmc4_sq2 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
