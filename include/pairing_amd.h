@@ -104,6 +104,14 @@ int pa_fq12_mul_batch(const pa_fq12 *a, const pa_fq12 *b, pa_fq12 *out, size_t n
 int pa_fq12_square_batch(const pa_fq12 *a, pa_fq12 *out, size_t n);                /* fq12.rs:99-114 */
 int pa_fq12_inverse_batch(const pa_fq12 *a, pa_fq12 *out, uint8_t *ok, size_t n);  /* fq12.rs:132-148 */
 int pa_fq12_frobenius_map_batch(const pa_fq12 *a, pa_fq12 *out, size_t n, size_t power); /* fq12.rs:90-97 */
+int pa_fq2_inverse_batch(const pa_fq2 *a, pa_fq2 *out, uint8_t *ok, size_t n);    /* fq2.rs:138-155 */
+int pa_fq2_frobenius_map_batch(const pa_fq2 *a, pa_fq2 *out, size_t n, size_t power); /* fq2.rs:157-159 */
+int pa_fq6_square_batch(const pa_fq6 *a, pa_fq6 *out, size_t n);                   /* fq6.rs:166-197 */
+int pa_fq6_inverse_batch(const pa_fq6 *a, pa_fq6 *out, uint8_t *ok, size_t n);    /* fq6.rs:250-301 */
+int pa_fq6_frobenius_map_batch(const pa_fq6 *a, pa_fq6 *out, size_t n, size_t power); /* fq6.rs:157-164 */
+/* Field::pow, lib.rs:306-324, one exponent (exp_words u64, little-endian) for every element */
+int pa_fq_pow_batch(const pa_fq *a, const uint64_t *exp, size_t exp_words, pa_fq *out, size_t n);
+int pa_fq12_pow_batch(const pa_fq12 *a, const uint64_t *exp, size_t exp_words, pa_fq12 *out, size_t n);
 /* Fq12::mul_by_014, fq12.rs:34-48 */
 int pa_fq12_mul_by_014_batch(const pa_fq12 *a, const pa_fq2 *c0, const pa_fq2 *c1, const pa_fq2 *c4,
                              pa_fq12 *out, size_t n);
@@ -127,8 +135,54 @@ int pa_pairing_batch(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out,
 int pa_g1_batch_normalization(pa_g1 *v, size_t n);
 /* Wnaf::new().base(*base, n).scalar(scalars[i]) for every i (wnaf.rs:93-107,
  * 169-178): out[i] = scalars[i] * base as a Jacobian point (equal as a point to
- * the reference's; representation-independent PartialEq, ec.rs:45-85). */
+ * the reference's; representation-independent PartialEq, ec.rs:45-85).  Any
+ * 256-bit FrRepr is multiplied exactly; the reference's wnaf_form wraps
+ * (add_nocarry, wnaf.rs:30-35) for raw reprs within 2^w of 2^256, values no
+ * Fr::into_repr produces, so those two differ only there. */
 int pa_g1_wnaf_fixed_base(const pa_g1 *base, const pa_fr_repr *scalars, size_t n, pa_g1 *out);
+
+/* ---- CurveProjective / CurveAffine per-op batches, G1 and G2 ----
+ * The `curve_impl!` group law (ec.rs:1-621) for both groups, one item per
+ * lane, replaying the reference's formula sequence: Jacobian outputs equal
+ * the reference's X, Y, Z words bit for bit (zero = z == 0; a zero produced
+ * by P + (-P) keeps the x, y words the formulas leave, ec.rs:398, 477). */
+/* CurveProjective::double, dbl-2009-l, ec.rs:296-354 */
+int pa_g1_double_batch(const pa_g1 *a, pa_g1 *out, size_t n);
+int pa_g2_double_batch(const pa_g2 *a, pa_g2 *out, size_t n);
+/* CurveProjective::add_assign, add-2007-bl, ec.rs:356-444: out[i] = a[i] + b[i] */
+int pa_g1_add_batch(const pa_g1 *a, const pa_g1 *b, pa_g1 *out, size_t n);
+int pa_g2_add_batch(const pa_g2 *a, const pa_g2 *b, pa_g2 *out, size_t n);
+/* CurveProjective::add_assign_mixed, madd-2007-bl, ec.rs:446-526 */
+int pa_g1_add_mixed_batch(const pa_g1 *a, const pa_g1_affine *b, pa_g1 *out, size_t n);
+int pa_g2_add_mixed_batch(const pa_g2 *a, const pa_g2_affine *b, pa_g2 *out, size_t n);
+/* CurveProjective::negate, ec.rs:528-532 */
+int pa_g1_negate_batch(const pa_g1 *a, pa_g1 *out, size_t n);
+int pa_g2_negate_batch(const pa_g2 *a, pa_g2 *out, size_t n);
+/* CurveProjective::sub_assign = negate + add_assign, lib.rs:156-160 */
+int pa_g1_sub_batch(const pa_g1 *a, const pa_g1 *b, pa_g1 *out, size_t n);
+int pa_g2_sub_batch(const pa_g2 *a, const pa_g2 *b, pa_g2 *out, size_t n);
+/* CurveProjective::into_affine, ec.rs:586-619 (zero -> the point at infinity) */
+int pa_g1_into_affine_batch(const pa_g1 *a, pa_g1_affine *out, size_t n);
+int pa_g2_into_affine_batch(const pa_g2 *a, pa_g2_affine *out, size_t n);
+/* CurveAffine::into_projective, ec.rs:570-582 */
+int pa_g1_into_projective_batch(const pa_g1_affine *a, pa_g1 *out, size_t n);
+int pa_g2_into_projective_batch(const pa_g2_affine *a, pa_g2 *out, size_t n);
+/* G2 CurveProjective::batch_normalization, ec.rs:246-294, in place */
+int pa_g2_batch_normalization(pa_g2 *v, size_t n);
+/* G2 Wnaf::new().base(*base, n).scalar(scalars[i]) (wnaf.rs:93-107, 169-178):
+ * out[i] = scalars[i] * base, equal as a point to the reference's (PartialEq,
+ * ec.rs:45-85).  Any 256-bit FrRepr is multiplied exactly; the reference's
+ * wnaf_form instead wraps (add_nocarry, wnaf.rs:30-35) for raw reprs within
+ * 2^w of 2^256, values no Fr::into_repr produces. */
+int pa_g2_wnaf_fixed_base(const pa_g2 *base, const pa_fr_repr *scalars, size_t n, pa_g2 *out);
+/* CurveProjective::recommended_wnaf_for_scalar / _for_num_scalars
+ * (lib.rs:166-174; G1 ec.rs:895-921, G2 ec.rs:1586-1612): the window the
+ * reference's Wnaf would pick (returned as a positive int).  The GPU
+ * fixed-base path does not depend on it (signed base-256 comb). */
+int pa_g1_recommended_wnaf_for_scalar(const pa_fr_repr *scalar);
+int pa_g2_recommended_wnaf_for_scalar(const pa_fr_repr *scalar);
+int pa_g1_recommended_wnaf_for_num_scalars(size_t num_scalars);
+int pa_g2_recommended_wnaf_for_num_scalars(size_t num_scalars);
 
 /* ---- point encodings and square roots (SURVEY.md §8 f, rank 1) ----
  * Wire format of src/bls12_381/README.md "Serialization": big-endian
@@ -237,6 +291,23 @@ int pa_g1_multiexp_device(const pa_g1_affine *bases, const pa_fr_repr *s, size_t
                           size_t workspace_bytes, void *stream);
 int pa_g2_multiexp_device(const pa_g2_affine *bases, const pa_fr_repr *s, size_t n, pa_g2 *out, void *workspace,
                           size_t workspace_bytes, void *stream);
+/* G2 batch_normalization and fixed-base multiply on device memory; the G2
+ * table / workspace hold pa_g2_fixed_base_table_words() /
+ * pa_g2_fixed_base_workspace_words() u64 */
+int pa_g2_batch_normalization_device(pa_g2 *v, size_t n, void *stream);
+size_t pa_g2_fixed_base_table_words(void);
+size_t pa_g2_fixed_base_workspace_words(void);
+int pa_g2_wnaf_fixed_base_device(const pa_g2 *base, const pa_fr_repr *scalars, pa_g2 *out, size_t n,
+                                 uint64_t *table, uint64_t *workspace, void *stream);
+/* group law on device memory (see the host batches above) */
+int pa_g1_double_batch_device(const pa_g1 *a, pa_g1 *out, size_t n, void *stream);
+int pa_g2_double_batch_device(const pa_g2 *a, pa_g2 *out, size_t n, void *stream);
+int pa_g1_add_batch_device(const pa_g1 *a, const pa_g1 *b, pa_g1 *out, size_t n, void *stream);
+int pa_g2_add_batch_device(const pa_g2 *a, const pa_g2 *b, pa_g2 *out, size_t n, void *stream);
+int pa_g1_add_mixed_batch_device(const pa_g1 *a, const pa_g1_affine *b, pa_g1 *out, size_t n, void *stream);
+int pa_g2_add_mixed_batch_device(const pa_g2 *a, const pa_g2_affine *b, pa_g2 *out, size_t n, void *stream);
+int pa_g1_into_affine_batch_device(const pa_g1 *a, pa_g1_affine *out, size_t n, void *stream);
+int pa_g2_into_affine_batch_device(const pa_g2 *a, pa_g2_affine *out, size_t n, void *stream);
 int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
                                       void *stream);
 int pa_final_exponentiation_batch_device(const pa_fq12 *in, pa_fq12 *out, uint8_t *ok, size_t n, void *stream);

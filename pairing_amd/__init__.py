@@ -16,7 +16,7 @@ Device-resident entry points for torch tensors live in `pairing_amd.device`.
 """
 import numpy as np
 
-from ._native import (W_FQ, W_FQ2, W_FQ6, W_FQ12, W_FR, W_G1A, W_G1, W_G2A, W_G2, W_G2P, PairingError,
+from ._native import (W_FQ, W_FQ2, W_FQ6, W_FQ12, W_FR, W_G1A, W_G1, W_G2A, W_G2, W_G2P, PairingError, _lib,
                       as_rows, call, device_count, ptr, set_device, set_pairing_kernel, version)
 
 __all__ = [
@@ -24,6 +24,7 @@ __all__ = [
     "fq_mul", "fq_square", "fq_add", "fq_sub", "fq_inverse",
     "fq2_mul", "fq2_square", "fq6_mul", "fq12_mul", "fq12_square", "fq12_inverse",
     "fq12_frobenius_map", "fq12_cyclotomic_square", "fq12_mul_by_014",
+    "fq2_inverse", "fq2_frobenius_map", "fq6_square", "fq6_inverse", "fq6_frobenius_map", "fq_pow", "fq12_pow",
     "g1_batch_normalization", "g1_wnaf_fixed_base",
     "g2_prepare", "miller_loop_batch", "multi_miller_loop", "final_exponentiation", "pairing",
     "multi_miller_loop_affine", "multi_pairing", "pairing_multi_gpu",
@@ -31,6 +32,11 @@ __all__ = [
     "fr_mul", "fr_square", "fr_add", "fr_sub", "fr_double", "fr_negate", "fr_inverse",
     "fr_from_repr", "fr_into_repr", "fr_pow", "fr_legendre", "fr_sqrt",
     "g1_affine_mul", "g2_affine_mul", "g1_mul_assign", "g2_mul_assign", "g1_multiexp", "g2_multiexp",
+    "g1_double", "g2_double", "g1_add", "g2_add", "g1_add_mixed", "g2_add_mixed", "g1_negate", "g2_negate",
+    "g1_sub", "g2_sub", "g1_into_affine", "g2_into_affine", "g1_into_projective", "g2_into_projective",
+    "g2_batch_normalization", "g2_wnaf_fixed_base",
+    "g1_recommended_wnaf_for_scalar", "g2_recommended_wnaf_for_scalar",
+    "g1_recommended_wnaf_for_num_scalars", "g2_recommended_wnaf_for_num_scalars",
 ]
 
 
@@ -111,6 +117,56 @@ def fq12_cyclotomic_square(a):
 
 def fq12_inverse(a):
     return _inverse("pa_fq12_inverse_batch", a, W_FQ12)
+
+
+def fq2_inverse(a):
+    """Fq2::inverse (fq2.rs:138-155): (values, ok)."""
+    return _inverse("pa_fq2_inverse_batch", a, W_FQ2)
+
+
+def fq2_frobenius_map(a, power):
+    """Fq2::frobenius_map (fq2.rs:157-159)."""
+    return _frob("pa_fq2_frobenius_map_batch", a, W_FQ2, power)
+
+
+def fq6_square(a):
+    """Fq6::square (fq6.rs:166-197)."""
+    return _unary("pa_fq6_square_batch", a, W_FQ6)
+
+
+def fq6_inverse(a):
+    """Fq6::inverse (fq6.rs:250-301): (values, ok)."""
+    return _inverse("pa_fq6_inverse_batch", a, W_FQ6)
+
+
+def fq6_frobenius_map(a, power):
+    """Fq6::frobenius_map (fq6.rs:157-164)."""
+    return _frob("pa_fq6_frobenius_map_batch", a, W_FQ6, power)
+
+
+def _frob(name, a, width, power):
+    a = as_rows(a, width, "a")
+    out = np.empty_like(a)
+    call(name, ptr(a), ptr(out), a.shape[0], int(power))
+    return out
+
+
+def _pow(name, a, width, exp_limbs):
+    a = as_rows(a, width, "a")
+    e = np.ascontiguousarray(np.asarray(exp_limbs, dtype=np.uint64).reshape(-1))
+    out = np.empty_like(a)
+    call(name, ptr(a), ptr(e), e.size, ptr(out), a.shape[0])
+    return out
+
+
+def fq_pow(a, exp_limbs):
+    """Field::pow (lib.rs:306-324) for Fq, one exponent (u64 LE limbs) for every element."""
+    return _pow("pa_fq_pow_batch", a, W_FQ, exp_limbs)
+
+
+def fq12_pow(a, exp_limbs):
+    """Field::pow (lib.rs:306-324) for Fq12."""
+    return _pow("pa_fq12_pow_batch", a, W_FQ12, exp_limbs)
 
 
 def fq12_frobenius_map(a, power):
@@ -418,3 +474,131 @@ def g1_multiexp(bases, scalars):
 
 def g2_multiexp(bases, scalars):
     return _multiexp("pa_g2_multiexp", bases, scalars, W_G2A, W_G2)
+
+
+# ---- CurveProjective / CurveAffine surface for G1 and G2 (ec.rs:1-621) ----
+_JW = {1: W_G1, 2: W_G2}
+_AW = {1: W_G1A, 2: W_G2A}
+
+
+def _group_unary(group, op, a, in_width, out_width):
+    a = as_rows(a, in_width, "points")
+    out = np.zeros((a.shape[0], out_width), np.uint64)
+    call("pa_g%d_%s_batch" % (group, op), ptr(a), ptr(out), a.shape[0])
+    return out
+
+
+def _group_binary(group, op, a, b, b_width):
+    a = as_rows(a, _JW[group], "a")
+    b = as_rows(b, b_width, "b")
+    if a.shape[0] != b.shape[0]:
+        raise ValueError("operand lengths differ: %d vs %d" % (a.shape[0], b.shape[0]))
+    out = np.zeros_like(a)
+    call("pa_g%d_%s_batch" % (group, op), ptr(a), ptr(b), ptr(out), a.shape[0])
+    return out
+
+
+def g1_double(a):
+    """CurveProjective::double (dbl-2009-l, ec.rs:296-354), Jacobian words bit-exact."""
+    return _group_unary(1, "double", a, W_G1, W_G1)
+
+
+def g2_double(a):
+    return _group_unary(2, "double", a, W_G2, W_G2)
+
+
+def g1_add(a, b):
+    """CurveProjective::add_assign (add-2007-bl, ec.rs:356-444)."""
+    return _group_binary(1, "add", a, b, W_G1)
+
+
+def g2_add(a, b):
+    return _group_binary(2, "add", a, b, W_G2)
+
+
+def g1_add_mixed(a, b):
+    """CurveProjective::add_assign_mixed (madd-2007-bl, ec.rs:446-526), b affine."""
+    return _group_binary(1, "add_mixed", a, b, W_G1A)
+
+
+def g2_add_mixed(a, b):
+    return _group_binary(2, "add_mixed", a, b, W_G2A)
+
+
+def g1_negate(a):
+    """CurveProjective::negate (ec.rs:528-532)."""
+    return _group_unary(1, "negate", a, W_G1, W_G1)
+
+
+def g2_negate(a):
+    return _group_unary(2, "negate", a, W_G2, W_G2)
+
+
+def g1_sub(a, b):
+    """CurveProjective::sub_assign = negate + add_assign (lib.rs:156-160)."""
+    return _group_binary(1, "sub", a, b, W_G1)
+
+
+def g2_sub(a, b):
+    return _group_binary(2, "sub", a, b, W_G2)
+
+
+def g1_into_affine(a):
+    """CurveProjective::into_affine (ec.rs:586-619)."""
+    return _group_unary(1, "into_affine", a, W_G1, W_G1A)
+
+
+def g2_into_affine(a):
+    return _group_unary(2, "into_affine", a, W_G2, W_G2A)
+
+
+def g1_into_projective(a):
+    """CurveAffine::into_projective (ec.rs:570-582)."""
+    return _group_unary(1, "into_projective", a, W_G1A, W_G1)
+
+
+def g2_into_projective(a):
+    return _group_unary(2, "into_projective", a, W_G2A, W_G2)
+
+
+def g2_batch_normalization(v):
+    """G2 CurveProjective::batch_normalization (ec.rs:246-294); returns the normalized copy."""
+    v = as_rows(v, W_G2, "v").copy()
+    call("pa_g2_batch_normalization", ptr(v), v.shape[0])
+    return v
+
+
+def g2_wnaf_fixed_base(base, scalars):
+    """G2 Wnaf::new().base(base, n).scalar(s) (wnaf.rs:93-107, 169-178): points equal to s_i * base."""
+    b = as_rows(base, W_G2, "base")
+    s = as_rows(scalars, 4, "scalars")
+    out = np.empty((s.shape[0], W_G2), np.uint64)
+    call("pa_g2_wnaf_fixed_base", ptr(b), ptr(s), s.shape[0], ptr(out))
+    return out
+
+
+def _window(name, arg):
+    w = getattr(_lib, name)(arg)
+    if w <= 0:
+        raise PairingError("%s failed (%d)" % (name, w))
+    return w
+
+
+def g1_recommended_wnaf_for_scalar(scalar):
+    """CurveProjective::recommended_wnaf_for_scalar for G1 (ec.rs:895-905), scalar a FrRepr row."""
+    s = as_rows(scalar, 4, "scalar")
+    return _window("pa_g1_recommended_wnaf_for_scalar", ptr(s))
+
+
+def g2_recommended_wnaf_for_scalar(scalar):
+    s = as_rows(scalar, 4, "scalar")
+    return _window("pa_g2_recommended_wnaf_for_scalar", ptr(s))
+
+
+def g1_recommended_wnaf_for_num_scalars(n):
+    """CurveProjective::recommended_wnaf_for_num_scalars for G1 (ec.rs:907-921)."""
+    return _window("pa_g1_recommended_wnaf_for_num_scalars", int(n))
+
+
+def g2_recommended_wnaf_for_num_scalars(n):
+    return _window("pa_g2_recommended_wnaf_for_num_scalars", int(n))

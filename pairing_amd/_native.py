@@ -12,6 +12,7 @@ include/pairing_amd.h):
 """
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -30,7 +31,31 @@ class PairingError(RuntimeError):
     """A negative status code from the C ABI (see include/pairing_amd.h)."""
 
 
+def _share_torch_hip_runtime():
+    """Make this library and torch use ONE HIP runtime in the process.
+
+    The torch wheel ships its own libamdhip64.so (soname libamdhip64.so.7,
+    loaded by torch's libc10_hip through RPATH $ORIGIN), while
+    libpairing_amd.so needs libamdhip64.so.7 from /opt/rocm.  Imported after
+    torch, this library binds to torch's runtime by soname; imported before
+    it, two runtimes would end up in the process and torch's would find no
+    device.  So torch's runtime file is loaded first (without importing
+    torch): a later `import torch` then reuses it (same file), and the
+    stream handles and device pointers of the device.py layer belong to the
+    runtime that launches our kernels.  PA_SYSTEM_HIP=1 keeps /opt/rocm's."""
+    if "torch" in sys.modules or os.environ.get("PA_SYSTEM_HIP") == "1":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    path = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
 def _load():
+    _share_torch_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             "pairing_amd: HIP library %s is missing -- build it with "
@@ -110,6 +135,30 @@ _SIGS = {
     "pa_g1_multiexp_device": [_P, _P, _N, _P, _P, _N, _P],
     "pa_g2_multiexp_device": [_P, _P, _N, _P, _P, _N, _P],
 }
+for _g in (1, 2):
+    for _op in ("double", "negate", "into_affine", "into_projective"):
+        _SIGS["pa_g%d_%s_batch" % (_g, _op)] = [_P, _P, _N]
+    for _op in ("add", "add_mixed", "sub"):
+        _SIGS["pa_g%d_%s_batch" % (_g, _op)] = [_P, _P, _P, _N]
+    for _op in ("double", "into_affine"):
+        _SIGS["pa_g%d_%s_batch_device" % (_g, _op)] = [_P, _P, _N, _P]
+    for _op in ("add", "add_mixed"):
+        _SIGS["pa_g%d_%s_batch_device" % (_g, _op)] = [_P, _P, _P, _N, _P]
+    _SIGS["pa_g%d_recommended_wnaf_for_scalar" % _g] = [_P]
+    _SIGS["pa_g%d_recommended_wnaf_for_num_scalars" % _g] = [_N]
+_SIGS.update({
+    "pa_fq2_inverse_batch": [_P, _P, _P, _N],
+    "pa_fq2_frobenius_map_batch": [_P, _P, _N, _N],
+    "pa_fq6_square_batch": [_P, _P, _N],
+    "pa_fq6_inverse_batch": [_P, _P, _P, _N],
+    "pa_fq6_frobenius_map_batch": [_P, _P, _N, _N],
+    "pa_fq_pow_batch": [_P, _P, _N, _P, _N],
+    "pa_fq12_pow_batch": [_P, _P, _N, _P, _N],
+    "pa_g2_batch_normalization": [_P, _N],
+    "pa_g2_batch_normalization_device": [_P, _N, _P],
+    "pa_g2_wnaf_fixed_base": [_P, _P, _N, _P],
+    "pa_g2_wnaf_fixed_base_device": [_P, _P, _P, _N, _P, _P, _P],
+})
 for _name, _args in _SIGS.items():
     _fn = getattr(_lib, _name)
     _fn.argtypes = _args
@@ -117,6 +166,8 @@ for _name, _args in _SIGS.items():
 _lib.pa_version.restype = ctypes.c_char_p
 _lib.pa_g1_fixed_base_table_words.restype = ctypes.c_size_t
 _lib.pa_g1_fixed_base_workspace_words.restype = ctypes.c_size_t
+_lib.pa_g2_fixed_base_table_words.restype = ctypes.c_size_t
+_lib.pa_g2_fixed_base_workspace_words.restype = ctypes.c_size_t
 _lib.pa_last_error.restype = ctypes.c_char_p
 _lib.pa_multiexp_workspace_bytes.argtypes = [ctypes.c_int, _N]
 _lib.pa_multiexp_workspace_bytes.restype = ctypes.c_size_t

@@ -168,6 +168,46 @@ int pa_fq12_inverse_batch(const pa_fq12* a, pa_fq12* out, uint8_t* ok, size_t n)
 int pa_fq12_frobenius_map_batch(const pa_fq12* a, pa_fq12* out, size_t n, size_t power) {
     return host_field_op(pa::OP_FQ12_FROB, a, nullptr, out, nullptr, n, 576, 576, (int)(power % 12));
 }
+int pa_fq2_inverse_batch(const pa_fq2* a, pa_fq2* out, uint8_t* ok, size_t n) {
+    if (n && !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null ok");
+    return host_field_op(pa::OP_FQ2_INV, a, nullptr, out, ok, n, 96, 96, 0);
+}
+int pa_fq2_frobenius_map_batch(const pa_fq2* a, pa_fq2* out, size_t n, size_t power) {
+    return host_field_op(pa::OP_FQ2_FROB, a, nullptr, out, nullptr, n, 96, 96, (int)(power % 2));
+}
+int pa_fq6_square_batch(const pa_fq6* a, pa_fq6* out, size_t n) {
+    return host_field_op(pa::OP_FQ6_SQR, a, nullptr, out, nullptr, n, 288, 288, 0);
+}
+int pa_fq6_inverse_batch(const pa_fq6* a, pa_fq6* out, uint8_t* ok, size_t n) {
+    if (n && !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null ok");
+    return host_field_op(pa::OP_FQ6_INV, a, nullptr, out, ok, n, 288, 288, 0);
+}
+int pa_fq6_frobenius_map_batch(const pa_fq6* a, pa_fq6* out, size_t n, size_t power) {
+    return host_field_op(pa::OP_FQ6_FROB, a, nullptr, out, nullptr, n, 288, 288, (int)(power % 6));
+}
+namespace {
+int host_field_pow(int op, const void* a, const uint64_t* exp, size_t exp_words, void* out, size_t n,
+                   size_t bytes) {
+    if (n == 0) return PA_OK;
+    if (!a || !out || (exp_words && !exp)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (exp_words > (1u << 20)) return fail(PA_ERR_INVALID_ARGUMENT, "exponent too long");
+    DevBuf da, de, dout;
+    int rc;
+    if ((rc = upload(da, a, bytes * n)) || (rc = upload(de, exp, 8 * exp_words))) return rc;
+    PA_TRY(dout.alloc(bytes * n), "hipMalloc");
+    PA_TRY(pa::launch_field_op(op, da.as<uint64_t>(), de.as<uint64_t>(), dout.as<uint64_t>(), nullptr, n,
+                               (int)exp_words, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, bytes * n);
+}
+}  // namespace
+int pa_fq_pow_batch(const pa_fq* a, const uint64_t* exp, size_t exp_words, pa_fq* out, size_t n) {
+    return host_field_pow(pa::OP_FQ_POW, a, exp, exp_words, out, n, 48);
+}
+int pa_fq12_pow_batch(const pa_fq12* a, const uint64_t* exp, size_t exp_words, pa_fq12* out, size_t n) {
+    return host_field_pow(pa::OP_FQ12_POW, a, exp, exp_words, out, n, 576);
+}
 // not in the public header: cyclotomic squaring, exposed for the parity tests
 int pa_fq12_cyclotomic_square_batch(const pa_fq12* a, pa_fq12* out, size_t n) {
     return host_field_op(pa::OP_FQ12_CYC_SQR, a, nullptr, out, nullptr, n, 576, 576, 0);
@@ -641,6 +681,153 @@ int pa_g2_multiexp_device(const pa_g2_affine* bases, const pa_fr_repr* scalars, 
                           workspace_bytes, (hipStream_t)stream),
            "kernel launch");
     return PA_OK;
+}
+
+// ---- CurveProjective / CurveAffine surface, G1 and G2 (kernels_group.hip) ----
+namespace {
+constexpr size_t jac_bytes(int group) { return group == 1 ? sizeof(pa_g1) : sizeof(pa_g2); }
+constexpr size_t aff_bytes(int group) { return group == 1 ? sizeof(pa_g1_affine) : sizeof(pa_g2_affine); }
+size_t op_in_bytes(int group, int op) { return op == pa::GROUP_FROM_AFFINE ? aff_bytes(group) : jac_bytes(group); }
+size_t op_b_bytes(int group, int op) {
+    if (op == pa::GROUP_ADD || op == pa::GROUP_SUB) return jac_bytes(group);
+    return op == pa::GROUP_ADD_MIXED ? aff_bytes(group) : 0;
+}
+size_t op_out_bytes(int group, int op) { return op == pa::GROUP_INTO_AFFINE ? aff_bytes(group) : jac_bytes(group); }
+
+int host_group_op(int group, int op, const void* a, const void* b, void* out, size_t n) {
+    if (n == 0) return PA_OK;
+    const size_t ib = op_in_bytes(group, op), bb = op_b_bytes(group, op), ob = op_out_bytes(group, op);
+    if (!a || !out || (bb && !b)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf da, db, dout;
+    int rc;
+    if ((rc = upload(da, a, ib * n))) return rc;
+    if (bb && (rc = upload(db, b, bb * n))) return rc;
+    PA_TRY(dout.alloc(ob * n), "hipMalloc");
+    PA_TRY(pa::launch_group_op(group, op, da.as<uint64_t>(), db.as<uint64_t>(), dout.as<uint64_t>(), n, nullptr),
+           "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, ob * n);
+}
+int device_group_op(int group, int op, const void* a, const void* b, void* out, size_t n, void* stream) {
+    if (n && (!a || !out || (op_b_bytes(group, op) && !b))) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_group_op(group, op, (const uint64_t*)a, (const uint64_t*)b, (uint64_t*)out, n,
+                               (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+
+// FrRepr::num_bits (fr.rs:58 via the repr macro): 256 minus leading zeros
+int repr_num_bits(const pa_fr_repr* s) {
+    for (int w = 3; w >= 0; w--)
+        if (s->l[w]) return 64 * w + 64 - __builtin_clzll(s->l[w]);
+    return 0;
+}
+int window_for_count(size_t n, const size_t* rec, int m) {
+    int ret = 4;
+    for (int k = 0; k < m && n > rec[k]; k++) ret++;
+    return ret;
+}
+}  // namespace
+
+#define PA_GROUP_ENTRIES(G, JAC, AFF)                                                                            \
+    int pa_g##G##_double_batch(const JAC* a, JAC* out, size_t n) {                                              \
+        return host_group_op(G, pa::GROUP_DOUBLE, a, nullptr, out, n);                                          \
+    }                                                                                                           \
+    int pa_g##G##_add_batch(const JAC* a, const JAC* b, JAC* out, size_t n) {                                    \
+        return host_group_op(G, pa::GROUP_ADD, a, b, out, n);                                                   \
+    }                                                                                                           \
+    int pa_g##G##_add_mixed_batch(const JAC* a, const AFF* b, JAC* out, size_t n) {                              \
+        return host_group_op(G, pa::GROUP_ADD_MIXED, a, b, out, n);                                             \
+    }                                                                                                           \
+    int pa_g##G##_negate_batch(const JAC* a, JAC* out, size_t n) {                                              \
+        return host_group_op(G, pa::GROUP_NEGATE, a, nullptr, out, n);                                          \
+    }                                                                                                           \
+    int pa_g##G##_sub_batch(const JAC* a, const JAC* b, JAC* out, size_t n) {                                    \
+        return host_group_op(G, pa::GROUP_SUB, a, b, out, n);                                                   \
+    }                                                                                                           \
+    int pa_g##G##_into_affine_batch(const JAC* a, AFF* out, size_t n) {                                         \
+        return host_group_op(G, pa::GROUP_INTO_AFFINE, a, nullptr, out, n);                                     \
+    }                                                                                                           \
+    int pa_g##G##_into_projective_batch(const AFF* a, JAC* out, size_t n) {                                     \
+        return host_group_op(G, pa::GROUP_FROM_AFFINE, a, nullptr, out, n);                                     \
+    }                                                                                                           \
+    int pa_g##G##_double_batch_device(const JAC* a, JAC* out, size_t n, void* stream) {                         \
+        return device_group_op(G, pa::GROUP_DOUBLE, a, nullptr, out, n, stream);                                \
+    }                                                                                                           \
+    int pa_g##G##_add_batch_device(const JAC* a, const JAC* b, JAC* out, size_t n, void* stream) {              \
+        return device_group_op(G, pa::GROUP_ADD, a, b, out, n, stream);                                         \
+    }                                                                                                           \
+    int pa_g##G##_add_mixed_batch_device(const JAC* a, const AFF* b, JAC* out, size_t n, void* stream) {        \
+        return device_group_op(G, pa::GROUP_ADD_MIXED, a, b, out, n, stream);                                   \
+    }                                                                                                           \
+    int pa_g##G##_into_affine_batch_device(const JAC* a, AFF* out, size_t n, void* stream) {                    \
+        return device_group_op(G, pa::GROUP_INTO_AFFINE, a, nullptr, out, n, stream);                           \
+    }
+
+PA_GROUP_ENTRIES(1, pa_g1, pa_g1_affine)
+PA_GROUP_ENTRIES(2, pa_g2, pa_g2_affine)
+#undef PA_GROUP_ENTRIES
+
+int pa_g2_batch_normalization(pa_g2* v, size_t n) {
+    if (n == 0) return PA_OK;
+    if (!v) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf dv;
+    int rc;
+    if ((rc = upload(dv, v, sizeof(pa_g2) * n))) return rc;
+    PA_TRY(pa::launch_g2_batch_normalize(dv.as<uint64_t>(), n, nullptr), "kernel launch");
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(v, dv, sizeof(pa_g2) * n);
+}
+int pa_g2_batch_normalization_device(pa_g2* v, size_t n, void* stream) {
+    if (n && !v) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g2_batch_normalize((uint64_t*)v, n, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
+size_t pa_g2_fixed_base_table_words(void) { return pa::g2_comb_table_words(); }
+size_t pa_g2_fixed_base_workspace_words(void) { return pa::g2_comb_workspace_words(); }
+int pa_g2_wnaf_fixed_base_device(const pa_g2* base, const pa_fr_repr* scalars, pa_g2* out, size_t n,
+                                 uint64_t* table, uint64_t* workspace, void* stream) {
+    if (n == 0) return PA_OK;
+    if (!base || !scalars || !out || !table || !workspace) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g2_comb_table((const uint64_t*)base, table, workspace, (hipStream_t)stream), "kernel launch");
+    PA_TRY(pa::launch_g2_comb_mul(table, (const uint64_t*)scalars, (uint64_t*)out, n, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+int pa_g2_wnaf_fixed_base(const pa_g2* base, const pa_fr_repr* scalars, size_t n, pa_g2* out) {
+    if (n == 0) return PA_OK;
+    if (!base || !scalars || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf db, ds, dt, dw, dout;
+    int rc;
+    if ((rc = upload(db, base, sizeof(pa_g2))) || (rc = upload(ds, scalars, sizeof(pa_fr_repr) * n))) return rc;
+    PA_TRY(dt.alloc(8 * pa::g2_comb_table_words()), "hipMalloc");
+    PA_TRY(dw.alloc(8 * pa::g2_comb_workspace_words()), "hipMalloc");
+    PA_TRY(dout.alloc(sizeof(pa_g2) * n), "hipMalloc");
+    if ((rc = pa_g2_wnaf_fixed_base_device(db.as<pa_g2>(), ds.as<pa_fr_repr>(), dout.as<pa_g2>(), n,
+                                           dt.as<uint64_t>(), dw.as<uint64_t>(), nullptr)))
+        return rc;
+    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    return download(out, dout, sizeof(pa_g2) * n);
+}
+
+// window heuristics (ec.rs:895-921 for G1, 1586-1612 for G2)
+int pa_g1_recommended_wnaf_for_scalar(const pa_fr_repr* s) {
+    if (!s) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const int b = repr_num_bits(s);
+    return b >= 130 ? 4 : b >= 34 ? 3 : 2;
+}
+int pa_g2_recommended_wnaf_for_scalar(const pa_fr_repr* s) {
+    if (!s) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const int b = repr_num_bits(s);
+    return b >= 103 ? 4 : b >= 37 ? 3 : 2;
+}
+int pa_g1_recommended_wnaf_for_num_scalars(size_t num_scalars) {
+    static const size_t rec[12] = {1, 3, 7, 20, 43, 120, 273, 563, 1630, 3128, 7933, 62569};
+    return window_for_count(num_scalars, rec, 12);
+}
+int pa_g2_recommended_wnaf_for_num_scalars(size_t num_scalars) {
+    static const size_t rec[11] = {1, 3, 8, 20, 47, 126, 260, 826, 1501, 4555, 84071};
+    return window_for_count(num_scalars, rec, 11);
 }
 
 }  // extern "C"

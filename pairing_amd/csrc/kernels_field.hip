@@ -51,6 +51,28 @@ __global__ void __launch_bounds__(256) k_fq_mul_batch(const uint64_t* __restrict
     }
 }
 
+// Field::pow, lib.rs:306-324: square-and-multiply over the exponent's bits,
+// most significant first (BitIterator, lib.rs:582-610); leading zeros square
+// one, so starting at the top set bit gives the same value.
+template <class F>
+PA_DEV void field_pow(F& r, const F& x, const uint64_t* exp, int words) {
+    one(r);
+    bool started = false;
+#pragma unroll 1
+    for (int w = words - 1; w >= 0; w--) {
+        const uint64_t e = exp[w];
+#pragma unroll 1
+        for (int bit = 63; bit >= 0; bit--) {
+            if (started) sqr(r, r);
+            if ((e >> bit) & 1) {
+                if (started) mul(r, r, x);
+                else r = x;
+                started = true;
+            }
+        }
+    }
+}
+
 template <int OP>
 __global__ void __launch_bounds__(64) k_field_op(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
@@ -75,6 +97,35 @@ __global__ void __launch_bounds__(64) k_field_op(const uint64_t* __restrict__ a,
             ok[i] = k ? 1 : 0;
         }
         fq_store(out + 6 * i, z);
+    } else if constexpr (OP == OP_FQ_POW) {
+        Fq x, z;
+        fq_load(x, a + 6 * i);
+        field_pow(z, x, b, param);
+        fq_store(out + 6 * i, z);
+    } else if constexpr (OP == OP_FQ2_INV || OP == OP_FQ2_FROB) {
+        Fq2 x, z;
+        load(x, a + 12 * i);
+        if constexpr (OP == OP_FQ2_INV) {
+            const bool k = inverse(z, x);
+            if (!k) zero(z);
+            ok[i] = k ? 1 : 0;
+        } else {
+            frobenius_map(z, x, param);
+        }
+        store(out + 12 * i, z);
+    } else if constexpr (OP == OP_FQ6_SQR || OP == OP_FQ6_INV || OP == OP_FQ6_FROB) {
+        Fq6 x, z;
+        load(x, a + 36 * i);
+        if constexpr (OP == OP_FQ6_SQR) {
+            sqr(z, x);
+        } else if constexpr (OP == OP_FQ6_INV) {
+            const bool k = inverse(z, x);
+            if (!k) zero(z);
+            ok[i] = k ? 1 : 0;
+        } else {
+            frobenius_map(z, x, param);
+        }
+        store(out + 36 * i, z);
     } else if constexpr (OP == OP_FQ2_MUL || OP == OP_FQ2_SQR) {
         Fq2 x, y, z;
         load(x, a + 12 * i);
@@ -108,6 +159,8 @@ __global__ void __launch_bounds__(64) k_field_op(const uint64_t* __restrict__ a,
             frobenius_map(z, x, param);
         } else if constexpr (OP == OP_FQ12_CYC_SQR) {
             cyclotomic_sqr(z, x);
+        } else if constexpr (OP == OP_FQ12_POW) {
+            field_pow(z, x, b, param);
         }
         store(out + 72 * i, z);
     }
@@ -165,6 +218,13 @@ hipError_t launch_field_op(int op, const uint64_t* a, const uint64_t* b, uint64_
         PA_CASE(OP_FQ12_INV)
         PA_CASE(OP_FQ12_FROB)
         PA_CASE(OP_FQ12_CYC_SQR)
+        PA_CASE(OP_FQ2_INV)
+        PA_CASE(OP_FQ2_FROB)
+        PA_CASE(OP_FQ6_SQR)
+        PA_CASE(OP_FQ6_INV)
+        PA_CASE(OP_FQ6_FROB)
+        PA_CASE(OP_FQ_POW)
+        PA_CASE(OP_FQ12_POW)
 #undef PA_CASE
         default: return hipErrorInvalidValue;
     }

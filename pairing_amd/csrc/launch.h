@@ -23,6 +23,13 @@ enum FieldOp : int {
     OP_FQ12_INV,
     OP_FQ12_FROB,
     OP_FQ12_CYC_SQR,
+    OP_FQ2_INV,
+    OP_FQ2_FROB,
+    OP_FQ6_SQR,
+    OP_FQ6_INV,
+    OP_FQ6_FROB,
+    OP_FQ_POW,     // b = exponent words (device), param = their count
+    OP_FQ12_POW,
 };
 
 // Generic elementwise field op: out[i] = op(a[i], b[i]); `ok` (may be null)
@@ -92,6 +99,32 @@ hipError_t launch_g1_comb_mul(const uint64_t* table_aff, const uint64_t* scalars
 // (a side stream per device; same result bits)
 hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
                                 uint64_t* table, uint64_t* workspace, hipStream_t stream);
+
+// CurveProjective / CurveAffine per-op batches for G1 (group 1) and G2
+// (group 2), kernels_group.hip.  Records: Jacobian 18 / 36 u64, affine
+// 13 / 25 u64.  `b` is Jacobian for ADD / SUB, affine for ADD_MIXED, unused
+// otherwise; INTO_AFFINE writes affine records, FROM_AFFINE reads them.
+enum GroupOp : int {
+    GROUP_DOUBLE = 0,
+    GROUP_ADD,
+    GROUP_ADD_MIXED,
+    GROUP_NEGATE,
+    GROUP_SUB,
+    GROUP_INTO_AFFINE,
+    GROUP_FROM_AFFINE,
+};
+hipError_t launch_group_op(int group, int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
+                           hipStream_t stream);
+// G2 batch_normalization in place (n Jacobian records of 36 u64)
+hipError_t launch_g2_batch_normalize(uint64_t* v, size_t n, hipStream_t stream);
+// G2 fixed-base comb: table (g2_comb_table_words() u64, affine records)
+// built from `base` using `workspace` (g2_comb_workspace_words() u64), then
+// out[i] = scalars[i] * base (Jacobian)
+size_t g2_comb_table_words();
+size_t g2_comb_workspace_words();
+hipError_t launch_g2_comb_table(const uint64_t* base, uint64_t* table, uint64_t* workspace, hipStream_t stream);
+hipError_t launch_g2_comb_mul(const uint64_t* table, const uint64_t* scalars, uint64_t* out, size_t n,
+                              hipStream_t stream);
 
 // Scalar field Fr (kernels_fr.hip).  `flag` receives the Option / Result byte
 // (inverse, from_repr, sqrt) or the LegendreSymbol as int8 (0, 1, -1);

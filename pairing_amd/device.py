@@ -9,7 +9,7 @@ import ctypes
 
 import torch
 
-from ._native import W_FQ, W_FQ12, W_G1, W_G1A, W_G2A, _lib, call
+from ._native import W_FQ, W_FQ12, W_G1, W_G1A, W_G2, W_G2A, _lib, call
 
 
 def _stream_ptr(stream):
@@ -88,6 +88,31 @@ def fixed_base_buffers(dev):
 
 def g1_batch_normalization(v, stream=None):
     call("pa_g1_batch_normalization_device", _dptr(v, W_G1, "v"), v.shape[0], _stream_ptr(stream))
+
+
+def g2_batch_normalization(v, stream=None):
+    call("pa_g2_batch_normalization_device", _dptr(v, W_G2, "v"), v.shape[0], _stream_ptr(stream))
+
+
+def g2_fixed_base_buffers(dev):
+    """(table, workspace) device buffers for g2_wnaf_fixed_base."""
+    table = torch.empty(int(_lib.pa_g2_fixed_base_table_words()), dtype=torch.int64, device=dev)
+    ws = torch.empty(int(_lib.pa_g2_fixed_base_workspace_words()), dtype=torch.int64, device=dev)
+    return table, ws
+
+
+def g2_wnaf_fixed_base(base, scalars, out, table, ws, stream=None):
+    """out[i] = scalars[i] * base for G2 (base a (1,36) Jacobian record)."""
+    call("pa_g2_wnaf_fixed_base_device", _dptr(base, W_G2, "base"), _dptr(scalars, 4, "scalars"),
+         _dptr(out, W_G2, "out"), scalars.shape[0], ctypes.c_void_p(table.data_ptr()),
+         ctypes.c_void_p(ws.data_ptr()), _stream_ptr(stream))
+
+
+def group_add(group, a, b, out, stream=None):
+    """CurveProjective::add_assign over Jacobian rows in HBM: out = a + b (group 1 or 2)."""
+    w = W_G1 if group == 1 else W_G2
+    call("pa_g%d_add_batch_device" % group, _dptr(a, w, "a"), _dptr(b, w, "b"), _dptr(out, w, "out"),
+         a.shape[0], _stream_ptr(stream))
 
 
 def decode(group, enc, compressed, checked, out, status, stream=None):
