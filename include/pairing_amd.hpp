@@ -4,10 +4,16 @@
 // The reference (`pairing` v0.14.2, Rust) exposes the path as traits:
 //   Engine::{miller_loop, final_exponentiation, pairing}   src/lib.rs:34-110
 //   CurveAffine::{prepare, pairing_with, into_compressed, ...} lib.rs:185-234
-//   CurveProjective::batch_normalization                    lib.rs:114-181
+//   CurveProjective::{double, add_assign, add_assign_mixed, negate,
+//     sub_assign, mul_assign, into_affine, batch_normalization,
+//     recommended_wnaf_*}                                    lib.rs:114-181
 //   EncodedPoint::{into_affine, into_affine_unchecked, from_affine} lib.rs:236-264
-//   Field / SqrtField::{mul_assign, square, inverse, sqrt}  lib.rs:267-345
-//   Wnaf::new().base(g, n).scalar(s)                         wnaf.rs:73-179
+//   CurveAffine::{mul, negate, into_projective}             lib.rs:185-234
+//   Field / SqrtField::{add_assign, sub_assign, double, negate, mul_assign,
+//     square, inverse, frobenius_map, pow, sqrt}            lib.rs:267-345
+//     on Fq, Fq2, Fq6, Fq12 (+ Fq12::conjugate)
+//   Wnaf::new().base(g, n).scalar(s), Wnaf::new().scalar(s).base(g),
+//     shared()                                              wnaf.rs:73-179
 // The classes below keep those names, argument meanings and error behaviour
 // (Option -> std::optional, Result<_, GroupDecodingError> -> a thrown
 // GroupDecodingError), so code written against the crate reads the same.
@@ -53,7 +59,51 @@ bool bytes_zero(const T& a) {
     std::memset(&z, 0, sizeof z);
     return bytes_equal(a, z);
 }
+
+// Componentwise add / sub / negate of a tower element as a batch of its
+// Fq coordinates (each Fq coordinate of Fq2/Fq6/Fq12 adds independently,
+// fq2.rs:103-121, fq6.rs:111-155, fq12.rs:50-88).
+template <class T>
+void fq_add_n(const T& a, const T& b, T& out) {
+    check(pa_fq_add_batch(reinterpret_cast<const pa_fq*>(&a), reinterpret_cast<const pa_fq*>(&b),
+                          reinterpret_cast<pa_fq*>(&out), sizeof(T) / sizeof(pa_fq)),
+          "add_assign");
+}
+template <class T>
+void fq_sub_n(const T& a, const T& b, T& out) {
+    check(pa_fq_sub_batch(reinterpret_cast<const pa_fq*>(&a), reinterpret_cast<const pa_fq*>(&b),
+                          reinterpret_cast<pa_fq*>(&out), sizeof(T) / sizeof(pa_fq)),
+          "sub_assign");
+}
+// Field::pow (lib.rs:306-324) by square-and-multiply over the trait's own
+// square / mul_assign, for the types without a pow entry point
+template <class F>
+F pow_generic(const F& x, const std::vector<uint64_t>& exp) {
+    F r = F::one();
+    for (size_t w = exp.size(); w-- > 0;)
+        for (int bit = 63; bit >= 0; bit--) {
+            r.square();
+            if ((exp[w] >> bit) & 1) r.mul_assign(x);
+        }
+    return r;
+}
 }  // namespace detail
+
+// The Field trait (lib.rs:267-325) on each type: zero, one, is_zero, square,
+// double, negate, add_assign, sub_assign, mul_assign, inverse,
+// frobenius_map, pow; SqrtField::sqrt where the reference has it.
+#define PA_FIELD_COMMON(T)                                                     \
+    bool is_zero() const { return detail::bytes_zero(v); }                     \
+    bool operator==(const T& o) const { return detail::bytes_equal(v, o.v); }  \
+    bool operator!=(const T& o) const { return !(*this == o); }                \
+    void add_assign(const T& o) { detail::fq_add_n(v, o.v, v); }               \
+    void sub_assign(const T& o) { detail::fq_sub_n(v, o.v, v); }               \
+    void double_() { add_assign(*this); }                                      \
+    void negate() {                                                            \
+        T z;                                                                   \
+        z.sub_assign(*this);                                                   \
+        *this = z;                                                             \
+    }
 
 class Fq {
 public:
@@ -64,24 +114,20 @@ public:
         std::memcpy(r.v.l, detail::kR, sizeof r.v.l);
         return r;
     }
-    bool is_zero() const { return detail::bytes_zero(v); }
-    bool operator==(const Fq& o) const { return detail::bytes_equal(v, o.v); }
-    bool operator!=(const Fq& o) const { return !(*this == o); }
+    PA_FIELD_COMMON(Fq)
     void mul_assign(const Fq& o) { check(pa_fq_mul_batch(&v, &o.v, &v, 1), "Fq::mul_assign"); }
     void square() { check(pa_fq_square_batch(&v, &v, 1), "Fq::square"); }
-    void add_assign(const Fq& o) { check(pa_fq_add_batch(&v, &o.v, &v, 1), "Fq::add_assign"); }
-    void sub_assign(const Fq& o) { check(pa_fq_sub_batch(&v, &o.v, &v, 1), "Fq::sub_assign"); }
-    void double_() { add_assign(*this); }
-    void negate() {
-        Fq z;
-        z.sub_assign(*this);
-        *this = z;
-    }
+    void frobenius_map(size_t) {}  // fq.rs:905-907: no effect in a prime field
     std::optional<Fq> inverse() const {
         Fq r;
         uint8_t ok = 0;
         check(pa_fq_inverse_batch(&v, &r.v, &ok, 1), "Fq::inverse");
         return ok ? std::optional<Fq>(r) : std::nullopt;
+    }
+    Fq pow(const std::vector<uint64_t>& exp) const {
+        Fq r;
+        check(pa_fq_pow_batch(&v, exp.empty() ? nullptr : exp.data(), exp.size(), &r.v, 1), "Fq::pow");
+        return r;
     }
     std::optional<Fq> sqrt() const {
         Fq r;
@@ -100,17 +146,45 @@ public:
         r.v.c0 = Fq::one().v;
         return r;
     }
-    bool is_zero() const { return detail::bytes_zero(v); }
-    bool operator==(const Fq2& o) const { return detail::bytes_equal(v, o.v); }
-    bool operator!=(const Fq2& o) const { return !(*this == o); }
+    PA_FIELD_COMMON(Fq2)
     void mul_assign(const Fq2& o) { check(pa_fq2_mul_batch(&v, &o.v, &v, 1), "Fq2::mul_assign"); }
     void square() { check(pa_fq2_square_batch(&v, &v, 1), "Fq2::square"); }
+    void frobenius_map(size_t power) { check(pa_fq2_frobenius_map_batch(&v, &v, 1, power), "Fq2::frobenius_map"); }
+    std::optional<Fq2> inverse() const {
+        Fq2 r;
+        uint8_t ok = 0;
+        check(pa_fq2_inverse_batch(&v, &r.v, &ok, 1), "Fq2::inverse");
+        return ok ? std::optional<Fq2>(r) : std::nullopt;
+    }
+    Fq2 pow(const std::vector<uint64_t>& exp) const { return detail::pow_generic(*this, exp); }
     std::optional<Fq2> sqrt() const {
         Fq2 r;
         uint8_t ok = 0;
         check(pa_fq2_sqrt_batch(&v, &r.v, &ok, 1), "Fq2::sqrt");
         return ok ? std::optional<Fq2>(r) : std::nullopt;
     }
+};
+
+class Fq6 {
+public:
+    pa_fq6 v{};
+    static Fq6 zero() { return Fq6(); }
+    static Fq6 one() {
+        Fq6 r;
+        r.v.c0 = Fq2::one().v;
+        return r;
+    }
+    PA_FIELD_COMMON(Fq6)
+    void mul_assign(const Fq6& o) { check(pa_fq6_mul_batch(&v, &o.v, &v, 1), "Fq6::mul_assign"); }
+    void square() { check(pa_fq6_square_batch(&v, &v, 1), "Fq6::square"); }
+    void frobenius_map(size_t power) { check(pa_fq6_frobenius_map_batch(&v, &v, 1, power), "Fq6::frobenius_map"); }
+    std::optional<Fq6> inverse() const {
+        Fq6 r;
+        uint8_t ok = 0;
+        check(pa_fq6_inverse_batch(&v, &r.v, &ok, 1), "Fq6::inverse");
+        return ok ? std::optional<Fq6>(r) : std::nullopt;
+    }
+    Fq6 pow(const std::vector<uint64_t>& exp) const { return detail::pow_generic(*this, exp); }
 };
 
 class Fq12 {
@@ -122,11 +196,14 @@ public:
         r.v.c0.c0.c0 = Fq::one().v;
         return r;
     }
-    bool is_zero() const { return detail::bytes_zero(v); }
-    bool operator==(const Fq12& o) const { return detail::bytes_equal(v, o.v); }
-    bool operator!=(const Fq12& o) const { return !(*this == o); }
+    PA_FIELD_COMMON(Fq12)
     void mul_assign(const Fq12& o) { check(pa_fq12_mul_batch(&v, &o.v, &v, 1), "Fq12::mul_assign"); }
     void square() { check(pa_fq12_square_batch(&v, &v, 1), "Fq12::square"); }
+    void conjugate() {  // fq12.rs:30-32
+        Fq6 c1{v.c1};
+        c1.negate();
+        v.c1 = c1.v;
+    }
     void frobenius_map(size_t power) {
         check(pa_fq12_frobenius_map_batch(&v, &v, 1, power), "Fq12::frobenius_map");
     }
@@ -136,7 +213,13 @@ public:
         check(pa_fq12_inverse_batch(&v, &r.v, &ok, 1), "Fq12::inverse");
         return ok ? std::optional<Fq12>(r) : std::nullopt;
     }
+    Fq12 pow(const std::vector<uint64_t>& exp) const {
+        Fq12 r;
+        check(pa_fq12_pow_batch(&v, exp.empty() ? nullptr : exp.data(), exp.size(), &r.v, 1), "Fq12::pow");
+        return r;
+    }
 };
+#undef PA_FIELD_COMMON
 
 // FrRepr: 4 x u64 little-endian canonical scalar (fr.rs:58)
 struct FrRepr {
@@ -239,34 +322,44 @@ private:
 };
 
 // ---------------- curve points (ec.rs) ----------------
-class G1 {  // Jacobian, zero iff z == 0 (ec.rs:224-240)
-public:
-    pa_g1 v{};
-    static G1 zero() {
-        G1 r;
-        r.v.y = Fq::one().v;
-        return r;
-    }
-    bool is_zero() const { return Fq{v.z}.is_zero(); }
-    // CurveProjective::batch_normalization (ec.rs:246-294)
-    static void batch_normalization(std::vector<G1>& v) {
-        check(pa_g1_batch_normalization(v.empty() ? nullptr : &v[0].v, v.size()), "G1::batch_normalization");
-    }
-    inline class G1Affine into_affine() const;   // ec.rs:586-619
-};
-
 class G1Prepared;
 class G2Prepared;
+template <int G> class Projective;
+using G1 = Projective<1>;   // Jacobian, zero iff z == 0 (ec.rs:224-240)
+using G2 = Projective<2>;
+
+// The affine half of the curve_impl! macro (ec.rs:13-29, 97-189) for either group.
+#define PA_AFFINE_COMMON(A, RAW, PROJ, BASE, G)                                                     \
+    RAW v{};                                                                                       \
+    static A zero() { /* ec.rs:158-164 */                                                          \
+        A r;                                                                                       \
+        r.v.y = BASE::one().v;                                                                     \
+        r.v.infinity = 1;                                                                          \
+        return r;                                                                                  \
+    }                                                                                              \
+    bool is_zero() const { return v.infinity != 0; }                                               \
+    bool operator==(const A& o) const {                                                            \
+        return v.infinity == o.v.infinity &&                                                       \
+               (v.infinity || (detail::bytes_equal(v.x, o.v.x) && detail::bytes_equal(v.y, o.v.y))); \
+    }                                                                                              \
+    bool operator!=(const A& o) const { return !(*this == o); }                                    \
+    /* CurveAffine::negate, ec.rs:166-172 */                                                       \
+    void negate() {                                                                                \
+        if (!is_zero()) {                                                                          \
+            BASE y{v.y};                                                                           \
+            y.negate();                                                                            \
+            v.y = y.v;                                                                             \
+        }                                                                                          \
+    }                                                                                              \
+    /* CurveAffine::into_projective, ec.rs:570-582 */                                              \
+    inline PROJ into_projective() const;                                                           \
+    /* CurveAffine::mul, ec.rs:174-177: the reference's double-and-add, bit-exact Jacobian words */ \
+    inline PROJ mul(const FrRepr& s) const;                                                        \
+    static inline std::vector<PROJ> mul_batch(const std::vector<A>& p, const std::vector<FrRepr>& s);
 
 class G1Affine {
 public:
-    pa_g1_affine v{};
-    static G1Affine zero() {  // ec.rs:158-164
-        G1Affine r;
-        r.v.y = Fq::one().v;
-        r.v.infinity = 1;
-        return r;
-    }
+    PA_AFFINE_COMMON(G1Affine, pa_g1_affine, G1, Fq, 1)
     static G1Affine one() {  // ec.rs:877-883 (fq.rs generator words)
         G1Affine r;
         const uint64_t x[6] = {0x5cb38790fd530c16ULL, 0x7817fc679976fff5ULL, 0x154f95c7143ba1c1ULL,
@@ -277,18 +370,6 @@ public:
         std::memcpy(r.v.y.l, y, 48);
         return r;
     }
-    bool is_zero() const { return v.infinity != 0; }
-    bool operator==(const G1Affine& o) const {
-        return v.infinity == o.v.infinity && (v.infinity || (detail::bytes_equal(v.x, o.v.x) && detail::bytes_equal(v.y, o.v.y)));
-    }
-    G1 into_projective() const {
-        if (is_zero()) return G1::zero();
-        G1 r;
-        r.v.x = v.x;
-        r.v.y = v.y;
-        r.v.z = Fq::one().v;
-        return r;
-    }
     G1Prepared prepare() const;
     Fq12 pairing_with(const G2Affine& other) const;
     Encoded<G1Affine, 1, false> into_uncompressed() const { return Encoded<G1Affine, 1, false>::from_affine(*this); }
@@ -297,13 +378,7 @@ public:
 
 class G2Affine {
 public:
-    pa_g2_affine v{};
-    static G2Affine zero() {
-        G2Affine r;
-        r.v.y.c0 = Fq::one().v;
-        r.v.infinity = 1;
-        return r;
-    }
+    PA_AFFINE_COMMON(G2Affine, pa_g2_affine, G2, Fq2, 2)
     static G2Affine one() {  // ec.rs:1543-1555
         G2Affine r;
         const uint64_t xc0[6] = {0xf5f28fa202940a10ULL, 0xb3f5fb2687b4961aULL, 0xa1a893b53e2ae580ULL,
@@ -320,15 +395,168 @@ public:
         std::memcpy(r.v.y.c1.l, yc1, 48);
         return r;
     }
-    bool is_zero() const { return v.infinity != 0; }
-    bool operator==(const G2Affine& o) const {
-        return v.infinity == o.v.infinity && (v.infinity || (detail::bytes_equal(v.x, o.v.x) && detail::bytes_equal(v.y, o.v.y)));
-    }
     G2Prepared prepare() const;
     Fq12 pairing_with(const G1Affine& other) const;
     Encoded<G2Affine, 2, false> into_uncompressed() const { return Encoded<G2Affine, 2, false>::from_affine(*this); }
     Encoded<G2Affine, 2, true> into_compressed() const { return Encoded<G2Affine, 2, true>::from_affine(*this); }
 };
+#undef PA_AFFINE_COMMON
+
+// The C ABI of each group, for the Projective template
+template <int G> struct GroupAbi;
+template <> struct GroupAbi<1> {
+    using Raw = pa_g1;
+    using RawAffine = pa_g1_affine;
+    using Affine = G1Affine;
+    using Base = Fq;
+    static constexpr auto dbl = &pa_g1_double_batch;
+    static constexpr auto add = &pa_g1_add_batch;
+    static constexpr auto add_mixed = &pa_g1_add_mixed_batch;
+    static constexpr auto neg = &pa_g1_negate_batch;
+    static constexpr auto sub = &pa_g1_sub_batch;
+    static constexpr auto to_affine = &pa_g1_into_affine_batch;
+    static constexpr auto from_affine = &pa_g1_into_projective_batch;
+    static constexpr auto normalize = &pa_g1_batch_normalization;
+    static constexpr auto mul_assign = &pa_g1_mul_assign_batch;
+    static constexpr auto affine_mul = &pa_g1_affine_mul_batch;
+    static constexpr auto fixed_base = &pa_g1_wnaf_fixed_base;
+    static constexpr auto window_for_scalar = &pa_g1_recommended_wnaf_for_scalar;
+    static constexpr auto window_for_count = &pa_g1_recommended_wnaf_for_num_scalars;
+    static constexpr auto multiexp = &pa_g1_multiexp;
+};
+template <> struct GroupAbi<2> {
+    using Raw = pa_g2;
+    using RawAffine = pa_g2_affine;
+    using Affine = G2Affine;
+    using Base = Fq2;
+    static constexpr auto dbl = &pa_g2_double_batch;
+    static constexpr auto add = &pa_g2_add_batch;
+    static constexpr auto add_mixed = &pa_g2_add_mixed_batch;
+    static constexpr auto neg = &pa_g2_negate_batch;
+    static constexpr auto sub = &pa_g2_sub_batch;
+    static constexpr auto to_affine = &pa_g2_into_affine_batch;
+    static constexpr auto from_affine = &pa_g2_into_projective_batch;
+    static constexpr auto normalize = &pa_g2_batch_normalization;
+    static constexpr auto mul_assign = &pa_g2_mul_assign_batch;
+    static constexpr auto affine_mul = &pa_g2_affine_mul_batch;
+    static constexpr auto fixed_base = &pa_g2_wnaf_fixed_base;
+    static constexpr auto window_for_scalar = &pa_g2_recommended_wnaf_for_scalar;
+    static constexpr auto window_for_count = &pa_g2_recommended_wnaf_for_num_scalars;
+    static constexpr auto multiexp = &pa_g2_multiexp;
+};
+
+// CurveProjective (lib.rs:114-181) for G1 / G2: every operation is the
+// reference's formula sequence on the GPU (bit-exact Jacobian words);
+// operator== is the reference's representation-independent PartialEq
+// (ec.rs:45-85).  The *_batch statics make one ABI call for a whole vector.
+template <int G>
+class Projective {
+public:
+    using Abi = GroupAbi<G>;
+    using Affine = typename Abi::Affine;
+    using Base = typename Abi::Base;
+    typename Abi::Raw v{};
+
+    static Projective zero() {  // ec.rs:224-230
+        Projective r;
+        r.v.y = Base::one().v;
+        return r;
+    }
+    static Projective one() { return Affine::one().into_projective(); }  // ec.rs:232-234
+    bool is_zero() const { return Base{v.z}.is_zero(); }
+    bool is_normalized() const { return is_zero() || Base{v.z} == Base::one(); }  // ec.rs:242-244
+
+    void double_() { check(Abi::dbl(&v, &v, 1), "CurveProjective::double"); }
+    void add_assign(const Projective& o) { check(Abi::add(&v, &o.v, &v, 1), "CurveProjective::add_assign"); }
+    void add_assign_mixed(const Affine& o) {
+        check(Abi::add_mixed(&v, &o.v, &v, 1), "CurveProjective::add_assign_mixed");
+    }
+    void negate() { check(Abi::neg(&v, &v, 1), "CurveProjective::negate"); }
+    void sub_assign(const Projective& o) { check(Abi::sub(&v, &o.v, &v, 1), "CurveProjective::sub_assign"); }
+    void mul_assign(const FrRepr& s) { check(Abi::mul_assign(&v, &s.v, &v, 1), "CurveProjective::mul_assign"); }
+    Affine into_affine() const {
+        Affine a;
+        check(Abi::to_affine(&v, &a.v, 1), "CurveProjective::into_affine");
+        return a;
+    }
+    bool operator==(const Projective& o) const {
+        if (is_zero() || o.is_zero()) return is_zero() && o.is_zero();
+        return into_affine() == o.into_affine();
+    }
+    bool operator!=(const Projective& o) const { return !(*this == o); }
+
+    static size_t recommended_wnaf_for_scalar(const FrRepr& s) { return (size_t)Abi::window_for_scalar(&s.v); }
+    static size_t recommended_wnaf_for_num_scalars(size_t n) { return (size_t)Abi::window_for_count(n); }
+
+    // CurveProjective::batch_normalization (ec.rs:246-294), in place
+    static void batch_normalization(std::vector<Projective>& v) {
+        check(Abi::normalize(v.empty() ? nullptr : &v[0].v, v.size()), "CurveProjective::batch_normalization");
+    }
+    // ---- batched forms: out[i] = op(a[i], b[i]) in one ABI call ----
+    static std::vector<Projective> double_batch(const std::vector<Projective>& a) {
+        std::vector<Projective> out(a.size());
+        if (!a.empty()) check(Abi::dbl(&a[0].v, &out[0].v, a.size()), "double_batch");
+        return out;
+    }
+    static std::vector<Projective> add_batch(const std::vector<Projective>& a, const std::vector<Projective>& b) {
+        same_size(a.size(), b.size());
+        std::vector<Projective> out(a.size());
+        if (!a.empty()) check(Abi::add(&a[0].v, &b[0].v, &out[0].v, a.size()), "add_batch");
+        return out;
+    }
+    static std::vector<Projective> add_mixed_batch(const std::vector<Projective>& a, const std::vector<Affine>& b) {
+        same_size(a.size(), b.size());
+        std::vector<Projective> out(a.size());
+        if (!a.empty()) check(Abi::add_mixed(&a[0].v, &b[0].v, &out[0].v, a.size()), "add_mixed_batch");
+        return out;
+    }
+    static std::vector<Affine> into_affine_batch(const std::vector<Projective>& a) {
+        std::vector<Affine> out(a.size());
+        if (!a.empty()) check(Abi::to_affine(&a[0].v, &out[0].v, a.size()), "into_affine_batch");
+        return out;
+    }
+    static std::vector<Projective> mul_assign_batch(const std::vector<Projective>& a, const std::vector<FrRepr>& s) {
+        same_size(a.size(), s.size());
+        std::vector<Projective> out(a.size());
+        if (!a.empty()) check(Abi::mul_assign(&a[0].v, &s[0].v, &out[0].v, a.size()), "mul_assign_batch");
+        return out;
+    }
+    // sum_i s_i * bases_i (the prover's multiexp; Pippenger on the device),
+    // equal as a point to the sum of CurveAffine::mul results
+    static Projective multiexp(const std::vector<Affine>& bases, const std::vector<FrRepr>& s) {
+        same_size(bases.size(), s.size());
+        Projective r;
+        check(Abi::multiexp(bases.empty() ? nullptr : &bases[0].v, s.empty() ? nullptr : &s[0].v, bases.size(), &r.v),
+              "multiexp");
+        return r;
+    }
+
+private:
+    static void same_size(size_t a, size_t b) {
+        if (a != b) throw Error(PA_ERR_INVALID_ARGUMENT, "batch operands differ in length");
+    }
+};
+
+#define PA_AFFINE_DEFS(A, PROJ, G)                                                                   \
+    inline PROJ A::into_projective() const {                                                         \
+        PROJ r;                                                                                      \
+        check(GroupAbi<G>::from_affine(&v, &r.v, 1), "CurveAffine::into_projective");                \
+        return r;                                                                                    \
+    }                                                                                                \
+    inline PROJ A::mul(const FrRepr& s) const {                                                      \
+        PROJ r;                                                                                      \
+        check(GroupAbi<G>::affine_mul(&v, &s.v, &r.v, 1), "CurveAffine::mul");                       \
+        return r;                                                                                    \
+    }                                                                                                \
+    inline std::vector<PROJ> A::mul_batch(const std::vector<A>& p, const std::vector<FrRepr>& s) {   \
+        if (p.size() != s.size()) throw Error(PA_ERR_INVALID_ARGUMENT, "mul_batch: length mismatch"); \
+        std::vector<PROJ> out(p.size());                                                             \
+        if (!p.empty()) check(GroupAbi<G>::affine_mul(&p[0].v, &s[0].v, &out[0].v, p.size()), "mul_batch"); \
+        return out;                                                                                  \
+    }
+PA_AFFINE_DEFS(G1Affine, G1, 1)
+PA_AFFINE_DEFS(G2Affine, G2, 2)
+#undef PA_AFFINE_DEFS
 
 using G1Uncompressed = Encoded<G1Affine, 1, false>;
 using G1Compressed = Encoded<G1Affine, 1, true>;
@@ -381,16 +609,6 @@ public:
         return out;
     }
 };
-
-inline G1Affine G1::into_affine() const {
-    if (is_zero()) return G1Affine::zero();
-    std::vector<G1> t{*this};
-    if (!(Fq{v.z} == Fq::one())) batch_normalization(t);   // z -> 1 on the GPU
-    G1Affine a;
-    a.v.x = t[0].v.x;
-    a.v.y = t[0].v.y;
-    return a;
-}
 
 inline G1Prepared G1Affine::prepare() const { return G1Prepared{*this}; }
 inline G2Prepared G2Affine::prepare() const { return G2Prepared::from_affine_batch({*this})[0]; }
@@ -446,26 +664,61 @@ struct Bls12 {
 inline Fq12 G1Affine::pairing_with(const G2Affine& other) const { return Bls12::pairing(*this, other); }
 inline Fq12 G2Affine::pairing_with(const G1Affine& other) const { return Bls12::pairing(other, *this); }
 
-// ---------------- Wnaf fixed-base path (wnaf.rs:73-179), G1 ----------------
-// Wnaf::new().base(g, num_scalars) then .scalar(s): the GPU uses a fixed-base
-// comb, so only the resulting points (not the wNAF digits) match the
-// reference -- equality is representation-independent (ec.rs:45-85).
+// ---------------- Wnaf (wnaf.rs:73-179), G1 and G2 ----------------
+// Wnaf::new_().base(g, num_scalars).scalar(s): fixed base (wnaf.rs:93-107,
+// 169-178); Wnaf::new_().scalar(s).base(g): fixed scalar (wnaf.rs:111-128,
+// 156-166); shared() hands a copy to another thread (wnaf.rs:131-154).  The
+// window is the reference's recommended_wnaf_* choice (window()), but the GPU
+// multiplies with a signed base-256 comb (fixed base) or the reference's
+// mul_assign (fixed scalar), so the resulting POINTS equal the reference's
+// (PartialEq, ec.rs:45-85) while Jacobian words may differ.  Any 256-bit
+// FrRepr is multiplied exactly; the reference's wnaf_form wraps (add_nocarry,
+// wnaf.rs:30-35) for raw reprs within 2^window of 2^256, values no
+// Fr::into_repr produces.
+template <class P>
+class WnafBase {
+public:
+    WnafBase(const P& g, size_t num_scalars) : base_(g), window_(P::recommended_wnaf_for_num_scalars(num_scalars)) {}
+    size_t window() const { return window_; }
+    WnafBase shared() const { return *this; }
+    std::vector<P> scalars(const std::vector<FrRepr>& s) const {
+        std::vector<P> out(s.size());
+        if (!s.empty()) check(P::Abi::fixed_base(&base_.v, &s[0].v, s.size(), &out[0].v), "Wnaf::scalar");
+        return out;
+    }
+    P scalar(const FrRepr& s) const { return scalars({s})[0]; }
+
+private:
+    P base_;
+    size_t window_;
+};
+
+class WnafScalar {
+public:
+    explicit WnafScalar(const FrRepr& s) : s_(s) {}
+    template <class P>
+    P base(const P& g) const {
+        P r = g;
+        r.mul_assign(s_);
+        return r;
+    }
+    template <class P>
+    std::vector<P> bases(const std::vector<P>& g) const {
+        return P::mul_assign_batch(g, std::vector<FrRepr>(g.size(), s_));
+    }
+    template <class P>
+    static size_t window_for(const FrRepr& s) { return P::recommended_wnaf_for_scalar(s); }
+
+private:
+    FrRepr s_;
+};
+
 class Wnaf {
 public:
     static Wnaf new_() { return Wnaf(); }
-    Wnaf& base(const G1& g, size_t /*num_scalars*/) {
-        base_ = g;
-        return *this;
-    }
-    std::vector<G1> scalars(const std::vector<FrRepr>& s) const {
-        std::vector<G1> out(s.size());
-        if (!s.empty()) check(pa_g1_wnaf_fixed_base(&base_.v, &s[0].v, s.size(), &out[0].v), "Wnaf::scalar");
-        return out;
-    }
-    G1 scalar(const FrRepr& s) const { return scalars({s})[0]; }
-
-private:
-    G1 base_ = G1::zero();
+    template <class P>
+    WnafBase<P> base(const P& g, size_t num_scalars) const { return WnafBase<P>(g, num_scalars); }
+    WnafScalar scalar(const FrRepr& s) const { return WnafScalar(s); }
 };
 
 }  // namespace pairing_amd

@@ -3,11 +3,13 @@
 //   bls12_381/tests/mod.rs:23-52     test_pairing_result_against_relic
 //   src/tests/engine.rs:50-126       random_miller_loop_tests, random_bilinearity_tests
 //   bls12_381/tests/mod.rs:98-560    invalid-encoding suites (a representative subset)
-//   src/tests/curve.rs:68-179, 357-387  wNAF / batch_normalization agreement
-// Inputs that need a scalar multiplication on G2 (which the product does not
-// expose) come from a data file written by tests/test_cpp_mirror.py with the
-// C oracle: n, RELIC Fq12, then n records each of a*G1, b*G2, (ab)*G1,
-// e(aP, bQ) and the scalars a.
+//   src/tests/curve.rs:5-388         curve_tests<G> for G1 and G2: zero edge
+//                                    cases, addition, doubling, negation,
+//                                    multiplication, transformations, wNAF
+//   src/tests/field.rs:4-21, 224-235 Frobenius = pow(q), inversion
+// Reference-computed inputs (a*G1, b*G2, (ab)*G1, e(aP, bQ), the scalars
+// a) come from a data file written by tests/test_cpp_mirror.py with the C
+// oracle: n, RELIC Fq12, then n records of each.
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
@@ -162,6 +164,209 @@ static void wnaf_batch_normalization_tests(const Data& d) {
     auto v = Wnaf::new_().base(G1Affine::one().into_projective(), d.n).scalars(d.a);
     G1::batch_normalization(v);
     for (size_t i = 0; i < d.n; i++) EXPECT(v[i].into_affine() == d.a_p[i]);
+    // CurveAffine::mul on both groups reproduces the reference-made points
+    for (size_t i = 0; i < d.n; i++) EXPECT(G1Affine::one().mul(d.a[i]).into_affine() == d.a_p[i]);
+    auto b = G1Affine::mul_batch(std::vector<G1Affine>(d.n, G1Affine::one()), d.a);
+    for (size_t i = 0; i < d.n; i++) EXPECT(b[i].into_affine() == d.a_p[i]);
+}
+
+// ---- curve_tests<G> (curve.rs:5-388) with a small deterministic RNG ----
+struct XorShift {
+    uint64_t s = 0x5dbe62598d313d76ULL;
+    uint64_t next() {
+        s ^= s << 13;
+        s ^= s >> 7;
+        s ^= s << 17;
+        return s;
+    }
+    FrRepr scalar() { return FrRepr(next(), next(), next(), next() & 0x0fffffffffffffffULL); }  // < 2^252 < r
+};
+// r - s for s < r (Fr::negate on the canonical value, fr.rs:369-375)
+static FrRepr neg_scalar(const FrRepr& s) {
+    static const uint64_t r[4] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL,
+                                  0x73eda753299d7d48ULL};
+    FrRepr o;
+    unsigned __int128 borrow = 0;
+    for (int i = 0; i < 4; i++) {
+        const unsigned __int128 d = (unsigned __int128)r[i] - s.v.l[i] - borrow;
+        o.v.l[i] = (uint64_t)d;
+        borrow = (d >> 64) ? 1 : 0;
+    }
+    return o;
+}
+
+template <class P>
+static P rand_point(XorShift& rng) {
+    return P::Affine::one().mul(rng.scalar());
+}
+
+template <class P>
+static void curve_tests(int iters) {
+    XorShift rng;
+    using A = typename P::Affine;
+    {   // zero edge cases (curve.rs:8-44)
+        P z = P::zero();
+        z.negate();
+        EXPECT(z.is_zero());
+        z.double_();
+        EXPECT(z.is_zero());
+        P r = rand_point<P>(rng), rc = r;
+        r.add_assign(P::zero());
+        EXPECT(r == rc);
+        r.add_assign_mixed(A::zero());
+        EXPECT(r == rc);
+        P z2 = P::zero();
+        z2.add_assign(r);
+        z.add_assign_mixed(r.into_affine());
+        EXPECT(z == z2);
+        EXPECT(z == r);
+    }
+    for (int it = 0; it < iters; it++) {
+        P a = rand_point<P>(rng), b = rand_point<P>(rng), c = rand_point<P>(rng);
+        // addition (curve.rs:269-345): a + a == 2a (full and mixed), associativity
+        P aa = a, am = a, ad = a;
+        aa.add_assign(a);
+        am.add_assign_mixed(a.into_affine());
+        ad.double_();
+        EXPECT(aa == ad);
+        EXPECT(aa == am);
+        P t0 = a, t1 = c, t2 = b;
+        t0.add_assign(b);
+        t0.add_assign(c);
+        t1.add_assign(b);
+        t1.add_assign_mixed(a.into_affine());
+        t2.add_assign_mixed(c.into_affine());
+        t2.add_assign(a);
+        EXPECT(t0 == t1);
+        EXPECT(t0 == t2);
+        // doubling (curve.rs:210-235): 2(a + b) == 2a + 2b
+        P s1 = a;
+        s1.add_assign(b);
+        s1.double_();
+        P a2 = a, b2 = b;
+        a2.double_();
+        b2.double_();
+        P s2 = a2, s3 = a2;
+        s2.add_assign(b2);
+        s3.add_assign_mixed(b2.into_affine());
+        EXPECT(s1 == s2);
+        EXPECT(s1 == s3);
+        // negation (curve.rs:181-208): s r + (-s) r == 0
+        const FrRepr s = rng.scalar(), sn = neg_scalar(s);
+        P n1 = a, n2 = a;
+        n1.mul_assign(s);
+        n2.mul_assign(sn);
+        P n3 = n1, n4 = n1;
+        n3.add_assign(n2);
+        EXPECT(n3.is_zero());
+        n4.add_assign_mixed(n2.into_affine());
+        EXPECT(n4.is_zero());
+        n1.negate();
+        EXPECT(n1 == n2);
+        P d = a;
+        d.sub_assign(a);
+        EXPECT(d.is_zero());
+        // multiplication (curve.rs:237-267): s(a + b) == sa + sb == a.mul(s) + b.mul(s)
+        P m1 = a;
+        m1.add_assign(b);
+        m1.mul_assign(s);
+        P sa = a, sb = b;
+        sa.mul_assign(s);
+        sb.mul_assign(s);
+        P m2 = sa;
+        m2.add_assign(sb);
+        P m3 = a.into_affine().mul(s);
+        m3.add_assign(b.into_affine().mul(s));
+        EXPECT(m1 == m2);
+        EXPECT(m1 == m3);
+        // transformations (curve.rs:45-56, 347-388)
+        EXPECT(a == a.into_affine().into_projective());
+        EXPECT(a.into_affine().into_projective().into_affine() == a.into_affine());
+    }
+    {   // batch_normalization == into_affine (curve.rs:357-387), zero kept
+        std::vector<P> v;
+        for (int k = 0; k < 20; k++) {
+            P p = rand_point<P>(rng);
+            p.double_();
+            v.push_back(p);
+        }
+        v[3] = P::zero();
+        auto expect = P::into_affine_batch(v);
+        P::batch_normalization(v);
+        for (size_t k = 0; k < v.size(); k++) {
+            EXPECT(v[k].is_normalized());
+            EXPECT(v[k].into_affine() == expect[k]);
+        }
+    }
+    {   // wNAF (curve.rs:68-179): fixed base and fixed scalar == mul_assign
+        const P g = rand_point<P>(rng);
+        std::vector<FrRepr> sc;
+        for (int k = 0; k < 32; k++) sc.push_back(rng.scalar());
+        auto wb = Wnaf::new_().base(g, sc.size());
+        EXPECT(wb.window() == P::recommended_wnaf_for_num_scalars(sc.size()));
+        auto shared = wb.shared();
+        auto fixed = shared.scalars(sc);
+        for (size_t k = 0; k < sc.size(); k++) {
+            P e = g;
+            e.mul_assign(sc[k]);
+            EXPECT(fixed[k] == e);
+            EXPECT(Wnaf::new_().scalar(sc[k]).base(g) == e);
+        }
+        EXPECT(P::recommended_wnaf_for_num_scalars(1 << 18) >= 15);
+    }
+}
+
+// field.rs:4-21 (Frobenius == pow(q)), 224-235 (inversion)
+static void field_tests(const Data& d) {
+    const std::vector<uint64_t> q = {0xb9feffffffffaaabULL, 0x1eabfffeb153ffffULL, 0x6730d2a0f6b0f624ULL,
+                                     0x64774b84f38512bfULL, 0x4b1ba7b6434bacd7ULL, 0x1a0111ea397fe69aULL};
+    Fq2 a2 = Fq2::one();
+    a2.v.c1 = d.e_ab[0].v.c0.c1.c0;   // a nonzero Fq2 with both coordinates set
+    a2.v.c0 = d.e_ab[0].v.c1.c2.c1;
+    Fq6 a6{d.e_ab[0].v.c1};
+    Fq12 a12 = d.e_ab[1];
+    Fq2 p2 = a2;
+    Fq6 p6 = a6;
+    Fq12 p12 = a12;
+    for (size_t i = 0; i < 3; i++) {
+        Fq2 f2 = a2;
+        f2.frobenius_map(i);
+        EXPECT(f2 == p2);
+        Fq6 f6 = a6;
+        f6.frobenius_map(i);
+        EXPECT(f6 == p6);
+        Fq12 f12 = a12;
+        f12.frobenius_map(i);
+        EXPECT(f12 == p12);
+        p2 = p2.pow(q);
+        p6 = p6.pow(q);
+        p12 = p12.pow(q);
+    }
+    Fq2 i2 = a2.inverse().value();
+    i2.mul_assign(a2);
+    EXPECT(i2 == Fq2::one());
+    Fq6 i6 = a6.inverse().value();
+    i6.mul_assign(a6);
+    EXPECT(i6 == Fq6::one());
+    EXPECT(!Fq6::zero().inverse().has_value());
+    Fq6 s6 = a6, m6 = a6;
+    s6.square();
+    m6.mul_assign(a6);
+    EXPECT(s6 == m6);
+    Fq6 dd = a6, ad = a6;
+    dd.double_();
+    ad.add_assign(a6);
+    EXPECT(dd == ad);
+    ad.sub_assign(a6);
+    EXPECT(ad == a6);
+    // e(aP, bQ)^r == 1: pairing values have order r
+    const std::vector<uint64_t> r = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL,
+                                     0x73eda753299d7d48ULL};
+    EXPECT(d.e_ab[0].pow(r) == Fq12::one());
+    // conjugate = inverse on the cyclotomic subgroup
+    Fq12 c = d.e_ab[0];
+    c.conjugate();
+    EXPECT(c == d.e_ab[0].inverse().value());
 }
 
 // SqrtField (fq.rs:1147-1170)
@@ -192,6 +397,9 @@ int main(int argc, char** argv) {
             {"encoding_tests", [&] { encoding_tests(d); }},
             {"wnaf_batch_normalization_tests", [&] { wnaf_batch_normalization_tests(d); }},
             {"sqrt_tests", [&] { sqrt_tests(); }},
+            {"curve_tests<G1>", [&] { curve_tests<G1>(6); }},
+            {"curve_tests<G2>", [&] { curve_tests<G2>(4); }},
+            {"field_tests", [&] { field_tests(d); }},
         };
         for (const auto& t : tests) {
             const int before = g_failures;

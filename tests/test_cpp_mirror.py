@@ -1,8 +1,8 @@
 """The C++ mirror of the reference trait surface (include/pairing_amd.hpp):
 CPU -- it compiles with g++ against the C ABI and links libpairing_amd.so;
-GPU -- tests/cpp/test_engine.cpp (the reference's engine / encoding / wNAF
-tests written against the mirror) passes on the device, with inputs that need
-G2 scalar multiplication supplied by the C oracle."""
+GPU -- tests/cpp/test_engine.cpp (the reference's engine / encoding / curve /
+field / wNAF tests written against the mirror) passes on the device, with
+reference-computed inputs supplied by the C oracle."""
 import os
 import subprocess
 
@@ -57,4 +57,4 @@ def test_cpp_engine_suite_on_gpu(oracle, tmp_path):
     r = subprocess.run([exe, data], capture_output=True, text=True, timeout=600)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count("ok  ") == 6
+    assert r.stdout.count("ok  ") == 9
