@@ -4,10 +4,14 @@
 // kernels_field.hip / kernels_pairing.hip.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
+#include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "../../include/pairing_amd.h"
@@ -53,25 +57,159 @@ int hip_code(hipError_t e) {
         if (_e != hipSuccess) return fail(hip_code(_e), what, _e);  \
     } while (0)
 
-// RAII device buffer for the synchronous host-pointer entry points.
+// ---- per-thread device context of the host-pointer entry points ----
+// Every host-pointer call runs on its calling thread's own context for the
+// current device: a non-blocking compute stream, a copy stream for the
+// pipelined pairing path, grow-only device scratch slots and grow-only pinned
+// staging buffers.  So a call never hipMallocs in steady state, waits only
+// for its own stream (no device-wide synchronize), and calls from different
+// host threads run concurrently (the reference traits are Send + Sync,
+// lib.rs:120-121).  A thread's contexts go back to a process-wide pool when
+// the thread exits (no HIP call at that point) and are reused by new threads.
+struct HostCtx {
+    int dev = -1;
+    hipStream_t compute = nullptr, copy = nullptr, copy_out = nullptr;
+    std::vector<std::pair<void*, size_t>> slots;     // device scratch, used as a stack by DevBuf
+    size_t depth = 0;
+    std::pair<void*, size_t> pinned[4] = {};          // pinned host staging (pipelined pairing)
+    std::pair<void*, size_t> pipe[8] = {};            // device buffers of the pipelined pairing
+    hipEvent_t ev[16] = {};
+    size_t full_batch = 0;                            // pairings that fill the device once (one wave per SIMD)
+};
+
+struct CtxPool {
+    std::mutex mu;
+    std::vector<HostCtx*> free_ctx;
+};
+CtxPool& ctx_pool() {
+    static CtxPool* p = new CtxPool;   // never destroyed: thread exits may return contexts late
+    return *p;
+}
+
+struct ThreadCtxs {
+    HostCtx* by_dev[64] = {};
+    ~ThreadCtxs() {
+        CtxPool& pool = ctx_pool();
+        std::lock_guard<std::mutex> g(pool.mu);
+        for (HostCtx* c : by_dev)
+            if (c) {
+                c->depth = 0;
+                pool.free_ctx.push_back(c);
+            }
+    }
+};
+thread_local ThreadCtxs t_ctxs;
+
+hipError_t thread_ctx(HostCtx** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (HostCtx* c = t_ctxs.by_dev[dev]) {
+        *out = c;
+        return hipSuccess;
+    }
+    {
+        CtxPool& pool = ctx_pool();
+        std::lock_guard<std::mutex> g(pool.mu);
+        for (size_t k = 0; k < pool.free_ctx.size(); k++)
+            if (pool.free_ctx[k]->dev == dev) {
+                *out = t_ctxs.by_dev[dev] = pool.free_ctx[k];
+                pool.free_ctx.erase(pool.free_ctx.begin() + k);
+                return hipSuccess;
+            }
+    }
+    HostCtx* c = new HostCtx;
+    c->dev = dev;
+    if ((e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking)) != hipSuccess) {
+        delete c;   // (a stream created before the failure is leaked: rare, bounded)
+        return e;
+    }
+    for (auto& ev : c->ev)
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    *out = t_ctxs.by_dev[dev] = c;
+    return hipSuccess;
+}
+
+// grow-only buffer: reuse `b` if large enough (its last use has completed --
+// every call synchronizes its streams before returning)
+hipError_t grow(std::pair<void*, size_t>& b, size_t bytes, bool pinned) {
+    if (b.second >= bytes && b.first) return hipSuccess;
+    hipError_t e;
+    if (b.first && (e = pinned ? hipHostFree(b.first) : hipFree(b.first)) != hipSuccess) return e;
+    b = {nullptr, 0};
+    bytes = bytes < 4096 ? 4096 : bytes + bytes / 8;   // headroom: fewer regrowths for slowly rising sizes
+    if ((e = pinned ? hipHostMalloc(&b.first, bytes, hipHostMallocDefault) : hipMalloc(&b.first, bytes)) !=
+        hipSuccess) {
+        b.first = nullptr;
+        return e;
+    }
+    b.second = bytes;
+    return hipSuccess;
+}
+
+// One stream per device for the pipelined pairing kernels of every host
+// thread: two batches' kernels running at once on one GPU share its SIMDs
+// worse than back to back (each wave holds a whole SIMD), so the kernels of
+// concurrent callers queue on this stream while their copies overlap them.
+hipError_t pairing_stream(int dev, hipStream_t* out) {
+    static std::mutex mu;
+    static hipStream_t streams[64] = {};
+    std::lock_guard<std::mutex> g(mu);
+    if (!streams[dev]) {
+        hipError_t e = hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking);
+        if (e != hipSuccess) return e;
+    }
+    *out = streams[dev];
+    return hipSuccess;
+}
+
+// The calling thread's compute stream on the current device (host entries).
+hipStream_t call_stream() {
+    HostCtx* c = nullptr;
+    return thread_ctx(&c) == hipSuccess ? c->compute : nullptr;
+}
+hipError_t call_sync() {
+    HostCtx* c = nullptr;
+    hipError_t e = thread_ctx(&c);
+    return e != hipSuccess ? e : hipStreamSynchronize(c->compute);
+}
+
+// A device scratch buffer for a host-pointer entry point: the next slot of
+// the thread's context, released (not freed) when it goes out of scope.
 struct DevBuf {
     void* p = nullptr;
-    hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 1); }
+    HostCtx* ctx = nullptr;
+    hipError_t alloc(size_t bytes) {
+        hipError_t e = thread_ctx(&ctx);
+        if (e != hipSuccess) return e;
+        if (ctx->slots.size() <= ctx->depth) ctx->slots.resize(ctx->depth + 1, {nullptr, 0});
+        if ((e = grow(ctx->slots[ctx->depth], bytes ? bytes : 1, false)) != hipSuccess) {
+            ctx = nullptr;
+            return e;
+        }
+        p = ctx->slots[ctx->depth++].first;
+        return hipSuccess;
+    }
     ~DevBuf() {
-        if (p) (void)hipFree(p);
+        if (ctx) ctx->depth--;
     }
     template <class T>
     T* as() const { return static_cast<T*>(p); }
 };
 
-// Copy `count` host inputs of `bytes_each` into fresh device buffers.
 int upload(DevBuf& d, const void* host, size_t bytes) {
-    PA_TRY(d.alloc(bytes), "hipMalloc");
-    if (bytes) PA_TRY(hipMemcpy(d.p, host, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
+    PA_TRY(d.alloc(bytes), "device scratch");
+    if (bytes) PA_TRY(hipMemcpyAsync(d.p, host, bytes, hipMemcpyHostToDevice, d.ctx->compute), "H2D copy");
     return PA_OK;
 }
 int download(void* host, const DevBuf& d, size_t bytes) {
-    if (bytes) PA_TRY(hipMemcpy(host, d.p, bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+    if (bytes) {
+        PA_TRY(hipMemcpyAsync(host, d.p, bytes, hipMemcpyDeviceToHost, d.ctx->compute), "D2H copy");
+        PA_TRY(hipStreamSynchronize(d.ctx->compute), "D2H copy");
+    }
     return PA_OK;
 }
 
@@ -89,12 +227,12 @@ int host_field_op(int op, const void* a, const void* b, void* out, uint8_t* ok, 
     int rc;
     if ((rc = upload(da, a, in_bytes * n))) return rc;
     if (b && (rc = upload(db, b, in_bytes * n))) return rc;
-    PA_TRY(dout.alloc(out_bytes * n), "hipMalloc");
-    if (ok) PA_TRY(dok.alloc(n), "hipMalloc");
+    PA_TRY(dout.alloc(out_bytes * n), "device scratch");
+    if (ok) PA_TRY(dok.alloc(n), "device scratch");
     PA_TRY(pa::launch_field_op(op, da.as<uint64_t>(), db.as<uint64_t>(), dout.as<uint64_t>(), dok.as<uint8_t>(), n,
-                               param, nullptr),
+                               param, call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     if ((rc = download(out, dout, out_bytes * n))) return rc;
     if (ok && (rc = download(ok, dok, n))) return rc;
     return PA_OK;
@@ -194,11 +332,11 @@ int host_field_pow(int op, const void* a, const uint64_t* exp, size_t exp_words,
     DevBuf da, de, dout;
     int rc;
     if ((rc = upload(da, a, bytes * n)) || (rc = upload(de, exp, 8 * exp_words))) return rc;
-    PA_TRY(dout.alloc(bytes * n), "hipMalloc");
+    PA_TRY(dout.alloc(bytes * n), "device scratch");
     PA_TRY(pa::launch_field_op(op, da.as<uint64_t>(), de.as<uint64_t>(), dout.as<uint64_t>(), nullptr, n,
-                               (int)exp_words, nullptr),
+                               (int)exp_words, call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, bytes * n);
 }
 }  // namespace
@@ -222,11 +360,11 @@ int pa_fq12_mul_by_014_batch(const pa_fq12* a, const pa_fq2* c0, const pa_fq2* c
     if ((rc = upload(da, a, 576 * n)) || (rc = upload(d0, c0, 96 * n)) || (rc = upload(d1, c1, 96 * n)) ||
         (rc = upload(d4, c4, 96 * n)))
         return rc;
-    PA_TRY(dout.alloc(576 * n), "hipMalloc");
+    PA_TRY(dout.alloc(576 * n), "device scratch");
     PA_TRY(pa::launch_fq12_mul_by_014(da.as<uint64_t>(), d0.as<uint64_t>(), d1.as<uint64_t>(), d4.as<uint64_t>(),
-                                      dout.as<uint64_t>(), n, nullptr),
+                                      dout.as<uint64_t>(), n, call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, 576 * n);
 }
 
@@ -236,9 +374,9 @@ int pa_g2_prepare_batch(const pa_g2_affine* q, pa_g2_prepared* out, size_t n) {
     DevBuf dq, dout;
     int rc;
     if ((rc = upload(dq, q, sizeof(pa_g2_affine) * n))) return rc;
-    PA_TRY(dout.alloc(sizeof(pa_g2_prepared) * n), "hipMalloc");
-    PA_TRY(pa::launch_g2_prepare(dq.as<uint64_t>(), dout.as<uint64_t>(), n, nullptr), "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(dout.alloc(sizeof(pa_g2_prepared) * n), "device scratch");
+    PA_TRY(pa::launch_g2_prepare(dq.as<uint64_t>(), dout.as<uint64_t>(), n, call_stream()), "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, sizeof(pa_g2_prepared) * n);
 }
 
@@ -249,10 +387,10 @@ int pa_miller_loop_batch(const pa_g1_affine* p, const pa_g2_prepared* q, pa_fq12
     int rc;
     if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_prepared) * n)))
         return rc;
-    PA_TRY(dout.alloc(576 * n), "hipMalloc");
-    PA_TRY(pa::launch_miller_loop_prepared(dp.as<uint64_t>(), dq.as<uint64_t>(), dout.as<uint64_t>(), n, nullptr),
+    PA_TRY(dout.alloc(576 * n), "device scratch");
+    PA_TRY(pa::launch_miller_loop_prepared(dp.as<uint64_t>(), dq.as<uint64_t>(), dout.as<uint64_t>(), n, call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, 576 * n);
 }
 
@@ -271,12 +409,12 @@ int pa_multi_miller_loop(const pa_g1_affine* p, const pa_g2_prepared* q, size_t 
     int rc;
     if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_prepared) * n)))
         return rc;
-    PA_TRY(dwork.alloc(576 * n), "hipMalloc");
-    PA_TRY(dout.alloc(576), "hipMalloc");
-    PA_TRY(pa::launch_miller_loop_prepared(dp.as<uint64_t>(), dq.as<uint64_t>(), dwork.as<uint64_t>(), n, nullptr),
+    PA_TRY(dwork.alloc(576 * n), "device scratch");
+    PA_TRY(dout.alloc(576), "device scratch");
+    PA_TRY(pa::launch_miller_loop_prepared(dp.as<uint64_t>(), dq.as<uint64_t>(), dwork.as<uint64_t>(), n, call_stream()),
            "kernel launch");
-    PA_TRY(pa::launch_fq12_product(dwork.as<uint64_t>(), n, dout.as<uint64_t>(), nullptr), "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(pa::launch_fq12_product(dwork.as<uint64_t>(), n, dout.as<uint64_t>(), call_stream()), "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, 576);
 }
 
@@ -286,30 +424,165 @@ int pa_final_exponentiation_batch(const pa_fq12* in, pa_fq12* out, uint8_t* ok, 
     DevBuf din, dout, dok;
     int rc;
     if ((rc = upload(din, in, 576 * n))) return rc;
-    PA_TRY(dout.alloc(576 * n), "hipMalloc");
-    PA_TRY(dok.alloc(n), "hipMalloc");
-    PA_TRY(fe_launch(din.as<uint64_t>(), dout.as<uint64_t>(), dok.as<uint8_t>(), n, nullptr),
+    PA_TRY(dout.alloc(576 * n), "device scratch");
+    PA_TRY(dok.alloc(n), "device scratch");
+    PA_TRY(fe_launch(din.as<uint64_t>(), dout.as<uint64_t>(), dok.as<uint8_t>(), n, call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     if ((rc = download(out, dout, 576 * n))) return rc;
     return download(ok, dok, n);
 }
 
+}  // extern "C"
+
+namespace {
+
+// Host copy into / out of pinned staging, split over up to 8 threads for
+// large buffers (a single thread's memcpy would be slower than the DMA it
+// feeds).
+void pcopy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPiece = 2u << 20;
+    unsigned t = std::thread::hardware_concurrency();
+    t = t < 1 ? 1 : (t > 8 ? 8 : t);
+    if (bytes / kPiece < t) t = (unsigned)(bytes / kPiece);
+    if (t <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t per = (bytes + t - 1) / t;
+    std::vector<std::thread> th;
+    for (unsigned k = 1; k < t; k++) {
+        const size_t lo = per * k, len = lo >= bytes ? 0 : (bytes - lo < per ? bytes - lo : per);
+        if (len) th.emplace_back([=] { memcpy((char*)dst + lo, (const char*)src + lo, len); });
+    }
+    memcpy(dst, src, per < bytes ? per : bytes);
+    for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Engine::pairing over host buffers, pipelined: the batch is cut into chunks
+// of one device-filling wave count (one pairing per lane, one wave per SIMD:
+// multiProcessorCount x 4 x 64 = 65 536 on MI355X); chunk k's inputs are
+// staged into pinned memory and copied on the copy stream while chunk k-1
+// computes on the compute stream, and chunk k-1's results travel back while
+// chunk k computes.  Two pinned / device buffer sets alternate.
 int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n) {
     if (n == 0) return PA_OK;
     if (!p || !q || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
-    DevBuf dp, dq, dml, dout;
-    int rc;
-    if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_affine) * n)))
-        return rc;
-    PA_TRY(dml.alloc(576 * n), "hipMalloc");
-    PA_TRY(dout.alloc(576 * n), "hipMalloc");
-    PA_TRY(ml_launch(dp.as<uint64_t>(), dq.as<uint64_t>(), dml.as<uint64_t>(), n, nullptr), "kernel launch");
-    // Engine::pairing unwraps: a Miller-loop value is never zero, ok is not reported
-    PA_TRY(fe_launch(dml.as<uint64_t>(), dout.as<uint64_t>(), nullptr, n, nullptr),
-           "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
-    return download(out, dout, 576 * n);
+    HostCtx* c = nullptr;
+    PA_TRY(thread_ctx(&c), "device context");
+    hipStream_t ks = nullptr;   // kernels: the device's shared pairing stream
+    PA_TRY(pairing_stream(c->dev, &ks), "pairing stream");
+    if (!c->full_batch) {
+        int cus = 0;
+        PA_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev), "device attribute");
+        c->full_batch = (size_t)(cus > 0 ? cus : 1) * 4 * 64;
+    }
+    size_t chunk = c->full_batch;
+    if (const char* e = getenv("PA_PIPELINE_CHUNK")) {   // tests: exercise the pipeline at small n
+        const long v = strtol(e, nullptr, 10);
+        if (v > 0) chunk = (size_t)v;
+    }
+    const size_t nchunks = (n + chunk - 1) / chunk;
+    const size_t cap = n < chunk ? n : chunk;
+    constexpr size_t P1 = sizeof(pa_g1_affine), P2 = sizeof(pa_g2_affine), F12 = sizeof(pa_fq12);
+    const int bufs = nchunks > 1 ? 2 : 1;
+    for (int k = 0; k < bufs; k++) {
+        PA_TRY(grow(c->pinned[2 * k], cap * (P1 + P2), true), "pinned staging");
+        PA_TRY(grow(c->pinned[2 * k + 1], cap * F12, true), "pinned staging");
+        PA_TRY(grow(c->pipe[4 * k], cap * (P1 + P2), false), "device scratch");   // p | q
+        PA_TRY(grow(c->pipe[4 * k + 1], cap * F12, false), "device scratch");     // Miller values
+        PA_TRY(grow(c->pipe[4 * k + 2], cap * F12, false), "device scratch");     // e(p, q)
+    }
+    // PA_PIPELINE_TRACE=1: per-phase host timestamps on stderr (measurement only)
+    static const bool trace = getenv("PA_PIPELINE_TRACE") && getenv("PA_PIPELINE_TRACE")[0] == '1';
+    const auto t0 = std::chrono::steady_clock::now();
+    auto stamp = [&](const char* what, size_t ci) {
+        if (trace)
+            fprintf(stderr, "[pipeline] chunk %zu %-10s %8.3f ms\n", ci, what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
+    // Within a chunk the staging copies and the DMA may run in kPieces pieces
+    // (PA_PIPELINE_PIECES, 1..4), so the host copy of piece j overlaps the DMA
+    // of piece j - 1 (in) / j + 1 (out).
+    static const size_t kPieces = [] {
+        const char* e = getenv("PA_PIPELINE_PIECES");
+        const long v = e ? strtol(e, nullptr, 10) : 1;
+        return (size_t)(v < 1 ? 1 : (v > 4 ? 4 : v));
+    }();
+    hipEvent_t* h2d = c->ev;        // [k]: chunk's inputs copied (pinned in[k] free again)
+    hipEvent_t* done = c->ev + 2;   // [k]: chunk's kernels finished (device in[k], ml[k] free)
+    hipEvent_t* d2h = c->ev + 4;    // [k * kPieces + j]: piece j of the chunk's results in pinned out[k]
+    auto piece = [&](size_t cnt, size_t j, size_t* lo) {
+        const size_t per = (cnt + kPieces - 1) / kPieces;
+        *lo = per * j < cnt ? per * j : cnt;
+        return (per * (j + 1) < cnt ? per * (j + 1) : cnt) - *lo;
+    };
+    auto drain = [&](size_t ci) -> int {
+        const int k = (int)(ci & 1);
+        const size_t lo = ci * chunk, cnt = n - lo < chunk ? n - lo : chunk;
+        for (size_t j = 0; j < kPieces; j++) {
+            size_t a;
+            const size_t m = piece(cnt, j, &a);
+            if (!m) continue;
+            PA_TRY(hipEventSynchronize(d2h[k * kPieces + j]), "D2H copy");
+            pcopy(out + lo + a, (pa_fq12*)c->pinned[2 * k + 1].first + a, m * F12);
+        }
+        stamp("copied out", ci);
+        return PA_OK;
+    };
+    for (size_t ci = 0; ci < nchunks; ci++) {
+        const int k = (int)(ci & 1);
+        const size_t lo = ci * chunk, cnt = n - lo < chunk ? n - lo : chunk;
+        char* pin_p = (char*)c->pinned[2 * k].first;
+        char* pin_q = pin_p + cnt * P1;
+        char* dev_p = (char*)c->pipe[4 * k].first;
+        char* dev_q = dev_p + cnt * P1;
+        uint64_t* dev_ml = (uint64_t*)c->pipe[4 * k + 1].first;
+        uint64_t* dev_out = (uint64_t*)c->pipe[4 * k + 2].first;
+        if (ci >= 2) {
+            PA_TRY(hipEventSynchronize(h2d[k]), "H2D copy");
+            PA_TRY(hipStreamWaitEvent(c->copy, done[k], 0), "stream wait");
+        }
+        for (size_t j = 0; j < kPieces; j++) {
+            size_t a;
+            const size_t m = piece(cnt, j, &a);
+            if (!m) continue;
+            pcopy(pin_p + a * P1, p + lo + a, m * P1);
+            pcopy(pin_q + a * P2, q + lo + a, m * P2);
+            PA_TRY(hipMemcpyAsync(dev_p + a * P1, pin_p + a * P1, m * P1, hipMemcpyHostToDevice, c->copy), "H2D copy");
+            PA_TRY(hipMemcpyAsync(dev_q + a * P2, pin_q + a * P2, m * P2, hipMemcpyHostToDevice, c->copy), "H2D copy");
+        }
+        PA_TRY(hipEventRecord(h2d[k], c->copy), "event");
+        stamp("staged in", ci);
+        PA_TRY(hipStreamWaitEvent(ks, h2d[k], 0), "stream wait");
+        if (ci >= 2) PA_TRY(hipStreamWaitEvent(ks, d2h[k * kPieces + kPieces - 1], 0), "stream wait");
+        PA_TRY(ml_launch((const uint64_t*)dev_p, (const uint64_t*)dev_q, dev_ml, cnt, ks), "kernel launch");
+        // Engine::pairing unwraps: a Miller-loop value is never zero, ok is not reported
+        PA_TRY(fe_launch(dev_ml, dev_out, nullptr, cnt, ks), "kernel launch");
+        PA_TRY(hipEventRecord(done[k], ks), "event");
+        PA_TRY(hipStreamWaitEvent(c->copy_out, done[k], 0), "stream wait");
+        for (size_t j = 0; j < kPieces; j++) {
+            size_t a;
+            const size_t m = piece(cnt, j, &a);
+            if (!m) continue;
+            PA_TRY(hipMemcpyAsync((pa_fq12*)c->pinned[2 * k + 1].first + a, (const pa_fq12*)dev_out + a, m * F12,
+                                  hipMemcpyDeviceToHost, c->copy_out),
+                   "D2H copy");
+            PA_TRY(hipEventRecord(d2h[k * kPieces + j], c->copy_out), "event");
+        }
+        stamp("enqueued", ci);
+        if (ci >= 1) {
+            const int rc = drain(ci - 1);
+            if (rc) return rc;
+        }
+    }
+    const int rc = drain(nchunks - 1);
+    if (rc) return rc;
+    return PA_OK;   // the last chunk's D2H event has completed: so has everything before it
 }
 
 int pa_pairing_batch_multi_gpu(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n, int ndev) {
@@ -354,12 +627,12 @@ int pa_multi_miller_loop_affine(const pa_g1_affine* p, const pa_g2_affine* q, si
     int rc;
     if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_affine) * n)))
         return rc;
-    PA_TRY(dwork.alloc(576 * n), "hipMalloc");
-    PA_TRY(dout.alloc(576), "hipMalloc");
+    PA_TRY(dwork.alloc(576 * n), "device scratch");
+    PA_TRY(dout.alloc(576), "device scratch");
     // per-pair loops (infinity pairs give one, as mod.rs:50-54 skips them), then the product tree
-    PA_TRY(ml_launch(dp.as<uint64_t>(), dq.as<uint64_t>(), dwork.as<uint64_t>(), n, nullptr), "kernel launch");
-    PA_TRY(pa::launch_fq12_product(dwork.as<uint64_t>(), n, dout.as<uint64_t>(), nullptr), "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(ml_launch(dp.as<uint64_t>(), dq.as<uint64_t>(), dwork.as<uint64_t>(), n, call_stream()), "kernel launch");
+    PA_TRY(pa::launch_fq12_product(dwork.as<uint64_t>(), n, dout.as<uint64_t>(), call_stream()), "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, 576);
 }
 
@@ -381,12 +654,12 @@ int host_decode(int group, const uint8_t* enc, size_t n, int compressed, int che
     DevBuf de, dout, dst;
     int rc;
     if ((rc = upload(de, enc, enc_size(group, compressed) * n))) return rc;
-    PA_TRY(dout.alloc(rec * n), "hipMalloc");
-    PA_TRY(dst.alloc(n), "hipMalloc");
+    PA_TRY(dout.alloc(rec * n), "device scratch");
+    PA_TRY(dst.alloc(n), "device scratch");
     PA_TRY(pa::launch_decode(group, compressed, checked, de.as<uint8_t>(), n, dout.as<uint64_t>(),
-                             dst.as<uint8_t>(), nullptr),
+                             dst.as<uint8_t>(), call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     if ((rc = download(out, dout, rec * n))) return rc;
     return download(status, dst, n);
 }
@@ -397,9 +670,9 @@ int host_encode(int group, const void* in, size_t n, int compressed, uint8_t* en
     DevBuf din, de;
     int rc;
     if ((rc = upload(din, in, rec * n))) return rc;
-    PA_TRY(de.alloc(enc_size(group, compressed) * n), "hipMalloc");
-    PA_TRY(pa::launch_encode(group, compressed, din.as<uint64_t>(), n, de.as<uint8_t>(), nullptr), "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(de.alloc(enc_size(group, compressed) * n), "device scratch");
+    PA_TRY(pa::launch_encode(group, compressed, din.as<uint64_t>(), n, de.as<uint8_t>(), call_stream()), "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
     return download(enc, de, enc_size(group, compressed) * n);
 }
 int host_sqrt(int degree, const void* a, void* out, uint8_t* ok, size_t n) {
@@ -409,11 +682,11 @@ int host_sqrt(int degree, const void* a, void* out, uint8_t* ok, size_t n) {
     DevBuf da, dout, dok;
     int rc;
     if ((rc = upload(da, a, bytes))) return rc;
-    PA_TRY(dout.alloc(bytes), "hipMalloc");
-    PA_TRY(dok.alloc(n), "hipMalloc");
-    PA_TRY(pa::launch_sqrt(degree, da.as<uint64_t>(), n, dout.as<uint64_t>(), dok.as<uint8_t>(), nullptr),
+    PA_TRY(dout.alloc(bytes), "device scratch");
+    PA_TRY(dok.alloc(n), "device scratch");
+    PA_TRY(pa::launch_sqrt(degree, da.as<uint64_t>(), n, dout.as<uint64_t>(), dok.as<uint8_t>(), call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     if ((rc = download(out, dout, bytes))) return rc;
     return download(ok, dok, n);
 }
@@ -442,8 +715,8 @@ int pa_g1_batch_normalization(pa_g1* v, size_t n) {
     DevBuf dv;
     int rc;
     if ((rc = upload(dv, v, sizeof(pa_g1) * n))) return rc;
-    PA_TRY(pa::launch_g1_batch_normalize(dv.as<uint64_t>(), n, nullptr), "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(pa::launch_g1_batch_normalize(dv.as<uint64_t>(), n, call_stream()), "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
     return download(v, dv, sizeof(pa_g1) * n);
 }
 
@@ -453,13 +726,13 @@ int pa_g1_wnaf_fixed_base(const pa_g1* base, const pa_fr_repr* scalars, size_t n
     DevBuf db, ds, dt, dw, dout;
     int rc;
     if ((rc = upload(db, base, sizeof(pa_g1))) || (rc = upload(ds, scalars, sizeof(pa_fr_repr) * n))) return rc;
-    PA_TRY(dt.alloc(8 * pa::g1_comb_table_words()), "hipMalloc");
-    PA_TRY(dw.alloc(8 * pa::g1_comb_workspace_words()), "hipMalloc");
-    PA_TRY(dout.alloc(sizeof(pa_g1) * n), "hipMalloc");
+    PA_TRY(dt.alloc(8 * pa::g1_comb_table_words()), "device scratch");
+    PA_TRY(dw.alloc(8 * pa::g1_comb_workspace_words()), "device scratch");
+    PA_TRY(dout.alloc(sizeof(pa_g1) * n), "device scratch");
     PA_TRY(pa::launch_g1_fixed_base(db.as<uint64_t>(), ds.as<uint64_t>(), dout.as<uint64_t>(), n, dt.as<uint64_t>(),
-                                    dw.as<uint64_t>(), nullptr),
+                                    dw.as<uint64_t>(), call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, sizeof(pa_g1) * n);
 }
 
@@ -550,12 +823,12 @@ int host_fr_op(int op, const void* a, const void* b, void* out, uint8_t* flag, c
     if ((rc = upload(da, a, bytes))) return rc;
     if (fr_op_needs_b(op) && (rc = upload(db, b, bytes))) return rc;
     if (op == pa::FR_POW && (rc = upload(dexp, exp, 8 * exp_words))) return rc;
-    PA_TRY(dout.alloc(bytes), "hipMalloc");
-    if (has_flag) PA_TRY(dflag.alloc(n), "hipMalloc");
+    PA_TRY(dout.alloc(bytes), "device scratch");
+    if (has_flag) PA_TRY(dflag.alloc(n), "device scratch");
     PA_TRY(pa::launch_fr_op(op, da.as<uint64_t>(), db.as<uint64_t>(), dout.as<uint64_t>(), dflag.as<uint8_t>(),
-                            dexp.as<uint64_t>(), (int)exp_words, n, nullptr),
+                            dexp.as<uint64_t>(), (int)exp_words, n, call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     if (has_out && (rc = download(out, dout, bytes))) return rc;
     if (has_flag && (rc = download(flag, dflag, n))) return rc;
     return PA_OK;
@@ -616,11 +889,11 @@ int host_scalar_mul(int group, int projective, const void* p, const pa_fr_repr* 
     DevBuf dp, ds, dout;
     int rc;
     if ((rc = upload(dp, p, in_rec * n)) || (rc = upload(ds, s, sizeof(pa_fr_repr) * n))) return rc;
-    PA_TRY(dout.alloc(out_rec * n), "hipMalloc");
+    PA_TRY(dout.alloc(out_rec * n), "device scratch");
     PA_TRY(pa::launch_scalar_mul(group, projective, dp.as<uint64_t>(), ds.as<uint64_t>(), n, dout.as<uint64_t>(),
-                                 nullptr),
+                                 call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, out_rec * n);
 }
 int host_multiexp(int group, const void* bases, const pa_fr_repr* s, size_t n, void* out) {
@@ -631,12 +904,12 @@ int host_multiexp(int group, const void* bases, const pa_fr_repr* s, size_t n, v
     DevBuf db, ds, dout, dws;
     int rc;
     if ((rc = upload(db, bases, in_rec * n)) || (rc = upload(ds, s, sizeof(pa_fr_repr) * n))) return rc;
-    PA_TRY(dout.alloc(out_rec), "hipMalloc");
+    PA_TRY(dout.alloc(out_rec), "device scratch");
     const size_t ws = pa::msm_workspace_bytes(group, n);
-    PA_TRY(dws.alloc(ws), "hipMalloc");
-    PA_TRY(pa::launch_msm(group, db.as<uint64_t>(), ds.as<uint64_t>(), n, dout.as<uint64_t>(), dws.p, ws, nullptr),
+    PA_TRY(dws.alloc(ws), "device scratch");
+    PA_TRY(pa::launch_msm(group, db.as<uint64_t>(), ds.as<uint64_t>(), n, dout.as<uint64_t>(), dws.p, ws, call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, out_rec);
 }
 }  // namespace
@@ -702,10 +975,10 @@ int host_group_op(int group, int op, const void* a, const void* b, void* out, si
     int rc;
     if ((rc = upload(da, a, ib * n))) return rc;
     if (bb && (rc = upload(db, b, bb * n))) return rc;
-    PA_TRY(dout.alloc(ob * n), "hipMalloc");
-    PA_TRY(pa::launch_group_op(group, op, da.as<uint64_t>(), db.as<uint64_t>(), dout.as<uint64_t>(), n, nullptr),
+    PA_TRY(dout.alloc(ob * n), "device scratch");
+    PA_TRY(pa::launch_group_op(group, op, da.as<uint64_t>(), db.as<uint64_t>(), dout.as<uint64_t>(), n, call_stream()),
            "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, ob * n);
 }
 int device_group_op(int group, int op, const void* a, const void* b, void* out, size_t n, void* stream) {
@@ -774,8 +1047,8 @@ int pa_g2_batch_normalization(pa_g2* v, size_t n) {
     DevBuf dv;
     int rc;
     if ((rc = upload(dv, v, sizeof(pa_g2) * n))) return rc;
-    PA_TRY(pa::launch_g2_batch_normalize(dv.as<uint64_t>(), n, nullptr), "kernel launch");
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(pa::launch_g2_batch_normalize(dv.as<uint64_t>(), n, call_stream()), "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
     return download(v, dv, sizeof(pa_g2) * n);
 }
 int pa_g2_batch_normalization_device(pa_g2* v, size_t n, void* stream) {
@@ -800,13 +1073,13 @@ int pa_g2_wnaf_fixed_base(const pa_g2* base, const pa_fr_repr* scalars, size_t n
     DevBuf db, ds, dt, dw, dout;
     int rc;
     if ((rc = upload(db, base, sizeof(pa_g2))) || (rc = upload(ds, scalars, sizeof(pa_fr_repr) * n))) return rc;
-    PA_TRY(dt.alloc(8 * pa::g2_comb_table_words()), "hipMalloc");
-    PA_TRY(dw.alloc(8 * pa::g2_comb_workspace_words()), "hipMalloc");
-    PA_TRY(dout.alloc(sizeof(pa_g2) * n), "hipMalloc");
+    PA_TRY(dt.alloc(8 * pa::g2_comb_table_words()), "device scratch");
+    PA_TRY(dw.alloc(8 * pa::g2_comb_workspace_words()), "device scratch");
+    PA_TRY(dout.alloc(sizeof(pa_g2) * n), "device scratch");
     if ((rc = pa_g2_wnaf_fixed_base_device(db.as<pa_g2>(), ds.as<pa_fr_repr>(), dout.as<pa_g2>(), n,
-                                           dt.as<uint64_t>(), dw.as<uint64_t>(), nullptr)))
+                                           dt.as<uint64_t>(), dw.as<uint64_t>(), call_stream())))
         return rc;
-    PA_TRY(hipDeviceSynchronize(), "kernel execution");
+    PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, sizeof(pa_g2) * n);
 }
 

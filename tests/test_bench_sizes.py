@@ -129,3 +129,31 @@ def test_pairing_two_streams_concurrently(gpu, oracle):
     t = _threads()
     np.testing.assert_array_equal(_host(outs[0][2]), oracle.pairing(p0, q0, t))
     np.testing.assert_array_equal(_host(outs[1][2]), oracle.pairing(p1, q1, t))
+
+
+def test_pairing_host_pipeline_chunks_and_threads(gpu, oracle, monkeypatch):
+    """pa_pairing_batch on host buffers: a multi-chunk pipelined call
+    (PA_PIPELINE_CHUNK shrinks the chunk so the pipeline's double buffers
+    turn over, ragged last chunk) and two host threads calling at once (each
+    on its own per-thread stream and scratch), all bit-exact"""
+    import threading
+    import bench
+    p, q = bench.make_pairs(3000, 0, seed=3)
+    monkeypatch.setenv("PA_PIPELINE_CHUNK", "700")
+    got = gpu.pairing(p, q)
+    monkeypatch.delenv("PA_PIPELINE_CHUNK")
+    t = _threads()
+    exp = oracle.pairing(p, q, t)
+    np.testing.assert_array_equal(got, exp)
+    res = [None, None]
+
+    def run(k):
+        for _ in range(3):
+            res[k] = gpu.pairing(p[k * 1500:(k + 1) * 1500], q[k * 1500:(k + 1) * 1500])
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    np.testing.assert_array_equal(np.concatenate(res), exp)
