@@ -509,7 +509,7 @@ def main():
             value = ws * n * args.steps / elapsed
             metric, unit = "BLS12-381 pairings/sec at batch 2^16", "pairings/s"
             config = {"workload": "bls12_381 e(P_i,Q_i) batch (fused G2 prepare + Miller loop + final exp)",
-                      "kernel_variant": ["gen", "gen2"][int(os.environ.get("PA_PAIRING_KERNEL", "0"))],
+                      "kernel_variant": ["gen", "gen2", "coop", "gen"][int(os.environ.get("PA_PAIRING_KERNEL", "0"))],
                       "batch_per_gpu": n, "global_batch": n * ws, "parallelism": "shard%d+rccl_gather" % ws
                       if ws > 1 else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}

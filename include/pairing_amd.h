@@ -77,11 +77,16 @@ const char *pa_last_error(void);
 int pa_device_count(int *count);
 int pa_set_device(int device);
 int pa_synchronize(void);
-/* Tuning knob: how the generated Miller-loop / final-exponentiation kernels
- * (tools/pgen: own register allocation, code objects lib/pa_gen_*.hsaco
- * loaded at first use) lay a pairing out (identical results):
- *   0 = one pairing per lane (default)
- *   1 = a lane pair per pairing (twice the waves; A/B alternative)
+/* Tuning knob: which kernels run the Miller loop / final exponentiation
+ * (identical results):
+ *   0 = default: batches of more than PA_COOP_MAX (2048) pairings on the
+ *       generated one-pairing-per-lane kernels (tools/pgen: own register
+ *       allocation, code objects lib/pa_gen_*.hsaco loaded at first use),
+ *       smaller batches on the cooperative kernels (one wave per pairing,
+ *       kernels_coop.hip: ~1/10 of the latency, the verifier shape)
+ *   1 = generated kernels with a lane pair per pairing, every size (A/B)
+ *   2 = cooperative kernels for every size (A/B, tests)
+ *   3 = generated one-pairing-per-lane kernels for every size (A/B, tests)
  * Process-wide; not part of the reference interface. */
 int pa_set_pairing_kernel(int variant);
 

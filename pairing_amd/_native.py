@@ -193,8 +193,9 @@ def device_count():
 
 
 def set_pairing_kernel(variant):
-    """Layout of the generated pairing kernels: 0 one pairing per lane
-    (default), 1 a lane pair per pairing.  Identical results."""
+    """Pairing kernels: 0 default (one lane per pairing; batches <= 2048 on the
+    one-wave-per-pairing cooperative kernels), 1 lane pairs, 2 cooperative
+    for every size, 3 one lane per pairing for every size.  Identical results."""
     call("pa_set_pairing_kernel", int(variant))
 
 

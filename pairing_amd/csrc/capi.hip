@@ -21,15 +21,29 @@
 namespace {
 
 thread_local std::string g_last_error;
-// lanes per pairing of the generated Miller-loop / final-exponentiation
-// kernels (pa_set_pairing_kernel: 0 -> 1 lane, the default; 1 -> 2 lanes)
-int g_pairing_lanes = 1;
+// Pairing kernel selection (pa_set_pairing_kernel): 0 -> one lane per
+// pairing (the generated kernels), with batches of at most coop_max() pairs
+// on the cooperative one-wave-per-pairing kernels (kernels_coop.hip, ~1/10
+// of the latency); 1 -> lane pairs; 2 -> cooperative for every batch size;
+// 3 -> one lane per pairing for every batch size.
+int g_pairing_variant = 0;
+
+size_t coop_max() {
+    static const size_t v = [] {
+        const char* e = getenv("PA_COOP_MAX");   // A/B measurements
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)2048;
+    }();
+    return v;
+}
+bool use_coop(size_t n) { return g_pairing_variant == 2 || (g_pairing_variant == 0 && n <= coop_max()); }
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
-    return pa::launch_miller_loop_gen(g_pairing_lanes, p, q, out, n, s);
+    if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s);
+    return pa::launch_miller_loop_gen(g_pairing_variant == 1 ? 2 : 1, p, q, out, n, s);
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
-    return pa::launch_final_exp_gen(g_pairing_lanes, in, out, ok, n, s);
+    if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s);
+    return pa::launch_final_exp_gen(g_pairing_variant == 1 ? 2 : 1, in, out, ok, n, s);
 }
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
@@ -259,8 +273,8 @@ int pa_set_device(int device) {
     return PA_OK;
 }
 int pa_set_pairing_kernel(int variant) {
-    if (variant < 0 || variant > 1) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0 or 1");
-    g_pairing_lanes = variant + 1;
+    if (variant < 0 || variant > 3) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..3");
+    g_pairing_variant = variant;
     return PA_OK;
 }
 int pa_synchronize(void) {

@@ -138,6 +138,14 @@ class Prog:
         assert a.u <= 3, "sqr bound %d" % a.u
         return self._op("sqr", [a], 1)
 
+    def inv(self, a):
+        """a^-1 in the Fl domain (0 -> 0) as ONE op.  The cooperative kernels
+        (coop.py, kernels_coop.hip) run it on the 12-word core's binary GCD
+        (bgcd.h); the one-lane generated kernels use Tower.inv_fq's Fermat
+        chain instead."""
+        self._full(a)
+        return self._op("inv", [a], 1)
+
     # ---- wide (double-width, unreduced) values: lazy reduction ----
     def wsop(self, *args):
         """sum a_i b_i over the pairs (a0, b0, a1, b1, ...) as a 28-limb
@@ -226,6 +234,16 @@ class Prog:
     def set(self, name, v):
         assert v.u <= self.vars[name].u, "setvar %s: bound %d > %d" % (name, v.u, self.vars[name].u)
         self.cur.items.append(Op("setvar", None, [v], imm=name))
+
+    # ---- cooperative macro operands (coop.py): value slots addressed by
+    # (group, index); an arg is a stored field value of bound u, a ret stores
+    # a value (bound 1) ----
+    def arg(self, group, index, u=1):
+        return self._op("arg", [], u, imm=(group, index))
+
+    def ret(self, group, index, v):
+        assert v.u == 1, "a macro output must be reduced (bound 1)"
+        self.cur.items.append(Op("ret", None, [v], imm=(group, index)))
 
     # ---- kernel I/O (see kernels.py for the record layouts) ----
     def load(self, slot, slot1=None):
@@ -431,6 +449,9 @@ def evaluate(prog, inputs, stats=None, trace=None):
             return tuple(a + ci - b for a, ci, b in zip(s[0], op.imm, s[1]))
         if k == "wred":
             return mont_reduce_wide(s[0], s[1])
+        if k == "inv":
+            v = val_of(s[0]) % Q
+            return tuple(gen_fl.limbs(R * R * pow(v, -1, Q) % Q if v else 0))
         raise ValueError(k)
 
     def step(op):
@@ -445,6 +466,11 @@ def evaluate(prog, inputs, stats=None, trace=None):
             r = vars_[op.imm]
         elif k == "setvar":
             vars_[op.imm] = s[0]
+            return
+        elif k == "arg":
+            r = [tuple(inputs[op.imm])] * L
+        elif k == "ret":
+            outs[op.imm] = s[0][0]
             return
         elif k == "load_raw":
             slots = op.imm if isinstance(op.imm, tuple) else (op.imm,) * L

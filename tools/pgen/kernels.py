@@ -186,10 +186,13 @@ def exp_by_x(p, T, V, f, x, tag):
     return T.conj12(V.get12(res))
 
 
-def final_exp_prog(lanes=1, lazy=False):
-    """lazy: False (Tower), True (TowerLazy) or "sq" (TowerLazySq)"""
+def final_exp_prog(lanes=1, lazy=False, tower_cls=None):
+    """lazy: False (Tower), True (TowerLazy) or "sq" (TowerLazySq);
+    tower_cls overrides the tower class (coop.py: inversion as one op)"""
     p = Prog("final_exp" if lanes == 1 else "final_exp2", lanes)
-    if lanes == 2:
+    if tower_cls is not None:
+        T = tower_cls(p)
+    elif lanes == 2:
         T = Tower2(p)
     else:
         T = {False: Tower, True: TowerLazy, "sq": TowerLazySq}[lazy](p)
