@@ -116,3 +116,13 @@ def test_sim_final_exp_kernel(which):
 def test_generated_code_objects_assemble(tmp_path):
     out = build_gen.build("small", str(tmp_path))
     assert os.path.getsize(out) > 0
+
+
+def test_coop_schedules_replay_equal_dsl():
+    """tools/pgen/coop.py: every cooperative macro's encoded schedule (LIN
+    chains, merged products, slot reuse) replayed with the exact limb
+    semantics equals the DSL macro it was built from"""
+    import coop
+    macros, consts = coop.build_all()
+    coop.check(macros, consts, trials=1)
+    assert sum(len(m.records) for m in macros) < 200
