@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 16, help="pairings per GPU per step")
-    ap.add_argument("--workload", choices=["pairing", "fq_mul", "fr_mul", "wnaf", "decode", "msm"], default="pairing")
+    ap.add_argument("--workload", choices=["pairing", "fq_mul", "fr_mul", "wnaf", "decode", "msm", "verify"],
+                    default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-stub", action="store_true",
@@ -442,6 +443,24 @@ def main():
             pdev.multiexp(1, bases, scal, msm_out, msm_ws, stream)
             if timed:
                 ev[1].record(stream)
+    elif args.workload == "verify":
+        # SURVEY.md §8 f rank 2, the verifier shape: one multi_pairing over a few
+        # pairs (Engine::miller_loop product + final_exponentiation, mod.rs:40-160)
+        # -- a latency, on the cooperative one-wave-per-pairing kernels
+        n = args.batch if args.batch != (1 << 16) else 2
+        p_np, q_np = make_pairs(n, rank, seed=3)
+        p = torch.from_numpy(p_np.view(np.int64)).to(dev)
+        q = torch.from_numpy(q_np.view(np.int64)).to(dev)
+        out = pdev.empty_records(1, 72, dev)
+        okb = torch.empty(1, dtype=torch.uint8, device=dev)
+        work = pdev.empty_records(n, 72, dev)
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            pdev.multi_pairing(p, q, out, okb, work, stream)
+            if timed:
+                ev[1].record(stream)
     elif args.workload == "fr_mul":
         g = np.random.default_rng(rank)
         n = args.batch if args.batch != (1 << 16) else (1 << 20)
@@ -543,6 +562,13 @@ def main():
             metric, unit = "G1 multi-scalar multiplication terms per second at n = 2^20", "terms/s"
             config = {"workload": "one G1 MSM sum_i s_i P_i over 2^20 distinct affine bases (Pippenger, c = 16)",
                       "batch_per_gpu": n, "global_batch": n * ws, "kernel_ms": {"multiexp": round(dom_ms, 3)}}
+        elif args.workload == "verify":
+            dom_name, dom_ms, dom_bytes = "multi_pairing", float(np.mean(k_ms["a"])), 304 * n + 577
+            value = dom_ms
+            metric, unit = "multi_pairing latency, %d pairs (verifier shape)" % n, "ms"
+            config = {"workload": "final_exponentiation(miller_loop([(P_i, Q_i)])) over %d pairs, inputs in HBM, "
+                                  "cooperative one-wave-per-pairing kernels" % n,
+                      "batch_per_gpu": n, "global_batch": n * ws, "kernel_ms": {"multi_pairing": round(dom_ms, 3)}}
         elif args.workload == "fr_mul":
             dom_name, dom_ms, dom_bytes = "fr_mul_batch", float(np.mean(k_ms["a"])), 96
             value = ws * n * args.steps / elapsed
@@ -599,6 +625,22 @@ def main():
                     "avg_launch_ms": round(dom_ms, 4),
                     "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS,
                             "bytes_per_unit": dom_bytes}}
+        if args.workload == "msm":
+            # VALU view: every term enters W = 17 windows; each entry is one mixed
+            # addition into a bucket (madd-2007-bl on the lazy core: 7 products + 4
+            # squarings, 7 x 392 + 4 x 301 limb MACs); the bucket sums and Horner
+            # steps are < 3 % on top and not counted
+            macs = 17 * (7 * 392 + 4 * 301)
+            mac_rate = macs * n / (dom_ms * 1e-3) / 1e12
+            roof = {"kernel": "g1_multiexp (all its kernels)", "bound": "valu", "achieved": round(mac_rate, 3),
+                    "peak": round(VALU_MAC_PEAK_T, 3), "unit": "T limb-MAC/s (28x28-bit v_mad_u64_u32)",
+                    "frac": mac_rate / VALU_MAC_PEAK_T, "traffic": traffic, "macs_per_unit": macs,
+                    "avg_launch_ms": round(dom_ms, 4),
+                    "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS, "bytes_per_unit": dom_bytes}}
+        if args.workload == "verify":
+            roof = {"kernel": "multi_pairing", "bound": "latency", "achieved": round(dom_ms, 4), "peak": None,
+                    "unit": "ms", "frac": None, "traffic": None,
+                    "note": "dependent product levels of one wave (DESIGN.md section 4, cooperative kernels)"}
         cpu = None
         if not args.no_cpu_baseline and ws == 1:
             if args.workload == "pairing":
@@ -611,12 +653,22 @@ def main():
                 cpu = cpu_baseline_msm(base_np, k_np, s_np, args.cpu_seconds)
             elif args.workload == "fr_mul":
                 cpu = cpu_baseline_fr_mul(a_np, b_np)
+            elif args.workload == "verify":
+                from oracle import binding as oracle
+                t0 = time.perf_counter()
+                reps = 20
+                for _ in range(reps):
+                    f = oracle.miller_loop(p_np, oracle.g2_prepare(q_np))
+                    oracle.final_exponentiation(f[None, :].copy())
+                cpu = {"value": (time.perf_counter() - t0) / reps * 1e3, "unit": "ms", "cores": 1, "kind": "port",
+                       "sample": "%d x multi_pairing of the same %d pairs, C restatement (oracle/), 1 thread"
+                                 % (reps, n)}
             else:
                 cpu = cpu_baseline_fq_mul(a_np, b_np, args.cpu_seconds)
         line = {"metric": metric, "value": value, "unit": unit, "n_gpus": ws, "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+                "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": args.workload != "verify",
                 "scaling": "weak", "vs_baseline": None,
-                "dtype": "u32 (14 x 28-bit lazy Montgomery limbs)" if args.workload == "pairing"
+                "dtype": "u32 (14 x 28-bit lazy Montgomery limbs)" if args.workload in ("pairing", "verify", "fq_mul")
                 else "u32 (256-bit Montgomery, 8 x u32 limbs)" if args.workload == "fr_mul"
                 else "u32 (14 x 28-bit lazy Montgomery limbs; 12 x u32 normalize)" if args.workload == "wnaf"
                 else "u32 (384-bit Montgomery, 12 x u32 limbs)",

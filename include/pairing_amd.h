@@ -316,6 +316,10 @@ int pa_g2_into_affine_batch_device(const pa_g2 *a, pa_g2_affine *out, size_t n, 
 int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
                                       void *stream);
 int pa_final_exponentiation_batch_device(const pa_fq12 *in, pa_fq12 *out, uint8_t *ok, size_t n, void *stream);
+/* pa_multi_pairing on device memory (the verifier's check without host copies); `work` holds n
+ * pa_fq12 (the per-pair Miller values, reduced in place to their product) */
+int pa_multi_pairing_device(const pa_g1_affine *p, const pa_g2_affine *q, size_t n, pa_fq12 *out, uint8_t *ok,
+                            pa_fq12 *work, void *stream);
 /* e(p[i], q[i]); `scratch` must hold n pa_fq12 (the Miller-loop values) */
 int pa_pairing_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, pa_fq12 *scratch,
                             size_t n, void *stream);

@@ -148,6 +148,7 @@ for _g in (1, 2):
     _SIGS["pa_g%d_recommended_wnaf_for_num_scalars" % _g] = [_N]
 _SIGS.update({
     "pa_fq2_inverse_batch": [_P, _P, _P, _N],
+    "pa_multi_pairing_device": [_P, _P, _N, _P, _P, _P, _P],
     "pa_fq2_frobenius_map_batch": [_P, _P, _N, _N],
     "pa_fq6_square_batch": [_P, _P, _N],
     "pa_fq6_inverse_batch": [_P, _P, _P, _N],

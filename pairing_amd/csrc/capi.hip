@@ -650,6 +650,28 @@ int pa_multi_miller_loop_affine(const pa_g1_affine* p, const pa_g2_affine* q, si
     return download(out, dout, 576);
 }
 
+int pa_multi_pairing_device(const pa_g1_affine* p, const pa_g2_affine* q, size_t n, pa_fq12* out, uint8_t* ok,
+                            pa_fq12* work, void* stream) {
+    if (!out || !ok || (n && (!p || !q || !work))) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {   // empty product: one, final_exponentiation(one) = one
+        pa_fq12 one;
+        memset(&one, 0, sizeof one);
+        const uint64_t r[6] = {0x760900000002fffdULL, 0xebf4000bc40c0002ULL, 0x5f48985753c758baULL,
+                               0x77ce585370525745ULL, 0x5c071a97a256ec6dULL, 0x15f65ec3fa80e493ULL};
+        memcpy(one.c0.c0.c0.l, r, sizeof r);
+        const uint8_t k = 1;
+        PA_TRY(hipMemcpyAsync(out, &one, sizeof one, hipMemcpyHostToDevice, s), "H2D copy");
+        PA_TRY(hipMemcpyAsync(ok, &k, 1, hipMemcpyHostToDevice, s), "H2D copy");
+        PA_TRY(hipStreamSynchronize(s), "H2D copy");   // the host sources go out of scope
+        return PA_OK;
+    }
+    PA_TRY(ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)work, n, s), "kernel launch");
+    PA_TRY(pa::launch_fq12_product((uint64_t*)work, n, (uint64_t*)work, s), "kernel launch");
+    PA_TRY(fe_launch((const uint64_t*)work, (uint64_t*)out, ok, 1, s), "kernel launch");
+    return PA_OK;
+}
+
 int pa_multi_pairing(const pa_g1_affine* p, const pa_g2_affine* q, size_t n, pa_fq12* out, uint8_t* ok) {
     if (!out || !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     pa_fq12 ml;

@@ -4,6 +4,7 @@
 // Layout: every operand is the reference's in-memory order (AoS, 6 x u64
 // per Fq), read with 16-byte loads: a wave reads 64 contiguous 48-byte
 // records = 3 KiB with three dwordx4 instructions, every byte used.
+#include "fl.h"
 #include "launch.h"
 #include "pairing.h"
 
@@ -71,6 +72,46 @@ PA_DEV void field_pow(F& r, const F& x, const uint64_t* exp, int words) {
             }
         }
     }
+}
+
+static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// Config-2 kernel: Fq::mul_assign on the lazy 28-bit core's product leaf.  The
+// 14-limb Montgomery product divides by R' = 2^392, the reference's by
+// R = 2^384 (fq.rs:909-960), so one operand enters shifted left by 8 bits:
+// a 2^8 < 2^389 still splits into 14 limbs below 2^28 (limb bound 1), and
+//   (a 2^8) b / 2^392 = a b / 2^384  (mod q),  output < (2^8 q^2 / R' + q) < 2q,
+// which one conditional subtraction makes canonical.  392 carry-free
+// multiply-accumulates instead of 292 multiply-accumulates + 288 carries.
+PA_DEV F<1> fl_split_shl8(const Fq& x) {
+    F<1> r;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+        const int bit = 28 * i - 8;   // limb i of x 2^8 = bits [bit, bit + 28) of x
+        uint64_t v;
+        if (bit < 0) {
+            v = (uint64_t)x.w[0] << 8;
+        } else {
+            const int wi = bit >> 5, sh = bit & 31;
+            v = (uint64_t)x.w[wi];
+            if (wi + 1 < 12) v |= (uint64_t)x.w[wi + 1] << 32;
+            v >>= sh;
+        }
+        r.w[i] = (uint32_t)v & FL_MASK;
+    }
+    return r;
+}
+__global__ void __launch_bounds__(256) k_fq_mul_batch_fl(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
+                                                          uint64_t* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fq x, y;
+    fq_load(x, a + 6 * i);
+    fq_load(y, b + 6 * i);
+    const F<1> xs = fl_split_shl8(x), ys = fl_split(y);
+    F<1> z;
+    fl_mul_leaf(z.w, xs.w, ys.w);
+    fq_store(out + 6 * i, fl_pack(fl_canon(z)));
 }
 
 template <int OP>
@@ -183,11 +224,20 @@ __global__ void __launch_bounds__(64) k_fq12_mul_by_014(const uint64_t* __restri
     store(out + 72 * i, z);
 }
 
-static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
-
 hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
                                hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    // Default: the lazy 28-bit core (k_fq_mul_batch_fl, 29.4 us at 2^20
+    // against 32.5 us for the 12 x u32 kernel, profiles/r02_fq_variants.txt).
+    // PA_FQ_VARIANT=0 selects the 12 x u32 streaming kernel for A/B runs.
+    static const int variant = [] {
+        const char* e = getenv("PA_FQ_VARIANT");
+        return e ? atoi(e) : 4;
+    }();
+    if (variant != 0) {
+        hipLaunchKernelGGL(k_fq_mul_batch_fl, dim3(blocks_for(n, 256)), dim3(256), 0, stream, a, b, out, n);
+        return hipGetLastError();
+    }
     size_t blocks = (n + 255) / 256;
     const StreamCfg c = stream_cfg();
     if (blocks > c.max_blocks) blocks = c.max_blocks;

@@ -116,6 +116,7 @@ hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStrea
         if (e != hipSuccess) return e;
         cnt = half;
     }
+    if (out == work) return hipSuccess;
     return hipMemcpyAsync(out, work, 72 * sizeof(uint64_t), hipMemcpyDeviceToDevice, stream);
 }
 

@@ -54,6 +54,14 @@ def pairing(p, q, out, scratch, stream=None):
          _dptr(scratch, W_FQ12, "scratch"), p.shape[0], _stream_ptr(stream))
 
 
+def multi_pairing(p, q, out, ok, work, stream=None):
+    """final_exponentiation(miller_loop(pairs)) over pairs resident in HBM (the verifier's
+    batch check, mod.rs:40-160): out (1, 72), ok (1,) uint8, work (n, 72) scratch."""
+    call("pa_multi_pairing_device", _dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"), p.shape[0],
+         _dptr(out, W_FQ12, "out"), ctypes.c_void_p(ok.data_ptr()), _dptr(work, W_FQ12, "work"),
+         _stream_ptr(stream))
+
+
 def g1_fixed_base_table(base, stream=None):
     """Build the fixed-base table for `base` (a (1,18) Jacobian record) in HBM."""
     dev = base.device

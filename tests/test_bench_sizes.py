@@ -157,3 +157,31 @@ def test_pairing_host_pipeline_chunks_and_threads(gpu, oracle, monkeypatch):
     for x in th:
         x.join()
     np.testing.assert_array_equal(np.concatenate(res), exp)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 5])
+def test_multi_pairing_device_matches_oracle(gpu, oracle, n):
+    """bench.py --workload verify: pa_multi_pairing_device (cooperative Miller
+    loops, product tree, one final exponentiation) == the oracle's
+    final_exponentiation(miller_loop(pairs)); the empty product is one"""
+    import torch
+    import bench
+    import pairing_amd.device as pdev
+    from helpers import fq12_one
+    p_np, q_np = bench.make_pairs(max(n, 1), 0, seed=3)
+    p_np, q_np = p_np[:n], q_np[:n]
+    out = pdev.empty_records(1, 72, "cuda:0")
+    ok = torch.zeros(1, dtype=torch.uint8, device="cuda:0")
+    work = pdev.empty_records(max(n, 1), 72, "cuda:0")
+    dp = _dev(np.ascontiguousarray(p_np)) if n else torch.zeros((0, 13), dtype=torch.int64, device="cuda:0")
+    dq = _dev(np.ascontiguousarray(q_np)) if n else torch.zeros((0, 25), dtype=torch.int64, device="cuda:0")
+    pdev.multi_pairing(dp, dq, out, ok, work)
+    torch.cuda.synchronize()
+    if n == 0:
+        exp = fq12_one()[0]
+    else:
+        f = oracle.miller_loop(np.ascontiguousarray(p_np), oracle.g2_prepare(np.ascontiguousarray(q_np)))
+        exp, eok = oracle.final_exponentiation(f[None, :].copy())
+        exp = exp[0]
+    assert int(ok.item()) == 1
+    np.testing.assert_array_equal(_host(out)[0], exp)
