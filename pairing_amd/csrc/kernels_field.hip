@@ -114,6 +114,21 @@ __global__ void __launch_bounds__(256) k_fq_mul_batch_fl(const uint64_t* __restr
     fq_store(out + 6 * i, fl_pack(fl_canon(z)));
 }
 
+// Probe for config 2 (PA_FQ_VARIANT=9, not the product path): the same record
+// traffic with no multiply (z = x ^ y), i.e. the access-pattern bound: 25.0 us at
+// 2^20 against 29.0 us with the multiply (profiles/r02_fq_variants_s7.txt; a
+// wave-coalesced LDS-staged form of the multiply kernel measured 29.4-29.7 us).
+__global__ void __launch_bounds__(256) k_fq_xor_probe(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
+                                                       uint64_t* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fq x, y;
+    fq_load(x, a + 6 * i);
+    fq_load(y, b + 6 * i);
+#pragma unroll
+    for (int k = 0; k < 12; k++) x.w[k] ^= y.w[k];
+    fq_store(out + 6 * i, x);
+}
 template <int OP>
 __global__ void __launch_bounds__(64) k_field_op(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
                                                  uint64_t* __restrict__ out, uint8_t* __restrict__ ok,
@@ -234,8 +249,20 @@ hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* o
         const char* e = getenv("PA_FQ_VARIANT");
         return e ? atoi(e) : 4;
     }();
+    if (variant == 9) {
+        hipLaunchKernelGGL(k_fq_xor_probe, dim3(blocks_for(n, 256)), dim3(256), 0, stream, a, b, out, n);
+        return hipGetLastError();
+    }
     if (variant != 0) {
-        hipLaunchKernelGGL(k_fq_mul_batch_fl, dim3(blocks_for(n, 256)), dim3(256), 0, stream, a, b, out, n);
+        // 27000 B of (unused) dynamic LDS per 256-thread block caps residency at
+        // 5 waves per SIMD: fewer waves finish their multiplies together after the
+        // last loads land (29.0 vs 30.0-30.3 us at 2^20; 3 waves: 32.2 us;
+        // profiles/r02_fq_occupancy.txt).  PA_FQ_LDS overrides it for A/B runs.
+        static const unsigned lds = [] {
+            const char* e = getenv("PA_FQ_LDS");
+            return e ? (unsigned)atoi(e) : 27000u;
+        }();
+        hipLaunchKernelGGL(k_fq_mul_batch_fl, dim3(blocks_for(n, 256)), dim3(256), lds, stream, a, b, out, n);
         return hipGetLastError();
     }
     size_t blocks = (n + 255) / 256;

@@ -51,8 +51,8 @@ U_MAX_SUB = 14  # SUB_C tables for subtrahend bounds 1..U_MAX_SUB
 KQ = (1 << 400) // Q
 assert KQ < (1 << 32)
 
-QS = 80  # q limbs in s[80:93]
-QI = 94  # qinv in s94
+QS = 40  # q limbs in s[40:53] (low: keeps the hipcc kernels under 80 SGPRs, 8 waves/SIMD)
+QI = 54  # qinv in s54
 
 
 def limbs(v, n=NL):

@@ -36,6 +36,32 @@ def small_prog():
     return p
 
 
+def cyc_probe_prog(iters=None):
+    """timing probe (not a product kernel): iters cyclotomic squarings in a loop,
+    the final exponentiation's hot loop body alone (tools/pgen/gpu_check.py cyc)"""
+    from tower import TowerLazySq
+    iters = iters or int(os.environ.get("PGEN_CYC_ITERS", "100"))
+    p = dsl.Prog("cyc")
+    T = TowerLazySq(p)
+    f = (((p.load(0), p.load(1)), (p.load(2), p.load(3)), (p.load(4), p.load(5))),
+         ((p.load(6), p.load(7)), (p.load(8), p.load(9)), (p.load(10), p.load(11))))
+    declare12(p, "acc", "A")
+    set12(p, "acc", f)
+    body = os.environ.get("PGEN_CYC_BODY", "cyc")
+    with p.loop(iters):
+        if body == "cyc":
+            set12(p, "acc", T.cyc_sqr(get12(p, "acc")))
+        else:   # k Fq4 squarings (a third of a cyclotomic square each): code-size probe
+            (a0, a1, a2), (b0, b1, b2) = get12(p, "acc")
+            pairs = [(a0, b1), (b0, a2), (a1, b2)]
+            outs = [T.fq4_sqr(x, y) for x, y in pairs[:int(body[3:])]] + pairs[int(body[3:]):]
+            (a0, b1), (b0, a2), (a1, b2) = outs
+            set12(p, "acc", ((a0, a1, a2), (b0, b1, b2)))
+    for i, v in enumerate(v for c6 in get12(p, "acc") for c2 in c6 for v in c2):
+        p.store(i, v)
+    return p
+
+
 def _mk(progf, cfgc, kname):
     cache = {}
 
@@ -55,6 +81,7 @@ def _mk(progf, cfgc, kname):
 
 PROGRAMS = {
     "small": _mk(small_prog, kcfg.FinalExpCfg, "pa_gen_small"),
+    "cyc": _mk(cyc_probe_prog, kcfg.FinalExpCfg, "pa_gen_cyc"),
     "ml": _mk(kernels.miller_loop_prog, kcfg.MillerLoopCfg, "pa_gen_miller_loop"),
     # default final exponentiation: lazy Fq4 squarings only (tower.TowerLazySq, -1.5 % time);
     # PGEN_FE_LAZY=0 / 1 builds the plain / fully lazy tower instead (A/B experiments)
@@ -67,7 +94,7 @@ PROGRAMS = {
     "mlz": _mk(lambda: kernels.miller_loop_prog(lazy=True), kcfg.MillerLoopCfg, "pa_gen_miller_loop_lazy"),
     "fez": _mk(lambda: kernels.final_exp_prog(lazy=True), kcfg.FinalExpCfg, "pa_gen_final_exp_lazy"),
 }
-FILES = {"small": "pa_gen_small.hsaco", "ml": "pa_gen_miller_loop.hsaco", "fe": "pa_gen_final_exp.hsaco",
+FILES = {"small": "pa_gen_small.hsaco", "cyc": "pa_gen_cyc.hsaco", "ml": "pa_gen_miller_loop.hsaco", "fe": "pa_gen_final_exp.hsaco",
          "ml2": "pa_gen_miller_loop2.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
          "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco"}
 

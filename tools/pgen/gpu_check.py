@@ -77,7 +77,7 @@ def main():
     global LANES
     LANES = prog.lanes
     rng = random.Random(5)
-    if which in ("small", "fe", "fe2"):
+    if which in ("small", "fe", "fe2", "cyc"):
         ins = [[rand_fq(rng) for _ in range(12)] for _ in range(n)]
         ins[1] = [0] * 12  # f == 0 lane
         rec_in = np.array([to_words(r) for r in ins], dtype=np.uint64)
