@@ -84,3 +84,65 @@ def test_sharded_pairing_world2_gloo(tmp_path, oracle, n):
     np.testing.assert_array_equal(res["out"].view(np.uint64), oracle.pairing(p, q, 4))
     single = oracle.miller_loop(p, oracle.g2_prepare(q))
     np.testing.assert_array_equal(res["prod"].view(np.uint64)[0], single)
+
+
+def _hip_worker(rank, world, port, n, result_path):
+    """Per-rank compute through the HIP C ABI (pairing_amd): each rank pairs its
+    shard and reduces its shard's Miller loops to one Fq12 on the GPU; the
+    exchange is gloo here (both ranks share the box's one GPU; RCCL needs a
+    device per rank, bench.py --gpus N uses it)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import pairing_amd
+    from pairing_amd.shard import sharded_batch, sharded_product
+
+    pairing_amd.set_device(0)
+    d = np.load(os.path.join(root, "tests", "golden", "bench_points.npz"))
+    p = torch.from_numpy(d["g1"][:n].view(np.int64).copy())
+    q = torch.from_numpy(d["g2"][:n].view(np.int64).copy())
+
+    def compute(ps, qs):
+        out = pairing_amd.pairing(ps.numpy().view(np.uint64), qs.numpy().view(np.uint64))
+        return torch.from_numpy(out.view(np.int64))
+
+    def local_product(ps, qs):
+        f = pairing_amd.multi_miller_loop_affine(ps.numpy().view(np.uint64), qs.numpy().view(np.uint64))
+        return torch.from_numpy(f.reshape(1, 72).view(np.int64).copy())
+
+    def combine(rows):
+        acc = rows[0:1].numpy().view(np.uint64).copy()
+        for r in range(1, rows.shape[0]):
+            acc = pairing_amd.fq12_mul(acc, rows[r:r + 1].numpy().view(np.uint64).copy())
+        fe, ok = pairing_amd.final_exponentiation(acc)
+        assert ok[0]
+        return torch.from_numpy(np.concatenate([acc, fe], axis=0).view(np.int64))
+
+    out = sharded_batch(p, q, compute)
+    prod = sharded_product(p, q, local_product, combine)
+    if rank == 0:
+        np.savez(result_path, out=out.numpy(), prod=prod.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [64, 1000])  # even / ragged shards; the product runs on the cooperative path (<= 2048)
+def test_sharded_pairing_world2_hip(tmp_path, oracle, n):
+    # the parent never touches the GPU (the ranks do; a rank without a device raises)
+    world = 2
+    path = str(tmp_path / "res.npz")
+    mp.spawn(_hip_worker, args=(world, _free_port(), n, path), nprocs=world, join=True)
+    res = np.load(path)
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "bench_points.npz"))
+    p, q = d["g1"][:n].copy(), d["g2"][:n].copy()
+    np.testing.assert_array_equal(res["out"].view(np.uint64), oracle.pairing(p, q, 8))
+    prod = res["prod"].view(np.uint64)
+    single = oracle.miller_loop(p, oracle.g2_prepare(q))
+    np.testing.assert_array_equal(prod[0], single)
+    fe, ok = oracle.final_exponentiation(single.reshape(1, 72).copy())
+    assert ok[0] == 1
+    np.testing.assert_array_equal(prod[1], fe[0])
