@@ -75,6 +75,12 @@ class ValState:
 
 
 S_ODD = 40          # s[40:41] lane mask of the odd lanes (lane pairs: role 1)
+# s[42:80) subtraction constants (loaded by the prologue): the SUBC[1] and
+# SUBC[2] limb tables, then (two SGPRs each: limb 0..12, limb 13) the wide
+# subtraction constants whose limbs 0..12 are equal; a - b = a + C - b is then
+# one v_sad_u32 per limb (|C_i - b_i| + a_i, C_i >= b_i by the bound tracking)
+S_CTAB, S_CTAB_END = 42, 80
+CTAB_FULL = (1, 2)
 
 # storage configurations: (V slots, A slots, L slots)
 STORAGE = {1: (17, 18, int(os.environ.get("PGEN_NL", 11))),  # one wave per SIMD: 256 VGPR + 256 AGPR, 40 KB LDS
@@ -111,6 +117,14 @@ class Emitter:
         self.defer_vm_wait = False   # batch the waits of one operation's HBM reloads
         self.vm_wait_owed = False
         self.vm_owed_seq = 0
+        self.ctab = {}               # constant key -> ("full", sgpr base) | ("uni", sgpr of limbs 0..12)
+        self.ctab_init = []          # (sgpr, value) loaded by the prologue
+        self.ctab_next = S_CTAB
+        if os.environ.get("PGEN_SAD", "1") == "1":
+            for ub in CTAB_FULL:
+                self.ctab[("sub", ub)] = ("full", self.ctab_next)
+                self.ctab_init += [(self.ctab_next + i, SUBC[ub][i]) for i in range(NL)]
+                self.ctab_next += NL
 
     # ---------------- emission helpers ----------------
     VMEM = ("global_load_dwordx2", "global_load_dword", "global_store_dwordx2", "global_store_byte",
@@ -420,8 +434,29 @@ class Emitter:
         for i in range(NL):
             self.i("v_add_u32", d + i, a + i, b + i)
 
+    def ctab_reg(self, key, c):
+        """SGPR of limb i of constant c (or None): full tables for SUBC[1], SUBC[2];
+        constants with equal limbs 0..12 take two SGPRs while the area lasts"""
+        if os.environ.get("PGEN_SAD", "1") != "1":
+            return None
+        e = self.ctab.get(key)
+        if e is None and all(x == c[0] for x in c[:NL - 1]) and self.ctab_next + 2 <= S_CTAB_END:
+            e = self.ctab[key] = ("uni", self.ctab_next)
+            self.ctab_init += [(self.ctab_next, c[0]), (self.ctab_next + 1, c[NL - 1])]
+            self.ctab_next += 2
+        if e is None:
+            return None
+        if e[0] == "full":
+            return lambda i: S(e[1] + i)
+        return lambda i: S(e[1] if i < NL - 1 else e[1] + 1)
+
     def emit_sub(self, a, b, d, ub):
         c = SUBC[ub]
+        r = self.ctab_reg(("sub", ub), c)
+        if r is not None:
+            for i in range(NL):
+                self.i("v_sad_u32", d + i, r(i), b + i, a + i)
+            return
         if d == b:
             assert a != b
             for i in range(NL):
@@ -434,6 +469,11 @@ class Emitter:
 
     def emit_csub(self, a, b, d, c):
         """a + C - b limb-wise, C given (wide-value halves)"""
+        r = self.ctab_reg(("csub", tuple(c)), c)
+        if r is not None:
+            for i in range(NL):
+                self.i("v_sad_u32", d + i, r(i), b + i, a + i)
+            return
         if d == b:
             assert a != b
             for i in range(NL):

@@ -47,6 +47,8 @@ class KernelCfg:
             i(("s_mov_b32", S(SQ + k), K(w)))
         i(("s_mov_b32", S(SQINV), K(QINV28)))
         i(("s_mov_b32", S(SKQ), K(KQ)))
+        for sreg, v in em.ctab_init:
+            i(("s_mov_b32", S(sreg), K(v)))
         wave_bytes = max(nmem, 1) * gen_fl.NL * 4 * 64
         i(("s_mul_i32", S(S_TMP), S(S_WG), K(wave_bytes)))
         i(("s_mul_hi_u32", S(S_TMP + 1), S(S_WG), K(wave_bytes)))
