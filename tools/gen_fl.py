@@ -76,6 +76,22 @@ def sub_constant(ub):
     return c, max(ulimb, uval)
 
 
+def sub_constant2(ulimb, vtop):
+    """C = k q with limbs c_i >= ulimb (2^28-1) (i < 13) and c_13 >= vtop 2^18 + 1:
+    for a subtrahend of limb bound ulimb and value bound vtop 2q (its top limb is
+    below value / 2^364 < vtop 2^18).  Returns (limbs, limb bound of C, value
+    bound of C in units of 2q)."""
+    lo = [ulimb * MASK] * (NL - 1) + [vtop * (1 << 18)]
+    minv = sum(c << (LB * i) for i, c in enumerate(lo))
+    k = -(-minv // Q)
+    d = k * Q - minv
+    c = [lo[i] + ((d >> (LB * i)) & MASK) for i in range(NL - 1)]
+    c.append(lo[NL - 1] + (d >> (LB * (NL - 1))))
+    assert sum(x << (LB * i) for i, x in enumerate(c)) == k * Q
+    assert all(x < (1 << 32) for x in c)
+    return c, max(-(-x // MASK) for x in c), (k * Q) // (2 * Q) + 1   # value < that 2q, strictly
+
+
 def leaf_sop(K):
     A = lambda p, i: 28 * p + i
     B = lambda p, i: 28 * p + 14 + i

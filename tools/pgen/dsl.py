@@ -32,6 +32,38 @@ for _ub in range(1, gen_fl.U_MAX_SUB + 1):
     SUBC[_ub], SUBCU[_ub] = gen_fl.sub_constant(_ub)
 U_MAX = 16
 COL_BOUND = 17
+# Value bounds (Val.vb, in units of 2q) are tracked apart from limb bounds (Val.u):
+# a Montgomery product of sum a_i b_i is < 2q whenever sum vb_a vb_b 4q^2 < q 2^392,
+# i.e. sum vb_a vb_b < 2^392 / 4q ~ 630 (VB_PROD below keeps a margin), whatever
+# the limb bounds (those only guard the 64-bit columns).  So a sum that only has
+# to feed products needs its LIMBS brought back below 2^28 ("norm": a carry pass,
+# 39 instructions), not its value below 2q ("red": quotient estimate + signed
+# k q subtraction, 62 instructions).
+VB_PROD = 600
+VB_RED = 64        # red's quotient estimate needs the value below 2^388
+VN = int(os.environ.get("PGEN_VN", "6"))   # norm instead of red while vb <= VN
+
+
+def _val_of(limbs):
+    return sum(int(x) << (LB * i) for i, x in enumerate(limbs))
+
+
+class _SubTables(dict):
+    """SUBC[ub] (int: the classic tables, subtrahend bounds u = vb = ub) and
+    SUBC[(u, vb)] (norm programs: a subtrahend of limb bound u whose value bound
+    vb exceeds u), built on demand; SUBCL / SUBCV: limb / value bound of C"""
+    def __missing__(self, key):
+        c, ul, uv = gen_fl.sub_constant2(*key)
+        self[key] = c
+        SUBCL[key], SUBCV[key] = ul, uv
+        return c
+
+
+SUBCL, SUBCV = {}, {}
+SUBC = _SubTables(SUBC)
+for _ub in list(SUBC):
+    _c, SUBCL[_ub], SUBCV[_ub] = gen_fl.sub_constant2(_ub, _ub)
+    assert _c == SUBC[_ub]
 
 
 def to_mont_limbs(x):
@@ -48,13 +80,15 @@ class Val:
     double-width unreduced product ("wide" value, see Prog.wsop): only its
     limb bound u is tracked here, the value bound of the pair is tracked by
     the code that builds it (tower.py Wide)."""
-    __slots__ = ("id", "u", "half")
+    __slots__ = ("id", "u", "half", "vb")
 
-    def __init__(self, id_, u, half=False):
+    def __init__(self, id_, u, half=False, vb=None):
         self.id, self.u, self.half = id_, u, half
+        self.vb = u if vb is None else vb     # value < vb 2q (full values)
 
     def __repr__(self):
-        return "v%d/u%d%s" % (self.id, self.u, "h" if self.half else "")
+        return "v%d/u%d%s%s" % (self.id, self.u, "" if self.vb == self.u else "/vb%d" % self.vb,
+                                "h" if self.half else "")
 
 
 class Op:
@@ -90,14 +124,16 @@ class If:
 
 
 class Var:
-    def __init__(self, name, u, home):
+    def __init__(self, name, u, home, vb=None):
         self.name, self.u, self.home = name, u, home
+        self.vb = u if vb is None else vb
 
 
 class Prog:
-    def __init__(self, name, lanes=1):
+    def __init__(self, name, lanes=1, use_norm=False):
         self.name = name
         self.lanes = lanes      # 2: a lane pair shares each pairing (tower2.py)
+        self.use_norm = use_norm  # red() may carry-normalize (see VB_PROD)
         self.root = Block()
         self.cur = self.root
         self.nval = 0
@@ -106,15 +142,16 @@ class Prog:
         self.stack = []
 
     # ---- plumbing ----
-    def _val(self, u, half=False):
+    def _val(self, u, half=False, vb=None):
         assert 1 <= u <= U_MAX, "bound %d out of range" % u
-        v = Val(self.nval, u, half)
+        v = Val(self.nval, u, half, vb)
+        assert half or 1 <= v.vb <= VB_RED * 16, "value bound %d out of range" % v.vb
         self.nval += 1
         return v
 
-    def _op(self, kind, srcs, u, imm=None):
+    def _op(self, kind, srcs, u, imm=None, vb=None):
         half = any(x.half for x in srcs) and kind in ("add", "csub", "getvar")
-        v = self._val(u, half) if u else None
+        v = self._val(u, half, vb) if u else None
         self.cur.items.append(Op(kind, v, list(srcs), imm))
         return v
 
@@ -126,16 +163,19 @@ class Prog:
     def mul(self, a, b):
         self._full(a, b)
         assert a.u * b.u <= COL_BOUND, "mul bound %d*%d" % (a.u, b.u)
+        assert a.vb * b.vb <= VB_PROD, "mul value bound %d*%d" % (a.vb, b.vb)
         return self._op("sop", [a, b], 1)
 
     def sop(self, a, b, c, d):
         self._full(a, b, c, d)
         assert a.u * b.u + c.u * d.u <= COL_BOUND, "sop bound %d*%d+%d*%d" % (a.u, b.u, c.u, d.u)
+        assert a.vb * b.vb + c.vb * d.vb <= VB_PROD, "sop value bound"
         return self._op("sop", [a, b, c, d], 1)
 
     def sqr(self, a):
         self._full(a)
         assert a.u <= 3, "sqr bound %d" % a.u
+        assert a.vb * a.vb <= VB_PROD, "sqr value bound %d" % a.vb
         return self._op("sqr", [a], 1)
 
     def inv(self, a):
@@ -154,6 +194,7 @@ class Prog:
         self._full(*args)
         assert len(args) % 2 == 0 and args
         assert sum(a.u * b.u for a, b in zip(args[0::2], args[1::2])) <= COL_BOUND, "wsop bound"
+        assert sum(a.vb * b.vb for a, b in zip(args[0::2], args[1::2])) <= VB_PROD, "wsop value bound"
         lo, hi = self._val(1, True), self._val(1, True)
         self.cur.items.append(Op("wsop", lo, list(args), dst2=hi))
         return lo, hi
@@ -177,45 +218,70 @@ class Prog:
         return self._op("wred", [lo, hi], u)
 
     def add(self, a, b):
-        return self._op("add", [a, b], a.u + b.u)
+        return self._op("add", [a, b], a.u + b.u, vb=None if a.half else a.vb + b.vb)
 
     def dbl(self, a):
         return self.add(a, a)
 
+    def sub_key(self, b):
+        """SUBC table for subtrahend b: limbs 0..12 need C_i >= b.u MASK, the top
+        limb (< value / 2^364 < vb 2^18) needs C_13 >= vb 2^18"""
+        if not self.use_norm or b.vb <= b.u:
+            assert b.u in SUBCU, "subtrahend bound %d" % b.u
+            return b.u
+        return (b.u, b.vb)
+
+    def sub_bounds(self, key):
+        """(limb bound, value bound) of the constant C of table `key`"""
+        SUBC[key]
+        if not self.use_norm:
+            return SUBCU[key], SUBCU[key]
+        return SUBCL[key], SUBCV[key]
+
+    def neg_u(self, b):
+        return self.sub_bounds(self.sub_key(b))[0]
+
     def sub(self, a, b):
         self._full(a, b)
-        assert b.u in SUBCU, "sub subtrahend bound %d" % b.u
-        return self._op("sub", [a, b], a.u + SUBCU[b.u], imm=b.u)
+        key = self.sub_key(b)
+        cu, cv = self.sub_bounds(key)
+        return self._op("sub", [a, b], a.u + cu, imm=key, vb=None if not self.use_norm else a.vb + cv)
 
     def neg(self, b):
         self._full(b)
-        assert b.u in SUBCU, "neg bound %d" % b.u
-        return self._cse("neg", [b], SUBCU[b.u], imm=b.u)
+        key = self.sub_key(b)
+        cu, cv = self.sub_bounds(key)
+        return self._cse("neg", [b], cu, imm=key, vb=None if not self.use_norm else cv)
 
     def red(self, a):
+        """bring a to limb bound 1: a carry pass ("norm", value unchanged) while
+        the value bound stays small, else the full reduction (value < 2q)"""
         self._full(a)
-        if a.u == 1:
+        if a.u == 1 and a.vb <= (VN if self.use_norm else 1):
             return a
-        return self._cse("red", [a], 1)
+        if self.use_norm and a.u <= 15 and a.vb <= VN:
+            return self._cse("norm", [a], 1, vb=a.vb)
+        assert a.vb <= VB_RED, "red value bound %d" % a.vb
+        return self._cse("red", [a], 1, vb=1)
 
-    def _cse(self, kind, srcs, u, imm=None):
+    def _cse(self, kind, srcs, u, imm=None, vb=None):
         """pure ops on the same operands in the same block are computed once"""
         memo = self.cur.__dict__.setdefault("memo", {})
         key = (kind, tuple(v.id for v in srcs), imm)
         if key not in memo:
-            memo[key] = self._op(kind, srcs, u, imm)
+            memo[key] = self._op(kind, srcs, u, imm, vb)
         return memo[key]
 
     # ---- lane-pair ops (two-lane programs) ----
     def swap(self, a):
         """the partner lane's value (v_mov_b32_dpp quad_perm:[1,0,3,2])"""
         assert self.lanes == 2
-        return self._cse("swap", [a], a.u)
+        return self._cse("swap", [a], a.u, vb=a.vb)
 
     def sel(self, a, b):
         """lane 0 takes a, lane 1 takes b"""
         assert self.lanes == 2
-        return self._cse("sel", [a, b], max(a.u, b.u))
+        return self._cse("sel", [a, b], max(a.u, b.u), vb=max(a.vb, b.vb))
 
     def const(self, x):
         """field element x (plain integer) as a canonical Fl constant"""
@@ -226,13 +292,21 @@ class Prog:
 
     # ---- state ----
     def var(self, name, u=1, home=None):
-        self.vars[name] = Var(name, u, home)
+        # under norm a variable may hold a carry-normalized value (bound VN;
+        # PGEN_VARVB overrides it for A/B); set() fully reduces anything larger
+        vb = int(os.environ.get("PGEN_VARVB", str(VN)))
+        self.vars[name] = Var(name, u, home, max(u, vb) if self.use_norm else u)
 
     def get(self, name):
-        return self._op("getvar", [], self.vars[name].u, imm=name)
+        var = self.vars[name]
+        return self._op("getvar", [], var.u, imm=name, vb=var.vb)
 
     def set(self, name, v):
         assert v.u <= self.vars[name].u, "setvar %s: bound %d > %d" % (name, v.u, self.vars[name].u)
+        if not v.half and v.vb > self.vars[name].vb:
+            assert v.vb <= VB_RED
+            v = self._cse("red", [v], 1, vb=1)
+        assert v.half or v.vb <= self.vars[name].vb, "setvar %s: value bound %d" % (name, v.vb)
         self.cur.items.append(Op("setvar", None, [v], imm=name))
 
     # ---- cooperative macro operands (coop.py): value slots addressed by
@@ -320,9 +394,10 @@ class Stats:
         self.counts[k] = self.counts.get(k, 0) + n
 
 
-def _check(limbs, u, what, half=False):
+def _check(limbs, u, what, half=False, vb=None):
     assert all(0 <= x <= u * MASK for x in limbs), "%s: limb bound u=%d violated" % (what, u)
-    assert half or val_of(limbs) < u * 2 * Q, "%s: value bound u=%d violated" % (what, u)
+    vb = u if vb is None else vb
+    assert half or val_of(limbs) < vb * 2 * Q, "%s: value bound vb=%d violated" % (what, vb)
 
 
 def wide_product(pairs):
@@ -390,6 +465,20 @@ def mont_sop(pairs):
     return tuple(gen_fl.limbs(out))
 
 
+def norm_limbs(x):
+    """the emitted carry pass: limbs 0..12 below 2^28, the value unchanged"""
+    r, c = [], 0
+    for i in range(NL - 1):
+        acc = x[i] + c
+        assert acc < (1 << 32)
+        r.append(acc & MASK)
+        c = acc >> 28
+    acc = x[NL - 1] + c
+    assert acc < (1 << 32)
+    r.append(acc)
+    return tuple(r)
+
+
 def red_limbs(x):
     p1 = x[12] * KQ
     p2 = x[13] * KQ
@@ -445,6 +534,8 @@ def evaluate(prog, inputs, stats=None, trace=None):
             return tuple(ci - b for ci, b in zip(c, s[0]))
         if k == "red":
             return red_limbs(s[0])
+        if k == "norm":
+            return norm_limbs(s[0])
         if k == "csub":
             return tuple(a + ci - b for a, ci, b in zip(s[0], op.imm, s[1]))
         if k == "wred":
@@ -505,7 +596,7 @@ def evaluate(prog, inputs, stats=None, trace=None):
         else:
             r = [lane_op(k, op, [x[ln] for x in s]) for ln in range(L)]
         for ln in range(L):
-            _check(r[ln], op.dst.u, repr(op), op.dst.half)
+            _check(r[ln], op.dst.u, repr(op), op.dst.half, op.dst.vb)
         env[op.dst.id] = r
         if trace is not None:
             trace.append((op.dst.id, r[0] if L == 1 else tuple(r), op))

@@ -87,8 +87,19 @@ STORAGE = {1: (17, 18, int(os.environ.get("PGEN_NL", 11))),  # one wave per SIMD
            2: (17, 0, 5)}       # two waves per SIMD: 256 VGPR, no AGPR, 20 KB LDS
 
 
+def plan_ctab(hist):
+    """the SGPR constant tables for a program, from a first emission's counts,
+    by instructions saved per SGPR: a full table costs 14 SGPRs; a wide constant
+    with equal limbs 0..12 costs one SGPR for its top limb plus one per distinct
+    repeated limb value"""
+    def uni(k, c):
+        return k[0] == "csub" and all(x == c[0] for x in c[:NL - 1])
+    items = sorted(hist.items(), key=lambda kv: -kv[1] * (7 if uni(*kv[0]) else 1))
+    return [kc for kc, n in items if n >= 1]
+
+
 class Emitter:
-    def __init__(self, prog, cfg):
+    def __init__(self, prog, cfg, ctab_plan=None):
         self.prog = prog
         self.cfg = cfg          # kernel config (kernels.py): loads / stores / flags
         self.code = []
@@ -119,12 +130,30 @@ class Emitter:
         self.vm_owed_seq = 0
         self.ctab = {}               # constant key -> ("full", sgpr base) | ("uni", sgpr of limbs 0..12)
         self.ctab_init = []          # (sgpr, value) loaded by the prologue
+        self.sub_hist = {}           # (constant key, limbs) -> dynamic count (plan_ctab)
         self.ctab_next = S_CTAB
+        self.ctab_fixed = False
         if os.environ.get("PGEN_SAD", "1") == "1":
-            for ub in CTAB_FULL:
-                self.ctab[("sub", ub)] = ("full", self.ctab_next)
-                self.ctab_init += [(self.ctab_next + i, SUBC[ub][i]) for i in range(NL)]
+            shared = {}          # repeated limb value -> its SGPR
+            for key, c in (ctab_plan if ctab_plan is not None else [(("sub", ub), SUBC[ub]) for ub in CTAB_FULL]):
+                if key[0] == "csub" and all(x == c[0] for x in c[:NL - 1]):
+                    need = 1 + (c[0] not in shared)
+                    if self.ctab_next + need > S_CTAB_END:
+                        continue
+                    if c[0] not in shared:
+                        shared[c[0]] = self.ctab_next
+                        self.ctab_init.append((self.ctab_next, c[0]))
+                        self.ctab_next += 1
+                    self.ctab[key] = ("uni", shared[c[0]], self.ctab_next)
+                    self.ctab_init.append((self.ctab_next, c[NL - 1]))
+                    self.ctab_next += 1
+                    continue
+                if self.ctab_next + NL > S_CTAB_END:
+                    continue
+                self.ctab[key] = ("full", self.ctab_next)
+                self.ctab_init += [(self.ctab_next + i, v) for i, v in enumerate(c)]
                 self.ctab_next += NL
+            self.ctab_fixed = ctab_plan is not None
 
     # ---------------- emission helpers ----------------
     VMEM = ("global_load_dwordx2", "global_load_dword", "global_store_dwordx2", "global_store_byte",
@@ -132,6 +161,7 @@ class Emitter:
 
     def i(self, *t):
         self.code.append(t)
+        self.dyn_instr = getattr(self, "dyn_instr", 0) + self.weight   # loop-weighted estimate
         m = t[0]
         if m in self.VMEM:
             self.vm_issued += 1
@@ -430,29 +460,44 @@ class Emitter:
             else:
                 self.i("v_mov_b32", d + i, ACC)
 
+    def emit_norm(self, x, d):
+        """carry pass: limbs 0..12 below 2^28, value unchanged (dsl.norm_limbs);
+        carry in v1, running sum in v0 (x may equal d: each limb is read first)"""
+        self.i("v_lshrrev_b32", ACC + 1, K(28), x)
+        self.i("v_and_b32", d, K(MASK), x)
+        for i in range(1, NL - 1):
+            self.i("v_add_u32", ACC, x + i, ACC + 1)
+            self.i("v_and_b32", d + i, K(MASK), ACC)
+            self.i("v_lshrrev_b32", ACC + 1, K(28), ACC)
+        self.i("v_add_u32", d + NL - 1, x + NL - 1, ACC + 1)
+
     def emit_add(self, a, b, d):
         for i in range(NL):
             self.i("v_add_u32", d + i, a + i, b + i)
 
     def ctab_reg(self, key, c):
-        """SGPR of limb i of constant c (or None): full tables for SUBC[1], SUBC[2];
-        constants with equal limbs 0..12 take two SGPRs while the area lasts"""
+        """SGPR of limb i of constant c (or None): the tables planned by plan_ctab
+        (or full SUBC[1], SUBC[2] tables, then constants with equal limbs 0..12,
+        two SGPRs each, while the area lasts)"""
+        hk = (key, tuple(c))
+        self.sub_hist[hk] = self.sub_hist.get(hk, 0) + self.weight
         if os.environ.get("PGEN_SAD", "1") != "1":
             return None
         e = self.ctab.get(key)
-        if e is None and all(x == c[0] for x in c[:NL - 1]) and self.ctab_next + 2 <= S_CTAB_END:
-            e = self.ctab[key] = ("uni", self.ctab_next)
+        if (e is None and not self.ctab_fixed and all(x == c[0] for x in c[:NL - 1])
+                and self.ctab_next + 2 <= S_CTAB_END):
+            e = self.ctab[key] = ("uni", self.ctab_next, self.ctab_next + 1)
             self.ctab_init += [(self.ctab_next, c[0]), (self.ctab_next + 1, c[NL - 1])]
             self.ctab_next += 2
         if e is None:
             return None
         if e[0] == "full":
             return lambda i: S(e[1] + i)
-        return lambda i: S(e[1] if i < NL - 1 else e[1] + 1)
+        return lambda i: S(e[1] if i < NL - 1 else e[2])
 
     def emit_sub(self, a, b, d, ub):
         c = SUBC[ub]
-        r = self.ctab_reg(("sub", ub), c)
+        r = self.ctab_reg(("sub", ub), tuple(c))
         if r is not None:
             for i in range(NL):
                 self.i("v_sad_u32", d + i, r(i), b + i, a + i)
@@ -782,6 +827,8 @@ class Emitter:
             self.emit_sop([(base[0], base[0])], d)
         elif k == "red":
             self.emit_red(base[0], d)
+        elif k == "norm":
+            self.emit_norm(base[0], d)
         elif k == "add":
             self.emit_add(base[0], base[1], d)
         elif k == "sub":
@@ -829,7 +876,7 @@ class Emitter:
                 self.kill(dvs)
 
     # ---------------- prefetch ----------------
-    COST = {"sop": None, "sqr": 460, "red": 62, "add": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
+    COST = {"sop": None, "sqr": 460, "red": 62, "norm": 39, "add": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
             "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14}
     # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
     AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}

@@ -214,8 +214,15 @@ class FinalExpCfg2(FinalExpCfg):
 
 def build(prog, cfg, debug=False):
     """allocate + emit: returns (code list, emitter)"""
-    from emit import Emitter
-    em = Emitter(prog, cfg)
+    import os
+    from emit import Emitter, plan_ctab
+    plan = None
+    if os.environ.get("PGEN_SAD", "1") == "1":
+        # first pass: which subtraction constants the program uses, how often
+        em0 = Emitter(prog, cfg)
+        em0.run_block(prog.root, top=True)
+        plan = plan_ctab(em0.sub_hist)
+    em = Emitter(prog, cfg, plan)
     em.debug = debug
     em.run_block(prog.root, top=True)
     body = em.code

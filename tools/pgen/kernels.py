@@ -9,11 +9,19 @@
 Infinity inputs (miller loop -> one) and f == 0 (final exp -> None) are
 lane selects done by the emitted prologue/epilogue, outside the DSL.
 """
+import os
+
 from dsl import Prog
 from tower import Tower, TowerLazy, TowerLazySq, X_ABS, declare12, get12, set12
 from tower2 import Tower2
 
 ML_MASK = (X_ABS >> 1) & ((1 << 62) - 1)  # bits 61..0 below the leading one of |x| >> 1
+
+
+def _norm(lanes):
+    """carry-normalize instead of reducing where value bounds allow (dsl.VB_PROD);
+    one-lane kernels only (PGEN_NORM=0: the full reduction everywhere, A/B)"""
+    return lanes == 1 and os.environ.get("PGEN_NORM", "1") == "1"
 
 
 def doubling_step(T, r):
@@ -73,7 +81,7 @@ ML_HOMES = {"px": "L", "py": "L", "qx0": "M", "qx1": "M", "qy0": "M", "qy1": "M"
 
 def miller_loop_prog(homes=None, lanes=1, lazy=False):
     homes = dict(ML_HOMES, **(homes or {}))
-    p = Prog("miller_loop" if lanes == 1 else "miller_loop2", lanes)
+    p = Prog("miller_loop" if lanes == 1 else "miller_loop2", lanes, use_norm=_norm(lanes))
     T = (TowerLazy(p) if lazy else Tower(p)) if lanes == 1 else Tower2(p)
     V = _Vars(p, lanes)
     for n in ("px", "py"):
@@ -189,7 +197,8 @@ def exp_by_x(p, T, V, f, x, tag):
 def final_exp_prog(lanes=1, lazy=False, tower_cls=None):
     """lazy: False (Tower), True (TowerLazy) or "sq" (TowerLazySq);
     tower_cls overrides the tower class (coop.py: inversion as one op)"""
-    p = Prog("final_exp" if lanes == 1 else "final_exp2", lanes)
+    p = Prog("final_exp" if lanes == 1 else "final_exp2", lanes,
+             use_norm=_norm(lanes) and tower_cls is None)
     if tower_cls is not None:
         T = tower_cls(p)
     elif lanes == 2:

@@ -32,6 +32,10 @@ class Tower:
     def red2(self, a): return (self.p.red(a[0]), self.p.red(a[1]))
     def u2(self, a): return max(a[0].u, a[1].u)
 
+    def nu(self, x):
+        """limb bound of neg(x) (dsl.Prog.sub_key / sub_bounds)"""
+        return self.p.neg_u(x)
+
     def xi(self, a):  # fq2.rs:41-45, * (u + 1)
         return (self.p.sub(a[0], a[1]), self.p.add(a[0], a[1]))
 
@@ -40,8 +44,7 @@ class Tower:
 
     def mul2(self, a, b):  # fq2.rs:123-136, schoolbook, one reduction per coordinate
         p = self.p
-        A, B = self.u2(a), self.u2(b)
-        if SUBCU[A] * B <= A * SUBCU[B]:
+        if self.nu(a[1]) * b[1].u <= a[1].u * self.nu(b[1]):
             c0 = p.sop(a[0], b[0], p.neg(a[1]), b[1])
         else:
             c0 = p.sop(a[0], b[0], a[1], p.neg(b[1]))
@@ -50,8 +53,7 @@ class Tower:
 
     def sqr2(self, a):  # fq2.rs:87-101
         p = self.p
-        A = self.u2(a)
-        if 2 * A * (A + SUBCU[A]) <= 17:
+        if (a[0].u + a[1].u) * (a[0].u + self.nu(a[1])) <= 17:
             c0 = p.mul(p.add(a[0], a[1]), p.sub(a[0], a[1]))
         else:
             c0 = p.sop(a[0], a[0], p.neg(a[1]), a[1])
@@ -299,7 +301,7 @@ class TowerLazy(Tower):
     # ---- wide Fq ----
     def w_sop(self, *args):
         lo, hi = self.p.wsop(*args)
-        vb = sum((a.u * 2 * Q) * (b.u * 2 * Q) for a, b in zip(args[0::2], args[1::2]))
+        vb = sum((a.vb * 2 * Q) * (b.vb * 2 * Q) for a, b in zip(args[0::2], args[1::2]))
         return Wide(lo, hi, vb, (vb - 1) >> 756)
 
     def w_norm(self, a):
@@ -346,8 +348,7 @@ class TowerLazy(Tower):
             p1 = self.w_sop(a[1], b[1])
             p2 = self.w_sop(p.add(a[0], a[1]), p.add(b[0], b[1]))
             return (self.w_sub(p0, p1), self.w_sub(p2, self.w_add(p0, p1)))
-        A, B = max(ua0, ua1), max(ub0, ub1)
-        if SUBCU[A] * B <= A * SUBCU[B]:
+        if self.nu(a[1]) * ub1 <= ua1 * self.nu(b[1]):
             c0 = self.w_sop(a[0], b[0], p.neg(a[1]), b[1])
         else:
             c0 = self.w_sop(a[0], b[0], a[1], p.neg(b[1]))
@@ -355,8 +356,7 @@ class TowerLazy(Tower):
 
     def w_sqr2(self, a):
         p = self.p
-        A = self.u2(a)
-        if 2 * A * (A + SUBCU[A]) <= 17:
+        if (a[0].u + a[1].u) * (a[0].u + self.nu(a[1])) <= 17:
             c0 = self.w_sop(p.add(a[0], a[1]), p.sub(a[0], a[1]))
         else:
             c0 = self.w_sop(a[0], a[0], p.neg(a[1]), a[1])
