@@ -344,6 +344,67 @@ class Prog:
         return _Ctx(self, If(mask, loop))
 
 
+def fuse_adds(prog):
+    """Rewrite, per block, adds whose operands are single-use adds / doublings of
+    the same block (values and bounds stay those of the outer op; the inner
+    value disappears):
+      add(x, x) of a single-use shl(y, s) or add(y, y)  -> shl(y, s + 1)   v_lshlrev_b32
+      add(shl(x, s), y) / add(add(x, x), y)             -> shladd(x, y; s) v_lshl_add_u32
+      add(add(a, b), c)                                 -> add3(a, b, c)   v_add3_u32
+    Returns the number of rewrites."""
+    n = 0
+
+    def walk(block):
+        nonlocal n
+        uses, defs = {}, {}
+        for it in block.items:
+            if isinstance(it, (Loop, If)):
+                walk(it.body)
+                continue
+            for v in it.srcs:
+                uses[v.id] = uses.get(v.id, 0) + 1
+            if it.dst is not None:
+                defs[it.dst.id] = it
+        dead = set()
+
+        def single(v, kinds):
+            d = defs.get(v.id)
+            if d is None or d.kind not in kinds or id(d) in dead:
+                return None
+            # a doubling add(x, x) reads v twice
+            return d if uses.get(v.id) == (2 if it.srcs[0].id == it.srcs[1].id else 1) else None
+
+        for it in block.items:
+            if isinstance(it, (Loop, If)) or it.kind != "add":
+                continue
+            a, b = it.srcs
+            if a.id == b.id:                        # a doubling
+                d = single(a, ("add", "shl"))
+                if d is not None and (d.kind == "shl" or d.srcs[0].id == d.srcs[1].id):
+                    sh = d.imm if d.kind == "shl" else 1
+                    it.kind, it.srcs, it.imm = "shl", [d.srcs[0]], sh + 1
+                    dead.add(id(d))
+                    n += 1
+                continue
+            for j, v in enumerate((a, b)):
+                other = it.srcs[1 - j]
+                d = single(v, ("add", "shl"))
+                if d is None:
+                    continue
+                if d.kind == "shl" or d.srcs[0].id == d.srcs[1].id:
+                    sh = d.imm if d.kind == "shl" else 1
+                    it.kind, it.srcs, it.imm = "shladd", [d.srcs[0], other], sh
+                else:
+                    it.kind, it.srcs = "add3", [d.srcs[0], d.srcs[1], other]
+                dead.add(id(d))
+                n += 1
+                break
+        block.items = [it for it in block.items if id(it) not in dead]
+
+    walk(prog.root)
+    return n
+
+
 def check_scopes(prog):
     """Only named variables cross into loop / branch bodies: every Val used in
     a body is defined in that same body (the allocator relies on it)."""
@@ -526,6 +587,12 @@ def evaluate(prog, inputs, stats=None, trace=None):
             return mont_sop([(s[0], s[0])])
         if k == "add":
             return tuple(a + b for a, b in zip(*s))
+        if k == "add3":
+            return tuple(a + b + c for a, b, c in zip(*s))
+        if k == "shladd":
+            return tuple((a << op.imm) + b for a, b in zip(*s))
+        if k == "shl":
+            return tuple(a << op.imm for a in s[0])
         if k == "sub":
             c = SUBC[op.imm]
             return tuple(a + ci - b for a, ci, b in zip(s[0], c, s[1]))

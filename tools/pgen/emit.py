@@ -831,6 +831,15 @@ class Emitter:
             self.emit_norm(base[0], d)
         elif k == "add":
             self.emit_add(base[0], base[1], d)
+        elif k == "add3":
+            for i in range(NL):
+                self.i("v_add3_u32", d + i, base[0] + i, base[1] + i, base[2] + i)
+        elif k == "shladd":
+            for i in range(NL):
+                self.i("v_lshl_add_u32", d + i, base[0] + i, K(op.imm), base[1] + i)
+        elif k == "shl":
+            for i in range(NL):
+                self.i("v_lshlrev_b32", d + i, K(op.imm), base[0] + i)
         elif k == "sub":
             self.emit_sub(base[0], base[1], d, op.imm)
         elif k == "csub":
@@ -876,7 +885,7 @@ class Emitter:
                 self.kill(dvs)
 
     # ---------------- prefetch ----------------
-    COST = {"sop": None, "sqr": 460, "red": 62, "norm": 39, "add": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
+    COST = {"sop": None, "sqr": 460, "red": 62, "norm": 39, "add": 14, "add3": 14, "shladd": 14, "shl": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
             "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14}
     # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
     AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}

@@ -216,6 +216,9 @@ def build(prog, cfg, debug=False):
     """allocate + emit: returns (code list, emitter)"""
     import os
     from emit import Emitter, plan_ctab
+    from dsl import fuse_adds
+    if prog.lanes == 1 and prog.use_norm and os.environ.get("PGEN_FUSE", "1") == "1":
+        fuse_adds(prog)
     plan = None
     if os.environ.get("PGEN_SAD", "1") == "1":
         # first pass: which subtraction constants the program uses, how often

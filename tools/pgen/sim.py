@@ -174,6 +174,8 @@ class Sim:
             wr(a[0], rd(a[1]) + rd(a[2]))
         elif m == "v_sub_u32":
             wr(a[0], rd(a[1]) - rd(a[2]))
+        elif m == "v_add3_u32":
+            wr(a[0], rd(a[1]) + rd(a[2]) + rd(a[3]))
         elif m == "v_sad_u32":   # |s0 - s1| + s2; the emitter relies on s0 >= s1
             x, y = rd(a[1]), rd(a[2])
             assert x >= y, "v_sad_u32: subtraction constant below the subtrahend limb"
