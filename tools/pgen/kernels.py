@@ -148,9 +148,12 @@ class _Vars:
             p.set(n + "0", v)
 
     def declare12(self, prefix, home=None):
+        """home: one storage tier for all 12 coordinates, or a 12-character string
+        of tiers per coordinate (e.g. "AAAAAAMMMMMM")"""
         for i in range(6):
             for c in (0, 1):
-                self.p.var("%s%d_%d" % (prefix, i, c), 1, home)
+                h = home[2 * i + c] if home is not None and len(home) == 12 else home
+                self.p.var("%s%d_%d" % (prefix, i, c), 1, h)
 
     def get12(self, prefix):
         xs = [self.get2("%s%d_" % (prefix, i)) for i in range(6)]
@@ -182,8 +185,10 @@ def exp_by_x(p, T, V, f, x, tag):
     """exp_by_x (mod.rs:116-121): f^|x| by square-and-multiply (lib.rs:306-324)
     with cyclotomic squarings, then conjugation (x < 0)"""
     base, res = "eb%s_" % tag, "er%s_" % tag
-    V.declare12(base, "M")
-    V.declare12(res, "A")
+    # the base f: 8 coordinates in AGPRs, 4 in the HBM workspace (FE 11.37 -> 11.11 ms
+    # against all 12 in HBM, profiles/r02_eb_home_ab.txt)
+    V.declare12(base, os.environ.get("PGEN_EB_HOME", "AAAAAAAAMMMM"))
+    V.declare12(res, os.environ.get("PGEN_ER_HOME", "A"))
     V.set12(base, f)
     V.set12(res, f)
     top = x.bit_length() - 1
