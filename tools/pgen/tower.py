@@ -8,6 +8,8 @@ next operation's bound check needs it.
 Element encodings: Fq2 = (c0, c1) of Val; Fq6 = 3-tuple of Fq2;
 Fq12 = (Fq6, Fq6).
 """
+import os
+
 from dsl import SUBCU, Q
 
 X_ABS = 0xD201000000010000  # |x|, x < 0 (mod.rs:23-25)
@@ -186,7 +188,13 @@ class Tower:
 
     # ---------------- inversion ----------------
     def inv_fq(self, a, tag):
-        """a^(q-2) (Fermat; the same value as fq.rs:849-902's Euclid for a != 0)"""
+        """a^(q-2) (Fermat; the same value as fq.rs:849-902's Euclid for a != 0):
+        a sliding window of 4 bits over the constant exponent -- 8 odd powers,
+        then 380 squarings and 78 multiplications (463 products against 608 for
+        bitwise square-and-multiply); PGEN_INV_W=0 selects the bitwise form"""
+        W = int(os.environ.get("PGEN_INV_W", "4"))
+        if W:
+            return self._inv_fq_window(a, tag, W)
         p = self.p
         e = Q - 2
         assert e.bit_length() == 381
@@ -203,6 +211,42 @@ class Tower:
                 p.set(vr, p.sqr(p.get(vr)))
                 with p.if_bit(mask, L):
                     p.set(vr, p.mul(p.get(vr), p.get(va)))
+        return p.get(vr)
+
+    def _inv_fq_window(self, a, tag, W):
+        p = self.p
+        bits = bin(Q - 2)[2:]
+        wins, i, zeros = [], 0, 0          # (squarings before the window's multiply, odd value)
+        while i < len(bits):
+            if bits[i] == "0":
+                zeros += 1
+                i += 1
+                continue
+            j = min(i + W, len(bits))
+            while bits[j - 1] == "0":
+                j -= 1
+            wins.append((zeros + (j - i), int(bits[i:j], 2)))
+            zeros, i = 0, j
+        tail = zeros
+        names = ["inv_t%d_%s" % (k, tag) for k in range(1 << (W - 1))]   # a^(2k+1)
+        for n in names:
+            p.var(n, 1, os.environ.get("PGEN_INV_HOME", "A"))
+        vr = "inv_r_" + tag
+        p.var(vr)
+        a2 = p.sqr(a)
+        t = a
+        for k, n in enumerate(names):
+            if k:
+                t = p.mul(t, a2)
+            p.set(n, t)
+        p.set(vr, p.get(names[(wins[0][1] - 1) // 2]))
+        for nsq, val in wins[1:]:
+            with p.loop(nsq):
+                p.set(vr, p.sqr(p.get(vr)))
+            p.set(vr, p.mul(p.get(vr), p.get(names[(val - 1) // 2])))
+        if tail:
+            with p.loop(tail):
+                p.set(vr, p.sqr(p.get(vr)))
         return p.get(vr)
 
     def inv2(self, a, tag):  # fq2.rs:138-155
