@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) k_fq_mul_batch_fl(const uint64_t* __restr
     const F<1> xs = fl_split_shl8(x), ys = fl_split(y);
     F<1> z;
     fl_mul_leaf(z.w, xs.w, ys.w);
-    fq_store(out + 6 * i, fl_pack(fl_canon(z)));
+    fq_store(out + 6 * i, fl_pack_canon(z));
 }
 
 // Probe for config 2 (PA_FQ_VARIANT=9, not the product path): the same record
