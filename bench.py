@@ -38,6 +38,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # shader clocks per wave-instruction per SIMD at a sustained 2.39 GHz,
 # 1024 SIMDs x 64 lanes -> limb multiply-accumulates per second
 VALU_MAC_PEAK_T = 1024 * 64 / 5.13 * 2.39e9 / 1e12
+# issue ceiling of the one-wave-per-SIMD pairing kernels: one wave issues at most
+# one instruction per 4 clk (SQ: one ACTIVE_INST quad-cycle per instruction), at
+# the 2.33 GHz the chip holds under them (GRBM_GUI_ACTIVE, profiles/r02_cyc_probe.txt)
+ISSUE_PEAK_T = 1024 * 64 / 4 * 2.33e9 / 1e12
 FQ12_BYTES = 576
 G1A_BYTES, G2A_BYTES = 104, 200  # ABI records (coordinates + infinity flag + pad)
 # algorithmic HBM bytes per pairing, per kernel (DESIGN.md "Roofline")
@@ -612,6 +616,12 @@ def main():
                     "avg_launch_ms": round(dom_ms, 4),
                     "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS,
                             "bytes_per_unit": dom_bytes}}
+            instr = work["final_exp" if dom_name == "final_exponentiation" else "miller_loop"].get("instructions")
+            if instr:
+                rate = instr * n / (dom_ms * 1e-3) / 1e12
+                roof["issue"] = {"achieved": round(rate, 3), "peak": round(ISSUE_PEAK_T, 3),
+                                 "unit": "T lane-instructions/s (one wave per SIMD)", "frac": rate / ISSUE_PEAK_T,
+                                 "instructions_per_unit": instr}
         if args.workload == "wnaf" and dom_name == "g1_fixed_base_mul":
             # VALU bound: each mixed addition (madd-2007-bl, ec.rs:446-526) is
             # 7 products + 4 squarings on the lazy 28-bit core (fl_gen.h

@@ -141,7 +141,10 @@ def write_work_json(outdir):
         prog = PROGRAMS[key]()[0]
         st = dsl.Stats()
         dsl.evaluate(prog, {k: rng.randrange(dsl.Q) for k in range(nin)}, st)
-        out[name] = {"limb_macs": macs(st.counts), "ops": st.counts}
+        em = PROGRAMS[key].cache["r"][5]
+        # instructions one lane executes (exact: the loop trip counts and branch
+        # masks are static, the emitter weights every instruction by them)
+        out[name] = {"limb_macs": macs(st.counts), "ops": st.counts, "instructions": round(em.dyn_instr)}
     with open(os.path.join(outdir, "pa_gen_work.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 
