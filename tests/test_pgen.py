@@ -126,3 +126,78 @@ def test_coop_schedules_replay_equal_dsl():
     macros, consts = coop.build_all()
     coop.check(macros, consts, trials=1)
     assert sum(len(m.records) for m in macros) < 200
+
+
+# ---- round 2: value bounds, carry normalization, add fusion, subtraction tables ----
+def test_subtraction_tables_dominate_subtrahends():
+    """SUBC[(u, v)]: a multiple of q whose limbs 0..12 are >= u (2^28 - 1) and whose
+    top limb covers any value below v 2q (top limb < v 2^18); its value bound is
+    strict (tools/gen_fl.py sub_constant2)"""
+    import gen_fl
+    for u in (1, 2, 3, 5):
+        for v in (1, 2, 6, 12):
+            c, ul, uv = gen_fl.sub_constant2(u, v)
+            val = dsl._val_of(c)
+            assert val % dsl.Q == 0
+            assert all(x >= u * dsl.MASK for x in c[:13]) and c[13] >= v << 18
+            assert val < uv * 2 * dsl.Q and all(x <= ul * dsl.MASK for x in c)
+            # the largest subtrahend of those bounds stays non-negative limb-wise
+            top = (v * 2 * dsl.Q - 1) >> (28 * 13)
+            assert c[13] >= min(top, u * dsl.MASK)
+
+
+def test_norm_keeps_value_and_limits_limbs():
+    r = random.Random(3)
+    for _ in range(200):
+        x = tuple(r.randrange(15 * dsl.MASK) for _ in range(13)) + (r.randrange(1 << 22),)
+        y = dsl.norm_limbs(x)
+        assert dsl._val_of(y) == dsl._val_of(x)
+        assert all(v <= dsl.MASK for v in y[:13])
+
+
+def test_products_reject_large_value_bounds():
+    p = dsl.Prog("t", use_norm=True)
+    a = p._op("const", [], 1, imm=tuple([0] * 14), vb=30)
+    with pytest.raises(AssertionError, match="value bound"):
+        p.mul(a, a)
+    b = p._op("const", [], 1, imm=tuple([0] * 14), vb=20)
+    p.mul(b, b)          # 400 <= VB_PROD
+
+
+def test_red_becomes_norm_only_for_small_value_bounds():
+    p = dsl.Prog("t", use_norm=True)
+    x = p._op("const", [], 1, imm=tuple([0] * 14))
+    s = p.add(p.add(x, x), x)                 # u = vb = 3
+    assert p.red(s).u == 1 and p.cur.items[-1].kind == "norm"
+    big = x
+    for _ in range(dsl.VN):
+        big = p.add(big, x)                   # vb = VN + 1
+    r = p.red(big)
+    assert p.cur.items[-1].kind == "red" and r.vb == 1
+    q = dsl.Prog("t")                         # coop / lane-pair programs: always the full reduction
+    y = q._op("const", [], 1, imm=tuple([0] * 14))
+    q.red(q.add(y, y))
+    assert q.cur.items[-1].kind == "red"
+
+
+def test_fuse_adds_preserves_values():
+    r = random.Random(5)
+    p = dsl.Prog("t", use_norm=True)
+    a, b, c, d = (p.load(k) for k in range(4))
+    t = p.add(a, b)
+    u = p.add(t, c)                            # add3
+    w = p.add(d, d)
+    w = p.add(w, w)                            # shl 2
+    z = p.add(w, u)                            # shladd
+    v = p.add(p.add(c, c), a)                  # shladd 1
+    for k, val in enumerate((u, z, v)):
+        p.store(k, p.red(val))
+    ins = {k: r.randrange(dsl.Q) for k in range(4)}
+    want = dsl.evaluate(p, ins)
+    n = dsl.fuse_adds(p)
+    kinds = [it.kind for it in p.root.items]
+    assert n >= 3 and "add3" in kinds and "shladd" in kinds
+    assert dsl.evaluate(p, ins) == want
+    Q = dsl.Q
+    assert want[0] == (ins[0] + ins[1] + ins[2]) % Q
+    assert want[1] == (4 * ins[3] + ins[0] + ins[1] + ins[2]) % Q
