@@ -180,6 +180,61 @@ PA_DEV bool sqrt(Fq2& r, const Fq2& a) {
     return true;
 }
 
+// Some square root of a in Fq2 (or false if a is not a square), for decoding:
+// point_from_x keeps the root whose sign matches the encoding flag, so any root
+// decodes to the same point.  Complex method for q = 3 mod 4: a = a0 + a1 u is
+// a square iff its norm n = a0^2 + a1^2 is one in Fq; with s = sqrt(n), one of
+// t = (a0 +- s) / 2 is a nonzero square x0^2 (unless a1 = 0), and
+// sqrt(a) = x0 + a1 / (2 x0) u.  Two or three Fq exponentiations instead of
+// fq2.rs:167-220's two Fq2 ones.  SqrtField::sqrt itself (k_sqrt) keeps the
+// reference's algorithm above.
+// 1/2 = (q + 1) / 2, Montgomery form (R = 2^384)
+__constant__ const uint64_t kHalfMont[6] = {0x1804000000015554ULL, 0x855000053ab00001ULL, 0x633cb57c253c276fULL,
+                                            0x6e22d1ec31ebb502ULL, 0xd3916126f2d14ca2ULL, 0x17fbb8571a006596ULL};
+PA_DEV bool sqrt_any(Fq2& r, const Fq2& a) {
+    if (is_zero(a)) {
+        zero(r);
+        return true;
+    }
+    Fq n, s, t, x0, x1;
+    {
+        Fq b;
+        fq_sqr(n, a.c0);
+        fq_sqr(b, a.c1);
+        fq_add(n, n, b);
+    }
+    if (!sqrt(s, n)) return false;
+    // t = (a0 + s) / 2: halve by a Montgomery product with 2^-1
+    Fq half;
+    fq_const(half, kHalfMont);
+    fq_add(t, a.c0, s);
+    fq_mul(t, t, half);
+    bool ok = sqrt(x0, t) && !fq_is_zero(x0);
+    if (!ok) {
+        fq_sub(t, a.c0, s);
+        fq_mul(t, t, half);
+        ok = sqrt(x0, t) && !fq_is_zero(x0);
+    }
+    if (!ok) {
+        // a1 = 0 and a0 not a square: sqrt(a0) = sqrt(-a0) u
+        if (!fq_is_zero(a.c1)) return false;
+        Fq m;
+        fq_neg(m, a.c0);
+        if (!sqrt(x1, m)) return false;
+        fq_zero(r.c0);
+        r.c1 = x1;
+        return true;
+    }
+    Fq d;
+    fq_add(d, x0, x0);
+    fq_inv(d, d);
+    fq_mul(x1, a.c1, d);
+    r.c0 = x0;
+    r.c1 = x1;
+    return true;
+}
+PA_DEV bool sqrt_any(Fq& r, const Fq& a) { return sqrt(r, a); }
+
 PA_DEV void coeff_b(Fq& b) { fq_const(b, kB); }
 PA_DEV void coeff_b(Fq2& b) {
     fq_const(b.c0, kB);
@@ -201,7 +256,7 @@ template <class F>
 PA_DEV bool point_from_x(Aff<F>& out, const F& x, bool greatest) {
     F rhs, y, negy;
     curve_rhs(rhs, x);
-    if (!sqrt(y, rhs)) return false;
+    if (!sqrt_any(y, rhs)) return false;
     neg(negy, y);
     out.x = x;
     out.y = ((cmp(y, negy) < 0) != greatest) ? y : negy;
