@@ -35,6 +35,7 @@ constexpr int kNormChunk = 8;         // points per lane in batch_normalization 
 
 // ---------------- batch_normalization ----------------
 __global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict__ v, size_t n) {
+    __builtin_amdgcn_s_setprio(2);   // latency-bound: ahead of a concurrent comb multiply's waves
     const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t begin = lane * kNormChunk;
     if (begin >= n) return;
@@ -93,6 +94,7 @@ __global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict_
 // T[i][d-1] = d * B_i (Jacobian), one lane per entry: double-and-add over d's 8 bits.
 __global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict__ bases, uint64_t* __restrict__ table_jac,
                                                      int e0, int e1) {
+    __builtin_amdgcn_s_setprio(2);   // table work of a later part runs beside the multiply
     const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= e1) return;
     const int i = e / kCombEntries, d = e % kCombEntries + 1;
@@ -111,6 +113,7 @@ __global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict_
 // representation (fl.h: 14 limbs, R = 2^392), 28 u32 per entry
 __global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table_fl,
                                                      int e0, int e1) {
+    __builtin_amdgcn_s_setprio(2);   // table work of a later part runs beside the multiply
     const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= e1) return;
     const F<1> x = fl_load(table_jac + (size_t)kG1Jac * e);
@@ -133,6 +136,9 @@ __global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict_
 __global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases,
                                                       int w0, int w1) {
     if (blockIdx.x != 0) return;
+    // the serial chain runs beside the (chip-filling) comb multiply of earlier
+    // parts: top issue priority on its SIMD, or it gets the multiply waves' leftovers
+    __builtin_amdgcn_s_setprio(3);
     const int lane = threadIdx.x;
     Jac<Fq> p0;
     load_jac(p0, w0 == 0 ? base : bases + kG1Jac * (w0 - 1));
@@ -266,58 +272,79 @@ hipError_t launch_g1_comb_mul(const uint64_t* table_fl, const uint64_t* scalars,
     return hipGetLastError();
 }
 
-// Table + multiply with the serial base chain overlapped: the table is built
-// in two window halves on a side stream; the multiply over the low half runs
-// on `stream` while the side stream is still doubling toward the high half's
-// bases.  Same result bits as launch_g1_comb_table + launch_g1_comb_mul.
+// Table + multiply with the serial base chain overlapped, in window parts: the
+// multiply over part p (accumulating into `out`) runs on `stream` while the
+// chain doubles toward later parts' bases and their table entries are built.
+// Same result bits as launch_g1_comb_table + launch_g1_comb_mul.
 hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
                                 uint64_t* table_fl, uint64_t* workspace, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
+    // two per-device side streams: `chain` runs the serial base chain part by
+    // part; `fill` turns each finished part's bases into its table entries
+    // (double-and-add, batch normalization, packing); the caller's stream
+    // multiplies part p while the chain and the table work on parts > p.
     static std::mutex mu;
-    static hipStream_t side[64] = {};
+    static hipStream_t side[64][2] = {};
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     {
         std::lock_guard<std::mutex> g(mu);
-        if (!side[dev] && (e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking)) != hipSuccess) return e;
+        for (int k = 0; k < 2; k++)
+            if (!side[dev][k] && (e = hipStreamCreateWithFlags(&side[dev][k], hipStreamNonBlocking)) != hipSuccess)
+                return e;
     }
-    hipStream_t aux = side[dev];
-    constexpr int kSplit = 17;  // windows [0, 17) need 128 doublings, [17, 33) another 128
-    hipEvent_t ev[3] = {};
+    hipStream_t chain = side[dev][0], fill = side[dev][1], mul = stream;
+    // parts of the 33 windows (PA_COMB_PARTS, 1..8): 3 measured best; more parts
+    // lose, each later chain part waiting for wave slots behind the previous
+    // part's multiply (profiles/r02_comb_parts.txt; a CU-masked chain stream and
+    // raised wave priorities did not change that)
+    static const int parts = [] {
+        const char* v = getenv("PA_COMB_PARTS");
+        const int k = v ? atoi(v) : 3;
+        return k < 1 ? 1 : (k > 8 ? 8 : k);
+    }();
+    int wb[9];
+    for (int p = 0; p <= parts; p++) wb[p] = (kCombWindows * p + parts - 1) / parts;
+    wb[parts] = kCombWindows;
+    hipEvent_t ev[2 + 2 * 8] = {};
     int made = 0;
     hipError_t err = hipSuccess;
     auto ck = [&](hipError_t x) {
         if (err == hipSuccess) err = x;
         return err == hipSuccess;
     };
-    for (; made < 3; made++)
+    for (; made < 2 + 2 * parts; made++)
         if (!ck(hipEventCreateWithFlags(&ev[made], hipEventDisableTiming))) break;
     uint64_t* bases = workspace;
     uint64_t* table_jac = workspace + (size_t)kG1Jac * kCombWindows;
-    const int e1 = kSplit * kCombEntries;
-    if (ck(hipEventRecord(ev[0], stream)) && ck(hipStreamWaitEvent(aux, ev[0], 0))) {
-        // side stream: the low half's bases, then the whole high half of the table
-        hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, aux, base, bases, 0, kSplit);
-        if (ck(hipGetLastError()) && ck(hipEventRecord(ev[1], aux)) &&
-            ck(comb_table_range(base, table_fl, workspace, kSplit, kCombWindows, aux)) &&
-            ck(hipEventRecord(ev[2], aux)) && ck(hipStreamWaitEvent(stream, ev[1], 0))) {
-            // caller's stream: low half of the table, low-half multiply, then the high half
-            hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(e1, 64)), dim3(64), 0, stream, bases, table_jac, 0,
-                               e1);
-            if (ck(hipGetLastError()) && ck(launch_g1_batch_normalize(table_jac, e1, stream))) {
-                hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1, 64)), dim3(64), 0, stream, table_jac,
-                                   table_fl, 0, e1);
-                hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_fl, scalars,
-                                   out, n, 0, kSplit, 1);
-                if (ck(hipGetLastError()) && ck(hipStreamWaitEvent(stream, ev[2], 0))) {
-                    hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_fl,
-                                       scalars, out, n, kSplit, kCombWindows, 0);
-                    ck(hipGetLastError());
-                }
-            }
+    if (ck(hipEventRecord(ev[0], stream)) && ck(hipStreamWaitEvent(chain, ev[0], 0)) &&
+        ck(hipStreamWaitEvent(fill, ev[0], 0)) && (mul == stream || ck(hipStreamWaitEvent(mul, ev[0], 0)))) {
+        for (int p = 0; p < parts && err == hipSuccess; p++) {
+            hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, chain, base, bases, wb[p], wb[p + 1]);
+            ck(hipGetLastError()) && ck(hipEventRecord(ev[1 + 2 * p], chain));
         }
+        for (int p = 0; p < parts && err == hipSuccess; p++) {
+            const int e0 = wb[p] * kCombEntries, e1 = wb[p + 1] * kCombEntries;
+            if (!ck(hipStreamWaitEvent(fill, ev[1 + 2 * p], 0))) break;
+            hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, fill, bases, table_jac, e0,
+                               e1);
+            if (!ck(hipGetLastError()) || !ck(launch_g1_batch_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, fill)))
+                break;
+            hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, fill, table_jac, table_fl,
+                               e0, e1);
+            ck(hipGetLastError()) && ck(hipEventRecord(ev[2 + 2 * p], fill));
+        }
+        for (int p = 0; p < parts && err == hipSuccess; p++) {
+            if (!ck(hipStreamWaitEvent(mul, ev[2 + 2 * p], 0))) break;
+            hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, mul, table_fl, scalars, out, n,
+                               wb[p], wb[p + 1], p == 0 ? 1 : 0);
+            ck(hipGetLastError());
+        }
+        // the caller's stream resumes after the last multiply
+        if (err == hipSuccess && mul != stream)
+            ck(hipEventRecord(ev[1 + 2 * parts], mul)) && ck(hipStreamWaitEvent(stream, ev[1 + 2 * parts], 0));
     }
     for (int k = 0; k < made; k++) (void)hipEventDestroy(ev[k]);
     return err;
