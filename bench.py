@@ -375,15 +375,17 @@ def main():
                 ev[2].record(stream)
 
         def comb_parts_ms(reps=3):
-            """table build and comb multiply as separate launches (untimed
-            region): the dominant kernel's own duration for the roofline"""
+            """the GLV table build and the GLV comb multiply as separate
+            stream-ordered launches (untimed region): the dominant kernel's own
+            duration for the roofline"""
             t_ms, m_ms = [], []
+            table, ws = pdev.fixed_base_buffers(dev)
             for _ in range(reps):
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 e[0].record(stream)
-                table, _ = pdev.g1_fixed_base_table(base, stream)
+                pdev.g1_fixed_base_glv_table(base, table, ws, stream)
                 e[1].record(stream)
-                pdev.g1_fixed_base_mul(table, scal, out, stream)
+                pdev.g1_fixed_base_glv_mul(base, table, ws, scal, out, stream)
                 e[2].record(stream)
                 torch.cuda.synchronize()
                 t_ms.append(e[0].elapsed_time(e[1]))
@@ -539,7 +541,7 @@ def main():
         elif args.workload == "wnaf":
             tot_ms, norm_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
             table_ms, mul_ms = comb_parts_ms()
-            dom_name, dom_ms, dom_bytes = ("g1_fixed_base_mul", mul_ms, 32 + 144) if mul_ms >= norm_ms else \
+            dom_name, dom_ms, dom_bytes = ("g1_glv_comb_mul", mul_ms, 32 + 144) if mul_ms >= norm_ms else \
                 ("g1_batch_normalize", norm_ms, 144 + 144)
             value = ws * n * args.steps / elapsed
             metric, unit = "G1 fixed-base scalar mults + batch_normalization per second at batch 2^18", "points/s"
@@ -547,7 +549,7 @@ def main():
                       "batch_per_gpu": n, "global_batch": n * ws,
                       "kernel_ms": {"table+fixed_base_mul (overlapped)": round(tot_ms, 3),
                                     "batch_normalize": round(norm_ms, 3),
-                                    "separately: table": round(table_ms, 3), "separately: fixed_base_mul": round(mul_ms, 3)}}
+                                    "separately: glv table": round(table_ms, 3), "separately: glv mul": round(mul_ms, 3)}}
         elif args.workload == "decode":
             g2_ms, g1_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
             dom_name, dom_ms, dom_bytes = ("g2_decode_compressed", g2_ms, 96 + 200 + 1) if g2_ms >= g1_ms else \
@@ -622,12 +624,15 @@ def main():
                 roof["issue"] = {"achieved": round(rate, 3), "peak": round(ISSUE_PEAK_T, 3),
                                  "unit": "T lane-instructions/s (one wave per SIMD)", "frac": rate / ISSUE_PEAK_T,
                                  "instructions_per_unit": instr}
-        if args.workload == "wnaf" and dom_name == "g1_fixed_base_mul":
+        if args.workload == "wnaf" and dom_name == "g1_glv_comb_mul":
             # VALU bound: each mixed addition (madd-2007-bl, ec.rs:446-526) is
             # 7 products + 4 squarings on the lazy 28-bit core (fl_gen.h
             # leaves: 392 / 301 v_mad_u64_u32); a scalar takes
-            # 32 * 255/256 + 1/2 nonzero comb digits on average
-            macs = (32 * 255 / 256 + 0.5) * (7 * 392 + 4 * 301)
+            # GLV split s = q x^2 + rem: 32.77 nonzero signed base-256 digits of
+            # rem and q together on average for s uniform below r (simulated
+            # over 2e4 scalars with kernels_curve.hip glv_split's arithmetic;
+            # the plain 33-window comb: 31.88)
+            macs = 32.77 * (7 * 392 + 4 * 301)
             mac_rate = macs * n / (dom_ms * 1e-3) / 1e12
             roof = {"kernel": dom_name, "bound": "valu", "achieved": round(mac_rate, 3),
                     "peak": round(VALU_MAC_PEAK_T, 3), "unit": "T limb-MAC/s (28x28-bit v_mad_u64_u32)",

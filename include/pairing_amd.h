@@ -285,9 +285,15 @@ size_t pa_g1_fixed_base_workspace_words(void);
 int pa_g1_fixed_base_table_device(const pa_g1 *base, uint64_t *table, uint64_t *workspace, void *stream);
 int pa_g1_fixed_base_mul_device(const uint64_t *table, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
                                 void *stream);
-/* Wnaf::new().base(base, n).scalar(s_i) for every i (wnaf.rs:93-107, 169-178) in one call: table build and
- * multiply with the table's serial base chain overlapped (a per-device side stream, ordered after `stream` by an
- * event); the same output bits as pa_g1_fixed_base_table_device + pa_g1_fixed_base_mul_device. */
+/* The same product in its GLV form as two stream-ordered stages (s = q x^2 + rem, s P = rem P - q phi(P) when
+ * phi(P) == -[x^2] P; the table's 17 base rows plus their phi images and a membership flag in `workspace`); the
+ * multiply stage falls back to a double-and-add from `base` when the flag says the base failed the check.  Equal as points to pa_g1_fixed_base_table_device + pa_g1_fixed_base_mul_device. */
+int pa_g1_fixed_base_glv_table_device(const pa_g1 *base, uint64_t *table, uint64_t *workspace, void *stream);
+int pa_g1_fixed_base_glv_mul_device(const pa_g1 *base, const uint64_t *table, const uint64_t *workspace,
+                                    const pa_fr_repr *scalars, pa_g1 *out, size_t n, void *stream);
+/* Wnaf::new().base(base, n).scalar(s_i) for every i (wnaf.rs:93-107, 169-178) in one call: the GLV table build
+ * and multiply with the table's serial base chain overlapped (per-device side streams, ordered after `stream` by
+ * events); equal as points to pa_g1_fixed_base_table_device + pa_g1_fixed_base_mul_device. */
 int pa_g1_wnaf_fixed_base_device(const pa_g1 *base, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
                                  uint64_t *table, uint64_t *workspace, void *stream);
 int pa_fq_mul_batch_device(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n, void *stream);

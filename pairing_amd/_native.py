@@ -98,6 +98,8 @@ _SIGS = {
     "pa_g1_fixed_base_table_device": [_P, _P, _P, _P],
     "pa_g1_fixed_base_mul_device": [_P, _P, _P, _N, _P],
     "pa_g1_wnaf_fixed_base_device": [_P, _P, _P, _N, _P, _P, _P],
+    "pa_g1_fixed_base_glv_table_device": [_P, _P, _P, _P],
+    "pa_g1_fixed_base_glv_mul_device": [_P, _P, _P, _P, _P, _N, _P],
     "pa_fq_mul_batch_device": [_P, _P, _P, _N, _P],
     "pa_miller_loop_fused_batch_device": [_P, _P, _P, _N, _P],
     "pa_final_exponentiation_batch_device": [_P, _P, _P, _N, _P],

@@ -806,6 +806,19 @@ int pa_g1_fixed_base_mul_device(const uint64_t* table, const pa_fr_repr* scalars
            "kernel launch");
     return PA_OK;
 }
+int pa_g1_fixed_base_glv_table_device(const pa_g1* base, uint64_t* table, uint64_t* workspace, void* stream) {
+    if (!base || !table || !workspace) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g1_glv_table((const uint64_t*)base, table, workspace, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
+int pa_g1_fixed_base_glv_mul_device(const pa_g1* base, const uint64_t* table, const uint64_t* workspace,
+                                    const pa_fr_repr* scalars, pa_g1* out, size_t n, void* stream) {
+    if (n && (!base || !table || !workspace || !scalars || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g1_glv_mul((const uint64_t*)base, table, workspace,
+                                 (const uint64_t*)scalars, (uint64_t*)out, n, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
 int pa_g1_wnaf_fixed_base_device(const pa_g1* base, const pa_fr_repr* scalars, pa_g1* out, size_t n,
                                  uint64_t* table, uint64_t* workspace, void* stream) {
     if (n && (!base || !scalars || !out || !table || !workspace)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");

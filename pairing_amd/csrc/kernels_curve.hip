@@ -32,9 +32,27 @@ constexpr int kG1Jac = 18;            // u64 words per Jacobian G1
 constexpr uint32_t kFlInfinity = 0xffffffffu;  // table entry marker: no lazy limb has all 32 bits set
 constexpr int kFlPair = 14;           // u64 words per table entry: x, y as 14 x 28-bit limbs (lazy core)
 constexpr int kNormChunk = 8;         // points per lane in batch_normalization (4 measured slower at 2^18)
+// GLV (endomorphism) form of the comb, used when the base passes the G1
+// membership test phi(P) == -[x^2] P (Scott, eprint 2021/1130; the decode
+// kernel's test): phi(x, y) = (beta x, y) acts on G1 as multiplication by
+// -x^2, so with s = q x^2 + rem (integer division, any 256-bit s)
+//   s P = rem P + q (x^2 P) = rem P + q psi(P),  psi(x, y) = (beta x, -y),
+// rem < 2^128, q < 2^129: 17 windows of each over rows T[0..16] and their
+// psi images T[17..33], after a base chain of 128 doublings instead of 256.
+// A base outside G1 (or off the curve) takes the plain 33-window comb; both
+// paths are launched, each kernel reading the membership flag and returning
+// at once when it is not its path's.
+constexpr int kGlvWindows = 17;
+constexpr int kTableRows = 2 * kGlvWindows;   // >= kCombWindows
+static_assert(kTableRows >= kCombWindows, "table rows");
+constexpr uint64_t kX2Lo = 0x0000000100000000ull, kX2Hi = 0xac45a4010001a402ull;   // x^2 = 0xd201000000010000^2
+// beta (a primitive cube root of unity in Fq, Montgomery R = 2^384), the decode kernel's kBeta
+__constant__ const uint64_t kGlvBeta[6] = {0x30f1361b798a64e8ULL, 0xf3b8ddab7ece5a2aULL, 0x16a8ca3ac61577f7ULL,
+                                           0xc26a2ff874fd029bULL, 0x3636b76660701c6eULL, 0x051ba4ab241b6160ULL};
+constexpr uint32_t kGateGlv = 1, kGatePlain = 0;   // membership flag values
 
 // ---------------- batch_normalization ----------------
-__global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict__ v, size_t n) {
+PA_DEV void g1_batch_normalize_chunk(uint64_t* __restrict__ v, size_t n) {
     __builtin_amdgcn_s_setprio(2);   // latency-bound: ahead of a concurrent comb multiply's waves
     const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t begin = lane * kNormChunk;
@@ -89,6 +107,9 @@ __global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict_
         }
     }
 }
+__global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict__ v, size_t n) {
+    g1_batch_normalize_chunk(v, n);
+}
 
 // ---------------- fixed-base comb ----------------
 // T[i][d-1] = d * B_i (Jacobian), one lane per entry: double-and-add over d's 8 bits.
@@ -98,21 +119,29 @@ __global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict_
     const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= e1) return;
     const int i = e / kCombEntries, d = e % kCombEntries + 1;
-    Jac<Fq> b, acc;
-    load_jac(b, bases + kG1Jac * i);
-    jac_zero(acc);
-#pragma unroll 1
-    for (int bit = 7; bit >= 0; bit--) {
-        jac_double(acc);
-        if ((d >> bit) & 1) jac_add(acc, b);
+    Jac<Fq> b0;
+    load_jac(b0, bases + kG1Jac * i);
+    if (fq_is_zero(b0.z)) {  // zero base: every multiple is this zero
+        store_jac(table_jac + (size_t)kG1Jac * e, b0);
+        return;
     }
-    store_jac(table_jac + (size_t)kG1Jac * e, acc);
+    // double-and-add from d's top bit on the lazy core (d < 2^8 < the order:
+    // no intermediate is zero)
+    const FlJac b = {fl_from_abi(b0.x), fl_from_abi(b0.y), fl_from_abi(b0.z)};
+    FlJac acc = b;
+    const int top = 31 - __builtin_clz(d);
+#pragma unroll 1
+    for (int bit = top - 1; bit >= 0; bit--) {
+        fl_jac_double(acc);
+        if ((d >> bit) & 1) fl_jac_add(acc, b);
+    }
+    fl_store_jac(table_jac + (size_t)kG1Jac * e, acc);
 }
 
 // normalized Jacobian table -> affine (x, y) in the lazy 28-bit core's
 // representation (fl.h: 14 limbs, R = 2^392), 28 u32 per entry
 __global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table_fl,
-                                                     int e0, int e1) {
+                                                     int e0, int e1, int phi_rows) {
     __builtin_amdgcn_s_setprio(2);   // table work of a later part runs beside the multiply
     const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= e1) return;
@@ -126,6 +155,17 @@ __global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict_
     for (int i = 0; i < 14; i++) {
         d[i] = zero ? kFlInfinity : x.w[i];
         d[14 + i] = zero ? kFlInfinity : y.w[i];
+    }
+    if (phi_rows) {  // GLV table: row 17 + i holds phi(T[i]) = (beta x, y)
+        Fq beta;
+        fq_load(beta, kGlvBeta);
+        const F<1> bx = mul(x, fl_from_abi(beta));
+        uint32_t* dp = d + 2 * kFlPair * kGlvWindows * kCombEntries;
+#pragma unroll
+        for (int i = 0; i < 14; i++) {
+            dp[i] = zero ? kFlInfinity : bx.w[i];
+            dp[14 + i] = zero ? kFlInfinity : y.w[i];
+        }
     }
 }
 
@@ -232,6 +272,191 @@ __global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__
     }
 }
 
+// GLV membership flag: *flag = kGateGlv iff phi(P) == -[x^2] P (or P is
+// zero: every path gives zero), computed as [|x|]([|x|] P) by two 64-bit
+// double-and-add chains on the lazy core (three lanes per doubling), then
+// compared in Jacobian coordinates.  One wave; runs beside the GLV table
+// build and multiply, and only the fallback's launches wait for it.
+__global__ void __launch_bounds__(64) k_g1_glv_check(const uint64_t* __restrict__ base, uint32_t* __restrict__ flag) {
+    if (blockIdx.x != 0) return;
+    const int lane = threadIdx.x;
+    Jac<Fq> p0;
+    load_jac(p0, base);
+    uint32_t glv = kGateGlv;
+    if (!fq_is_zero(p0.z)) {
+        FlJac p;
+        p.x = fl_from_abi(p0.x);
+        p.y = fl_from_abi(p0.y);
+        p.z = fl_from_abi(p0.z);
+        constexpr uint64_t kX = 0xd201000000010000ull;   // |x|, the BLS parameter (x < 0)
+        FlJac a = p, b = p;
+#pragma unroll 1
+        for (int round = 0; round < 2; round++) {   // a = |x| b, then b = a
+#pragma unroll 1
+            for (int bit = 62; bit >= 0; bit--) {
+                if (!fl_is_zero(a.z)) fl_jac_double_3lane(a, lane);
+                if ((kX >> bit) & 1) fl_jac_add(a, b);
+            }
+            b = a;
+        }
+        // phi(P) = (beta X_P, Y_P, Z_P) == -(X_A, Y_A, Z_A), A = [x^2] P
+        Fq beta;
+        fq_load(beta, kGlvBeta);
+        const F<1> za2 = sqr(a.z), zp2 = sqr(p.z);
+        const bool xs = fl_eq(mul(mul(p.x, fl_from_abi(beta)), za2), mul(a.x, zp2));
+        const bool ys = fl_is_zero(add(mul(mul(p.y, a.z), za2), mul(mul(a.y, p.z), zp2)));
+        glv = (!fl_is_zero(a.z) && xs && ys) ? kGateGlv : kGatePlain;
+    }
+    if (lane == 0) *flag = glv;
+}
+
+// s = q x^2 + rem for a 256-bit s (Barrett, HAC 14.42 without the final
+// corrections): q = floor(floor(s / 2^127) m / 2^129), m = floor(2^256 / x^2),
+// never above floor(s / x^2), so rem = s - q x^2 is in [0, 2 x^2) < 2^129
+// (one correction short at most) and q < 2^129: 17 signed base-256 digits each.
+PA_DEV void glv_split(const uint64_t s[4], uint64_t rem[3], uint64_t q[3]) {
+    constexpr uint64_t m[3] = {0x63f6e522f6cfee2eull, 0x7c6becf1e01faaddull, 1};
+    const uint64_t t[3] = {(s[1] >> 63) | (s[2] << 1), (s[2] >> 63) | (s[3] << 1), s[3] >> 63};
+    uint64_t pr[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const unsigned __int128 v = (unsigned __int128)t[i] * m[j] + pr[i + j] + c;
+            pr[i + j] = (uint64_t)v;
+            c = (uint64_t)(v >> 64);
+        }
+        pr[i + 3] = c;
+    }
+    q[0] = (pr[2] >> 1) | (pr[3] << 63);
+    q[1] = (pr[3] >> 1) | (pr[4] << 63);
+    q[2] = (pr[4] >> 1) | (pr[5] << 63);
+    // q x^2 mod 2^192
+    const unsigned __int128 a0 = (unsigned __int128)q[0] * kX2Lo;
+    const unsigned __int128 a1 = (unsigned __int128)q[0] * kX2Hi + (uint64_t)(a0 >> 64);
+    const unsigned __int128 b1 = (unsigned __int128)q[1] * kX2Lo + (uint64_t)a1;
+    const uint64_t w0 = (uint64_t)a0, w1 = (uint64_t)b1;
+    const uint64_t w2 = (uint64_t)(a1 >> 64) + (uint64_t)(b1 >> 64) + q[1] * kX2Hi + q[2] * kX2Lo;
+    unsigned __int128 d = (unsigned __int128)s[0] - w0;
+    rem[0] = (uint64_t)d;
+    d = (unsigned __int128)s[1] - w1 - (uint64_t)((d >> 64) & 1);
+    rem[1] = (uint64_t)d;
+    rem[2] = s[2] - w2 - (uint64_t)((d >> 64) & 1);
+}
+
+// next signed base-256 digit of a little-endian 3-word value (window `win`)
+PA_DEV int glv_digit(const uint64_t v[3], int win, int& carry) {
+    int d = carry + (int)((v[win >> 3] >> (8 * (win & 7))) & 0xff);
+    carry = d > 128 ? 1 : 0;
+    if (d > 128) d -= 256;
+    return d;
+}
+
+PA_DEV void comb_add_entry(FlJac& acc, bool& untouched, bool& changed, const uint64_t* table_fl, int row, int d,
+                           bool flip) {
+    const int ad = d < 0 ? -d : d;
+    const uint2* src = reinterpret_cast<const uint2*>(table_fl + (size_t)kFlPair * (row * kCombEntries + ad - 1));
+    F<1> tx, ty;
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        const uint2 a = src[k], b = src[7 + k];
+        tx.w[2 * k] = a.x;
+        tx.w[2 * k + 1] = a.y;
+        ty.w[2 * k] = b.x;
+        ty.w[2 * k + 1] = b.y;
+    }
+    if (tx.w[0] != kFlInfinity) {  // adding the identity is add_assign_mixed's no-op
+        const F<2> oy = ((d < 0) != flip) ? neg(ty) : relax<2>(ty);
+        fl_jac_add_mixed(acc, untouched, tx, oy);
+        changed = true;
+    }
+}
+
+// GLV comb multiply, windows [w0, w1) of both halves: s g = rem g + q psi(g)
+// with psi(g) = -phi(g), so a q digit d adds -d phi(T[win][|d|]) from row 17 + win.
+// Same accumulate/store protocol as k_g1_comb_mul.
+__global__ void __launch_bounds__(64) k_g1_glv_mul(const uint64_t* __restrict__ table_fl,
+                                                   const uint64_t* __restrict__ scalars, uint64_t* __restrict__ out,
+                                                   size_t n, int w0, int w1, int first,
+                                                   const uint32_t* __restrict__ gate) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (gate && *gate != kGateGlv)) return;
+    uint64_t s[4], rem[3], q[3];
+#pragma unroll
+    for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
+    glv_split(s, rem, q);
+    uint64_t* o = out + (size_t)kG1Jac * i;
+    FlJac acc;
+    bool untouched = true, changed = false;
+    if (first) {
+        acc.x = fl_zero();
+        acc.y = fl_one();
+        acc.z = fl_zero();
+    } else {
+        acc.x = fl_load(o);
+        acc.y = fl_load(o + 6);
+        acc.z = fl_load(o + 12);
+        untouched = false;
+    }
+    int cr = 0, cq = 0;
+    for (int win = 0; win < w0; win++) {
+        glv_digit(rem, win, cr);
+        glv_digit(q, win, cq);
+    }
+    // one add site for both halves (two inlined copies of the mixed addition
+    // outgrow the instruction cache): step 2 win + h, h = 1 the q digit
+    int dq = 0;
+#pragma unroll 1
+    for (int step = 2 * w0; step < 2 * w1; step++) {
+        const int win = step >> 1;
+        int d;
+        if ((step & 1) == 0) {
+            d = glv_digit(rem, win, cr);
+            dq = glv_digit(q, win, cq);
+        } else {
+            d = dq;
+        }
+        if (d != 0) comb_add_entry(acc, untouched, changed, table_fl, (step & 1) * kGlvWindows + win, d, step & 1);
+    }
+    if (!first && !changed) return;
+    if (untouched) {
+        Jac<Fq> z;
+        jac_zero(z);
+        store_jac(o, z);
+    } else {
+        fl_store(o, acc.x);
+        fl_store(o + 6, acc.y);
+        fl_store(o + 12, acc.z);
+    }
+}
+
+// s * P by double-and-add over the 256 scalar bits with full Jacobian
+// additions (add-2007-bl, ec.rs:356-444, doubling and zero cases inside), one
+// lane per scalar, for the GLV path's fallback (*gate == kGatePlain)
+__global__ void __launch_bounds__(64) k_g1_fixed_base_ladder(const uint64_t* __restrict__ base,
+                                                             const uint64_t* __restrict__ scalars,
+                                                             uint64_t* __restrict__ out, size_t n,
+                                                             const uint32_t* __restrict__ gate) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || *gate != kGatePlain) return;
+    const FlJac p = fl_load_jac(base);
+    FlJac acc = {fl_zero(), fl_one(), fl_zero()};
+#pragma unroll 1
+    for (int bit = 255; bit >= 0; bit--) {
+        if (!fl_is_zero(acc.z)) fl_jac_double(acc);
+        if ((scalars[4 * i + (bit >> 6)] >> (bit & 63)) & 1) fl_jac_add(acc, p);
+    }
+    uint64_t* o = out + (size_t)kG1Jac * i;
+    if (fl_is_zero(acc.z)) {
+        Jac<Fq> z;
+        jac_zero(z);
+        store_jac(o, z);
+    } else {
+        fl_store_jac(o, acc);
+    }
+}
+
 static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream) {
@@ -242,12 +467,19 @@ hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream) 
 }
 
 size_t g1_comb_workspace_words() {
-    return (size_t)kG1Jac * kCombWindows + (size_t)kG1Jac * kCombWindows * kCombEntries;
+    // bases, Jacobian table, then one u64 holding the GLV membership flag
+    return (size_t)kG1Jac * kCombWindows + (size_t)kG1Jac * kCombWindows * kCombEntries + 1;
 }
-size_t g1_comb_table_words() { return (size_t)kFlPair * kCombWindows * kCombEntries; }
+size_t g1_comb_table_words() { return (size_t)kFlPair * kTableRows * kCombEntries; }
 
+static uint32_t* glv_flag(const uint64_t* workspace) {
+    const uint64_t* f = workspace + (size_t)kG1Jac * kCombWindows + (size_t)kG1Jac * kCombWindows * kCombEntries;
+    return reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(f));
+}
+
+// bases + table rows [w0, w1) on one stream; `phi_rows` also writes the GLV rows 17 + i
 static hipError_t comb_table_range(const uint64_t* base, uint64_t* table_fl, uint64_t* workspace, int w0, int w1,
-                                   hipStream_t stream) {
+                                   int phi_rows, hipStream_t stream) {
     uint64_t* bases = workspace;
     uint64_t* table_jac = workspace + (size_t)kG1Jac * kCombWindows;
     const int e0 = w0 * kCombEntries, e1 = w1 * kCombEntries;
@@ -256,12 +488,12 @@ static hipError_t comb_table_range(const uint64_t* base, uint64_t* table_fl, uin
     const hipError_t e = launch_g1_batch_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, stream, table_jac, table_fl, e0,
-                       e1);
+                       e1, phi_rows);
     return hipGetLastError();
 }
 
 hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_fl, uint64_t* workspace, hipStream_t stream) {
-    return comb_table_range(base, table_fl, workspace, 0, kCombWindows, stream);
+    return comb_table_range(base, table_fl, workspace, 0, kCombWindows, 0, stream);
 }
 
 hipError_t launch_g1_comb_mul(const uint64_t* table_fl, const uint64_t* scalars, uint64_t* out, size_t n,
@@ -272,42 +504,80 @@ hipError_t launch_g1_comb_mul(const uint64_t* table_fl, const uint64_t* scalars,
     return hipGetLastError();
 }
 
-// Table + multiply with the serial base chain overlapped, in window parts: the
-// multiply over part p (accumulating into `out`) runs on `stream` while the
-// chain doubles toward later parts' bases and their table entries are built.
-// Same result bits as launch_g1_comb_table + launch_g1_comb_mul.
+// the GLV path's fallback, one launch that returns at once unless the base
+// failed the membership check (a base outside G1: the reference's types never
+// hold one, so throughput does not matter there, the launch count does)
+static hipError_t glv_fallback(const uint64_t* base, const uint64_t* workspace, const uint64_t* scalars, uint64_t* out,
+                               size_t n, hipStream_t stream) {
+    hipLaunchKernelGGL(k_g1_fixed_base_ladder, dim3(blocks_for(n, 64)), dim3(64), 0, stream, base, scalars, out, n,
+                       glv_flag(workspace));
+    return hipGetLastError();
+}
+
+hipError_t launch_g1_glv_table(const uint64_t* base, uint64_t* table_fl, uint64_t* workspace, hipStream_t stream) {
+    hipLaunchKernelGGL(k_g1_glv_check, dim3(1), dim3(64), 0, stream, base, glv_flag(workspace));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return comb_table_range(base, table_fl, workspace, 0, kGlvWindows, 1, stream);
+}
+
+hipError_t launch_g1_glv_mul(const uint64_t* base, const uint64_t* table_fl, const uint64_t* workspace, const uint64_t* scalars,
+                             uint64_t* out, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_g1_glv_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_fl, scalars, out, n, 0,
+                       kGlvWindows, 1, glv_flag(workspace));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return glv_fallback(base, workspace, scalars, out, n, stream);
+}
+
+// Table + multiply in one call, GLV form with the serial base chain
+// overlapped, in window parts of the 17 GLV windows: the chain (side stream 0)
+// doubles toward part p + 1's bases while side stream 1 builds part p's rows
+// and their phi images and the caller's stream multiplies part p.  Side
+// stream 2 runs the membership check from the start; after the last GLV
+// multiply the caller's stream waits for it and runs the plain 33-window comb
+// (table + multiply), whose kernels return at once unless the check failed.
+// Equal as points to launch_g1_comb_table + launch_g1_comb_mul.
 hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
                                 uint64_t* table_fl, uint64_t* workspace, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    // two per-device side streams: `chain` runs the serial base chain part by
-    // part; `fill` turns each finished part's bases into its table entries
-    // (double-and-add, batch normalization, packing); the caller's stream
-    // multiplies part p while the chain and the table work on parts > p.
     static std::mutex mu;
-    static hipStream_t side[64][2] = {};
+    static hipStream_t side[64][3] = {};
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     {
         std::lock_guard<std::mutex> g(mu);
-        for (int k = 0; k < 2; k++)
+        for (int k = 0; k < 3; k++)
             if (!side[dev][k] && (e = hipStreamCreateWithFlags(&side[dev][k], hipStreamNonBlocking)) != hipSuccess)
                 return e;
     }
-    hipStream_t chain = side[dev][0], fill = side[dev][1], mul = stream;
-    // parts of the 33 windows (PA_COMB_PARTS, 1..8): 3 measured best; more parts
-    // lose, each later chain part waiting for wave slots behind the previous
-    // part's multiply (profiles/r02_comb_parts.txt; a CU-masked chain stream and
-    // raised wave priorities did not change that)
+    hipStream_t chain = side[dev][0], fill = side[dev][1], check = side[dev][2], mul = stream;
+    static const bool serial = getenv("PA_COMB_SERIAL") && atoi(getenv("PA_COMB_SERIAL")) != 0;
+    if (serial) chain = fill = check = stream;   // measurement only: every kernel in order on the caller's stream
+    // parts of the 17 GLV windows (PA_COMB_PARTS, 1..8; PA_COMB_FIRST windows in
+    // part 0): 2 parts split 5 + 12 measured best (profiles/r02_glv_comb.txt) --
+    // a short first part starts the multiply early, a long second one hides the
+    // rest of the chain and its rows behind the first part's multiply
     static const int parts = [] {
         const char* v = getenv("PA_COMB_PARTS");
-        const int k = v ? atoi(v) : 3;
+        const int k = v ? atoi(v) : 2;
         return k < 1 ? 1 : (k > 8 ? 8 : k);
     }();
+    static const int first_w = [] {
+        const char* v = getenv("PA_COMB_FIRST");
+        return v ? atoi(v) : 5;
+    }();
     int wb[9];
-    for (int p = 0; p <= parts; p++) wb[p] = (kCombWindows * p + parts - 1) / parts;
-    wb[parts] = kCombWindows;
+    for (int p = 0; p <= parts; p++) wb[p] = (kGlvWindows * p + parts - 1) / parts;
+    if (parts > 1 && first_w > 0 && first_w < kGlvWindows - (parts - 2)) {
+        wb[1] = first_w;
+        for (int p = 2; p < parts; p++) wb[p] = first_w + ((kGlvWindows - first_w) * (p - 1) + parts - 2) / (parts - 1);
+    }
+    wb[parts] = kGlvWindows;
+    // ev[0]: start; ev[1 + 2p]: chain part p done; ev[2 + 2p]: rows of part p done; ev[1 + 2 parts]: check done
     hipEvent_t ev[2 + 2 * 8] = {};
     int made = 0;
     hipError_t err = hipSuccess;
@@ -319,8 +589,11 @@ hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, u
         if (!ck(hipEventCreateWithFlags(&ev[made], hipEventDisableTiming))) break;
     uint64_t* bases = workspace;
     uint64_t* table_jac = workspace + (size_t)kG1Jac * kCombWindows;
+    uint32_t* flag = glv_flag(workspace);
     if (ck(hipEventRecord(ev[0], stream)) && ck(hipStreamWaitEvent(chain, ev[0], 0)) &&
-        ck(hipStreamWaitEvent(fill, ev[0], 0)) && (mul == stream || ck(hipStreamWaitEvent(mul, ev[0], 0)))) {
+        ck(hipStreamWaitEvent(fill, ev[0], 0)) && ck(hipStreamWaitEvent(check, ev[0], 0))) {
+        hipLaunchKernelGGL(k_g1_glv_check, dim3(1), dim3(64), 0, check, base, flag);
+        ck(hipGetLastError()) && ck(hipEventRecord(ev[1 + 2 * parts], check));
         for (int p = 0; p < parts && err == hipSuccess; p++) {
             hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, chain, base, bases, wb[p], wb[p + 1]);
             ck(hipGetLastError()) && ck(hipEventRecord(ev[1 + 2 * p], chain));
@@ -333,18 +606,18 @@ hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, u
             if (!ck(hipGetLastError()) || !ck(launch_g1_batch_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, fill)))
                 break;
             hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, fill, table_jac, table_fl,
-                               e0, e1);
+                               e0, e1, 1);
             ck(hipGetLastError()) && ck(hipEventRecord(ev[2 + 2 * p], fill));
         }
         for (int p = 0; p < parts && err == hipSuccess; p++) {
             if (!ck(hipStreamWaitEvent(mul, ev[2 + 2 * p], 0))) break;
-            hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, mul, table_fl, scalars, out, n,
-                               wb[p], wb[p + 1], p == 0 ? 1 : 0);
+            hipLaunchKernelGGL(k_g1_glv_mul, dim3(blocks_for(n, 64)), dim3(64), 0, mul, table_fl, scalars, out, n,
+                               wb[p], wb[p + 1], p == 0 ? 1 : 0, nullptr);
             ck(hipGetLastError());
         }
-        // the caller's stream resumes after the last multiply
-        if (err == hipSuccess && mul != stream)
-            ck(hipEventRecord(ev[1 + 2 * parts], mul)) && ck(hipStreamWaitEvent(stream, ev[1 + 2 * parts], 0));
+        // fallback: the plain comb, live only when the base failed the check
+        if (err == hipSuccess && ck(hipStreamWaitEvent(mul, ev[1 + 2 * parts], 0)))
+            ck(glv_fallback(base, workspace, scalars, out, n, mul));
     }
     for (int k = 0; k < made; k++) (void)hipEventDestroy(ev[k]);
     return err;

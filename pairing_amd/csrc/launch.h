@@ -101,8 +101,13 @@ size_t g1_comb_workspace_words();
 hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_aff, uint64_t* workspace, hipStream_t stream);
 hipError_t launch_g1_comb_mul(const uint64_t* table_aff, const uint64_t* scalars, uint64_t* out, size_t n,
                               hipStream_t stream);
-// both in one call, the table's serial base chain overlapped with the multiply
-// (a side stream per device; same result bits)
+// GLV form as two stages on one stream (table rows + phi rows + membership
+// flag; multiply, with a double-and-add fallback for a base that failed the check)
+hipError_t launch_g1_glv_table(const uint64_t* base, uint64_t* table, uint64_t* workspace, hipStream_t stream);
+hipError_t launch_g1_glv_mul(const uint64_t* base, const uint64_t* table, const uint64_t* workspace, const uint64_t* scalars,
+                             uint64_t* out, size_t n, hipStream_t stream);
+// both in one call, the GLV table's serial base chain overlapped with the
+// multiply (side streams per device; equal as points)
 hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
                                 uint64_t* table, uint64_t* workspace, hipStream_t stream);
 

@@ -78,6 +78,19 @@ def g1_fixed_base_mul(table, scalars, out, stream=None):
          _dptr(out, W_G1, "out"), scalars.shape[0], _stream_ptr(stream))
 
 
+def g1_fixed_base_glv_table(base, table, ws, stream=None):
+    """GLV stage 1: table rows, their phi images and the membership flag (ws)."""
+    call("pa_g1_fixed_base_glv_table_device", _dptr(base, W_G1, "base"), ctypes.c_void_p(table.data_ptr()),
+         ctypes.c_void_p(ws.data_ptr()), _stream_ptr(stream))
+
+
+def g1_fixed_base_glv_mul(base, table, ws, scalars, out, stream=None):
+    """GLV stage 2: out[i] = scalars[i] * base (plain-comb fallback inside)."""
+    call("pa_g1_fixed_base_glv_mul_device", _dptr(base, W_G1, "base"), ctypes.c_void_p(table.data_ptr()),
+         ctypes.c_void_p(ws.data_ptr()), _dptr(scalars, 4, "scalars"), _dptr(out, W_G1, "out"), scalars.shape[0],
+         _stream_ptr(stream))
+
+
 def g1_wnaf_fixed_base(base, scalars, out, table, ws, stream=None):
     """out[i] = scalars[i] * base with the table built in the same call (its
     serial base chain overlapped with the multiply); table / ws as returned by

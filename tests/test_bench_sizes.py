@@ -185,3 +185,40 @@ def test_multi_pairing_device_matches_oracle(gpu, oracle, n):
         exp = exp[0]
     assert int(ok.item()) == 1
     np.testing.assert_array_equal(_host(out)[0], exp)
+
+
+@pytest.mark.parametrize("which", ["subgroup", "outside"])
+def test_g1_glv_stages_device_match_oracle(gpu, oracle, which):
+    """config 3's GLV stages as bench.py times them for the roofline
+    (pa_g1_fixed_base_glv_table_device, then pa_g1_fixed_base_glv_mul_device
+    with its plain-comb fallback) and the fused pa_g1_wnaf_fixed_base_device,
+    for a base in G1 and one outside it: equal as points to the reference's
+    wNAF (wnaf.rs:93-178), then bit-exact after batch_normalization."""
+    import torch
+    import decode_cases as D
+    import pairing_amd.device as pdev
+    from helpers import mont
+    pts, truth = D.subgroup_points(1, seed=70, n=1)
+    x, y = next(P for P, t in zip(pts, truth) if t == (which == "subgroup"))
+    z = 0x5eed % Q
+    base_np = np.array([mont(x * z * z) + mont(y * z * z * z) + mont(z)], np.uint64)
+    n = 4096 + 17
+    g = rng(71)
+    s = np.zeros((n, 4), np.uint64)
+    for k in range(n):
+        s[k] = limbs(int(g.integers(0, 1 << 62)) << 190 | int(g.integers(0, 1 << 62)) << 128
+                     | int(g.integers(0, 1 << 62)) << 64 | int(g.integers(0, 1 << 62)), 4)
+    base, scal = _dev(base_np), _dev(s)
+    table, ws = pdev.fixed_base_buffers("cuda:0")
+    out1 = pdev.empty_records(n, 18, "cuda:0")
+    out2 = pdev.empty_records(n, 18, "cuda:0")
+    pdev.g1_fixed_base_glv_table(base, table, ws)
+    pdev.g1_fixed_base_glv_mul(base, table, ws, scal, out1)
+    pdev.g1_wnaf_fixed_base(base, scal, out2, table, ws)
+    torch.cuda.synchronize()
+    got1, got2 = _host(out1), _host(out2)
+    idx = np.concatenate([np.arange(64), np.arange(n - 64, n)])
+    exp = oracle.g1_wnaf_fixed_base(base_np, np.ascontiguousarray(s[idx]), 8)
+    assert oracle.g1_eq(np.ascontiguousarray(got1[idx]), exp).all()
+    assert oracle.g1_eq(np.ascontiguousarray(got2[idx]), exp).all()
+    np.testing.assert_array_equal(oracle.g1_batch_normalization(got1), oracle.g1_batch_normalization(got2))

@@ -5,7 +5,7 @@ The bar is bit-exact: all of this is integer arithmetic with canonical
 import numpy as np
 import pytest
 
-from helpers import (Q, R_ORDER, RMONT, fq12_one, hexlimbs, limbs, load_json, random_fq, random_scalars,
+from helpers import (Q, R_ORDER, RMONT, fq12_one, hexlimbs, limbs, load_json, mont, random_fq, random_scalars,
                      relic_fq12, rng, set_infinity, small_scalars)
 
 pytestmark = pytest.mark.gpu
@@ -325,3 +325,35 @@ def test_g1_fixed_base_overlapped_halves(gpu, oracle, zero_base):
     assert oracle.g1_eq(got[:k], exp).all()
     if not zero_base:  # a zero base gives zeros whose (x, y) bits are whatever the add chain copied (ec.rs:398)
         np.testing.assert_array_equal(gpu.g1_batch_normalization(got[:k]), oracle.g1_batch_normalization(exp))
+
+
+_X2 = 0xd201000000010000 ** 2  # x^2, the GLV split's divisor (kernels_curve.hip glv_split)
+
+
+def _glv_edge_scalars():
+    vals = [0, 1, _X2 - 1, _X2, _X2 + 1, 2 * _X2 - 1, 2 * _X2, (1 << 128) - 1, 1 << 128,
+            (_X2 << 1) + (1 << 127), R_ORDER - 1, R_ORDER, (1 << 255) - 1, (1 << 256) - (1 << 200),
+            (1 << 128) * _X2, ((1 << 256) - (1 << 200)) // _X2 * _X2, 0x80 * _X2 + 0x80, 0x81 * _X2 + 0x81, (0x80 << 120) * _X2 + (0x81 << 120)]
+    return np.array([limbs(v, 4) for v in vals], np.uint64)
+
+
+@pytest.mark.parametrize("which", ["subgroup", "outside"])
+def test_g1_fixed_base_glv_and_fallback(gpu, oracle, which):
+    """pa_g1_wnaf_fixed_base takes the GLV split s = q x^2 + rem when the base
+    passes phi(P) == -[x^2] P and the plain 33-window comb otherwise (the
+    kernels of both are launched; the flag picks one).  Bases: on-curve points
+    in and outside G1 (cofactor components of order 3 and others, tests/
+    decode_cases.py), non-normalized (random z); scalars at the split's and the
+    signed digits' edges plus random ones.  Equal as points to the oracle's wNAF."""
+    import decode_cases as D
+    pts, truth = D.subgroup_points(1, seed=60, n=2)
+    sel = [P for P, t in zip(pts, truth) if t == (which == "subgroup")]
+    assert sel
+    g = rng(61)
+    s = np.concatenate([_glv_edge_scalars(), random_scalars(g, 200, bits=256)])
+    for k, (x, y) in enumerate(sel[:3]):
+        z = (k + 2) * 0x1234567 % Q
+        base = np.array([mont(x * z * z) + mont(y * z * z * z) + mont(z)], np.uint64)
+        got = gpu.g1_wnaf_fixed_base(base, s)
+        exp = oracle.g1_wnaf_fixed_base(base, s, NT)
+        assert oracle.g1_eq(got, exp).all(), (which, k)
