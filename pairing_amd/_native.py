@@ -17,7 +17,8 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libpairing_amd.so")
+# PA_LIB_PATH: an A/B build of the same sources (tools/curve_variants.sh); default the in-tree library
+LIB_PATH = os.environ.get("PA_LIB_PATH") or os.path.join(HERE, "lib", "libpairing_amd.so")
 
 W_FQ, W_FQ2, W_FQ6, W_FQ12 = 6, 12, 36, 72
 W_G1A, W_G1, W_G2A, W_G2 = 13, 18, 25, 36

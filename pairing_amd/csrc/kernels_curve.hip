@@ -31,6 +31,9 @@ constexpr int kCombEntries = 128;     // |d| in 1..128
 constexpr int kG1Jac = 18;            // u64 words per Jacobian G1
 constexpr uint32_t kFlInfinity = 0xffffffffu;  // table entry marker: no lazy limb has all 32 bits set
 constexpr int kFlPair = 14;           // u64 words per table entry: x, y as 14 x 28-bit limbs (lazy core)
+#ifndef PA_TABLE_NORM_CHUNK
+#define PA_TABLE_NORM_CHUNK 4   // 8 / 4 / 2 measured 2.40 / 2.31 / 2.32 ms (profiles/r02_glv_comb.txt)
+#endif
 constexpr int kNormChunk = 8;         // points per lane in batch_normalization (4 measured slower at 2^18)
 // GLV (endomorphism) form of the comb, used when the base passes the G1
 // membership test phi(P) == -[x^2] P (Scott, eprint 2021/1130; the decode
@@ -52,6 +55,7 @@ __constant__ const uint64_t kGlvBeta[6] = {0x30f1361b798a64e8ULL, 0xf3b8ddab7ece
 constexpr uint32_t kGateGlv = 1, kGatePlain = 0;   // membership flag values
 
 // ---------------- batch_normalization ----------------
+template <int kNormChunk>
 PA_DEV void g1_batch_normalize_chunk(uint64_t* __restrict__ v, size_t n) {
     __builtin_amdgcn_s_setprio(2);   // latency-bound: ahead of a concurrent comb multiply's waves
     const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -108,7 +112,13 @@ PA_DEV void g1_batch_normalize_chunk(uint64_t* __restrict__ v, size_t n) {
     }
 }
 __global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict__ v, size_t n) {
-    g1_batch_normalize_chunk(v, n);
+    g1_batch_normalize_chunk<kNormChunk>(v, n);
+}
+// the comb table's rows: a few hundred points, latency-bound (one inversion
+// per lane whatever the chunk), so shorter product chains per lane
+constexpr int kTableNormChunk = PA_TABLE_NORM_CHUNK;
+__global__ void __launch_bounds__(64) k_g1_table_normalize(uint64_t* __restrict__ v, size_t n) {
+    g1_batch_normalize_chunk<kTableNormChunk>(v, n);
 }
 
 // ---------------- fixed-base comb ----------------
@@ -376,6 +386,7 @@ PA_DEV void comb_add_entry(FlJac& acc, bool& untouched, bool& changed, const uin
 // GLV comb multiply, windows [w0, w1) of both halves: s g = rem g + q psi(g)
 // with psi(g) = -phi(g), so a q digit d adds -d phi(T[win][|d|]) from row 17 + win.
 // Same accumulate/store protocol as k_g1_comb_mul.
+// (4 waves per SIMD via launch bounds, <= 128 VGPRs, spills: 1.57 -> 2.75 ms)
 __global__ void __launch_bounds__(64) k_g1_glv_mul(const uint64_t* __restrict__ table_fl,
                                                    const uint64_t* __restrict__ scalars, uint64_t* __restrict__ out,
                                                    size_t n, int w0, int w1, int first,
@@ -459,6 +470,12 @@ __global__ void __launch_bounds__(64) k_g1_fixed_base_ladder(const uint64_t* __r
 
 static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
+static hipError_t table_normalize(uint64_t* v, size_t n, hipStream_t stream) {
+    const size_t lanes = (n + kTableNormChunk - 1) / kTableNormChunk;
+    hipLaunchKernelGGL(k_g1_table_normalize, dim3(blocks_for(lanes, 64)), dim3(64), 0, stream, v, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const size_t lanes = (n + kNormChunk - 1) / kNormChunk;
@@ -485,7 +502,7 @@ static hipError_t comb_table_range(const uint64_t* base, uint64_t* table_fl, uin
     const int e0 = w0 * kCombEntries, e1 = w1 * kCombEntries;
     hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, stream, base, bases, w0, w1);
     hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, stream, bases, table_jac, e0, e1);
-    const hipError_t e = launch_g1_batch_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, stream);
+    const hipError_t e = table_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, stream, table_jac, table_fl, e0,
                        e1, phi_rows);
@@ -603,7 +620,7 @@ hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, u
             if (!ck(hipStreamWaitEvent(fill, ev[1 + 2 * p], 0))) break;
             hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, fill, bases, table_jac, e0,
                                e1);
-            if (!ck(hipGetLastError()) || !ck(launch_g1_batch_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, fill)))
+            if (!ck(hipGetLastError()) || !ck(table_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, fill)))
                 break;
             hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, fill, table_jac, table_fl,
                                e0, e1, 1);
