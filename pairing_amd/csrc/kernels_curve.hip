@@ -31,9 +31,6 @@ constexpr int kCombEntries = 128;     // |d| in 1..128
 constexpr int kG1Jac = 18;            // u64 words per Jacobian G1
 constexpr uint32_t kFlInfinity = 0xffffffffu;  // table entry marker: no lazy limb has all 32 bits set
 constexpr int kFlPair = 14;           // u64 words per table entry: x, y as 14 x 28-bit limbs (lazy core)
-#ifndef PA_TABLE_NORM_CHUNK
-#define PA_TABLE_NORM_CHUNK 4   // 8 / 4 / 2 measured 2.40 / 2.31 / 2.32 ms (profiles/r02_glv_comb.txt)
-#endif
 constexpr int kNormChunk = 8;         // points per lane in batch_normalization (4 measured slower at 2^18)
 // GLV (endomorphism) form of the comb, used when the base passes the G1
 // membership test phi(P) == -[x^2] P (Scott, eprint 2021/1130; the decode
@@ -114,29 +111,36 @@ PA_DEV void g1_batch_normalize_chunk(uint64_t* __restrict__ v, size_t n) {
 __global__ void __launch_bounds__(64) k_g1_batch_normalize(uint64_t* __restrict__ v, size_t n) {
     g1_batch_normalize_chunk<kNormChunk>(v, n);
 }
-// the comb table's rows: a few hundred points, latency-bound (one inversion
-// per lane whatever the chunk), so shorter product chains per lane
-constexpr int kTableNormChunk = PA_TABLE_NORM_CHUNK;
-__global__ void __launch_bounds__(64) k_g1_table_normalize(uint64_t* __restrict__ v, size_t n) {
-    g1_batch_normalize_chunk<kTableNormChunk>(v, n);
-}
-
 // ---------------- fixed-base comb ----------------
-// T[i][d-1] = d * B_i (Jacobian), one lane per entry: double-and-add over d's 8 bits.
-__global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict__ bases, uint64_t* __restrict__ table_jac,
-                                                     int e0, int e1) {
+// T[i][d-1] = d * B_i as affine (x, y) in the lazy 28-bit core's
+// representation (fl.h: 14 limbs, R = 2^392, 28 u32 per entry), one lane per
+// entry: double-and-add over d's bits on the lazy core, then the lane's own
+// inversion of z (binary GCD) -- one launch instead of double-and-add, batch
+// normalization and packing (the table's rows sit on the multiply's critical
+// path, and every lane's inversion runs at once).  The entries are other
+// representatives (< 2q) of the same affine values; the multiply's outputs are
+// canonical at the store, so its bits do not change.  `phi_rows`: the GLV
+// table, row 17 + i also gets phi(T[i]) = (beta x, y).
+__global__ void __launch_bounds__(64) k_g1_comb_entries(const uint64_t* __restrict__ bases,
+                                                        uint64_t* __restrict__ table_fl, int e0, int e1,
+                                                        int phi_rows) {
     __builtin_amdgcn_s_setprio(2);   // table work of a later part runs beside the multiply
     const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= e1) return;
     const int i = e / kCombEntries, d = e % kCombEntries + 1;
     Jac<Fq> b0;
     load_jac(b0, bases + kG1Jac * i);
-    if (fq_is_zero(b0.z)) {  // zero base: every multiple is this zero
-        store_jac(table_jac + (size_t)kG1Jac * e, b0);
+    uint32_t* o = reinterpret_cast<uint32_t*>(table_fl + (size_t)kFlPair * e);
+    uint32_t* op = o + 2 * kFlPair * kGlvWindows * kCombEntries;
+    if (fq_is_zero(b0.z)) {  // zero base: every entry marked, skipped by the multiply
+#pragma unroll
+        for (int k = 0; k < 28; k++) {
+            o[k] = kFlInfinity;
+            if (phi_rows) op[k] = kFlInfinity;
+        }
         return;
     }
-    // double-and-add from d's top bit on the lazy core (d < 2^8 < the order:
-    // no intermediate is zero)
+    // from d's top bit (d < 2^8 < the order: no intermediate is zero)
     const FlJac b = {fl_from_abi(b0.x), fl_from_abi(b0.y), fl_from_abi(b0.z)};
     FlJac acc = b;
     const int top = 31 - __builtin_clz(d);
@@ -145,36 +149,25 @@ __global__ void __launch_bounds__(64) k_g1_comb_fill(const uint64_t* __restrict_
         fl_jac_double(acc);
         if ((d >> bit) & 1) fl_jac_add(acc, b);
     }
-    fl_store_jac(table_jac + (size_t)kG1Jac * e, acc);
-}
-
-// normalized Jacobian table -> affine (x, y) in the lazy 28-bit core's
-// representation (fl.h: 14 limbs, R = 2^392), 28 u32 per entry
-__global__ void __launch_bounds__(64) k_g1_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table_fl,
-                                                     int e0, int e1, int phi_rows) {
-    __builtin_amdgcn_s_setprio(2);   // table work of a later part runs beside the multiply
-    const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= e1) return;
-    const F<1> x = fl_load(table_jac + (size_t)kG1Jac * e);
-    const F<1> y = fl_load(table_jac + (size_t)kG1Jac * e + 6);
-    Fq z;
-    fq_load(z, table_jac + (size_t)kG1Jac * e + 12);
-    const bool zero = fq_is_zero(z);  // e.g. every entry of a zero base: marked, skipped by the multiply
-    uint32_t* d = reinterpret_cast<uint32_t*>(table_fl + (size_t)kFlPair * e);
+    Fq zi;
+    fq_inv(zi, fl_to_abi(acc.z));
+    const F<1> zf = fl_from_abi(zi);
+    const F<1> zz = sqr(zf);
+    const F<1> x = mul(acc.x, zz);
+    const F<1> y = mul(acc.y, mul(zz, zf));
 #pragma unroll
-    for (int i = 0; i < 14; i++) {
-        d[i] = zero ? kFlInfinity : x.w[i];
-        d[14 + i] = zero ? kFlInfinity : y.w[i];
+    for (int k = 0; k < 14; k++) {
+        o[k] = x.w[k];
+        o[14 + k] = y.w[k];
     }
-    if (phi_rows) {  // GLV table: row 17 + i holds phi(T[i]) = (beta x, y)
+    if (phi_rows) {
         Fq beta;
         fq_load(beta, kGlvBeta);
         const F<1> bx = mul(x, fl_from_abi(beta));
-        uint32_t* dp = d + 2 * kFlPair * kGlvWindows * kCombEntries;
 #pragma unroll
-        for (int i = 0; i < 14; i++) {
-            dp[i] = zero ? kFlInfinity : bx.w[i];
-            dp[14 + i] = zero ? kFlInfinity : y.w[i];
+        for (int k = 0; k < 14; k++) {
+            op[k] = bx.w[k];
+            op[14 + k] = y.w[k];
         }
     }
 }
@@ -470,12 +463,6 @@ __global__ void __launch_bounds__(64) k_g1_fixed_base_ladder(const uint64_t* __r
 
 static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
-static hipError_t table_normalize(uint64_t* v, size_t n, hipStream_t stream) {
-    const size_t lanes = (n + kTableNormChunk - 1) / kTableNormChunk;
-    hipLaunchKernelGGL(k_g1_table_normalize, dim3(blocks_for(lanes, 64)), dim3(64), 0, stream, v, n);
-    return hipGetLastError();
-}
-
 hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const size_t lanes = (n + kNormChunk - 1) / kNormChunk;
@@ -484,13 +471,13 @@ hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream) 
 }
 
 size_t g1_comb_workspace_words() {
-    // bases, Jacobian table, then one u64 holding the GLV membership flag
-    return (size_t)kG1Jac * kCombWindows + (size_t)kG1Jac * kCombWindows * kCombEntries + 1;
+    // the chain's bases, then one u64 holding the GLV membership flag
+    return (size_t)kG1Jac * kCombWindows + 1;
 }
 size_t g1_comb_table_words() { return (size_t)kFlPair * kTableRows * kCombEntries; }
 
 static uint32_t* glv_flag(const uint64_t* workspace) {
-    const uint64_t* f = workspace + (size_t)kG1Jac * kCombWindows + (size_t)kG1Jac * kCombWindows * kCombEntries;
+    const uint64_t* f = workspace + (size_t)kG1Jac * kCombWindows;
     return reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(f));
 }
 
@@ -498,14 +485,10 @@ static uint32_t* glv_flag(const uint64_t* workspace) {
 static hipError_t comb_table_range(const uint64_t* base, uint64_t* table_fl, uint64_t* workspace, int w0, int w1,
                                    int phi_rows, hipStream_t stream) {
     uint64_t* bases = workspace;
-    uint64_t* table_jac = workspace + (size_t)kG1Jac * kCombWindows;
     const int e0 = w0 * kCombEntries, e1 = w1 * kCombEntries;
     hipLaunchKernelGGL(k_g1_comb_bases, dim3(1), dim3(64), 0, stream, base, bases, w0, w1);
-    hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, stream, bases, table_jac, e0, e1);
-    const hipError_t e = table_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, stream, table_jac, table_fl, e0,
-                       e1, phi_rows);
+    hipLaunchKernelGGL(k_g1_comb_entries, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, stream, bases, table_fl, e0, e1,
+                       phi_rows);
     return hipGetLastError();
 }
 
@@ -605,7 +588,6 @@ hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, u
     for (; made < 2 + 2 * parts; made++)
         if (!ck(hipEventCreateWithFlags(&ev[made], hipEventDisableTiming))) break;
     uint64_t* bases = workspace;
-    uint64_t* table_jac = workspace + (size_t)kG1Jac * kCombWindows;
     uint32_t* flag = glv_flag(workspace);
     if (ck(hipEventRecord(ev[0], stream)) && ck(hipStreamWaitEvent(chain, ev[0], 0)) &&
         ck(hipStreamWaitEvent(fill, ev[0], 0)) && ck(hipStreamWaitEvent(check, ev[0], 0))) {
@@ -618,11 +600,7 @@ hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, u
         for (int p = 0; p < parts && err == hipSuccess; p++) {
             const int e0 = wb[p] * kCombEntries, e1 = wb[p + 1] * kCombEntries;
             if (!ck(hipStreamWaitEvent(fill, ev[1 + 2 * p], 0))) break;
-            hipLaunchKernelGGL(k_g1_comb_fill, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, fill, bases, table_jac, e0,
-                               e1);
-            if (!ck(hipGetLastError()) || !ck(table_normalize(table_jac + (size_t)kG1Jac * e0, e1 - e0, fill)))
-                break;
-            hipLaunchKernelGGL(k_g1_comb_pack, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, fill, table_jac, table_fl,
+            hipLaunchKernelGGL(k_g1_comb_entries, dim3(blocks_for(e1 - e0, 64)), dim3(64), 0, fill, bases, table_fl,
                                e0, e1, 1);
             ck(hipGetLastError()) && ck(hipEventRecord(ev[2 + 2 * p], fill));
         }
