@@ -557,26 +557,30 @@ hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, u
     hipStream_t chain = side[dev][0], fill = side[dev][1], check = side[dev][2], mul = stream;
     static const bool serial = getenv("PA_COMB_SERIAL") && atoi(getenv("PA_COMB_SERIAL")) != 0;
     if (serial) chain = fill = check = stream;   // measurement only: every kernel in order on the caller's stream
-    // parts of the 17 GLV windows (PA_COMB_PARTS, 1..8; PA_COMB_FIRST windows in
-    // part 0): 2 parts split 5 + 12 measured best (profiles/r02_glv_comb.txt) --
-    // a short first part starts the multiply early, a long second one hides the
-    // rest of the chain and its rows behind the first part's multiply
-    static const int parts = [] {
-        const char* v = getenv("PA_COMB_PARTS");
-        const int k = v ? atoi(v) : 2;
-        return k < 1 ? 1 : (k > 8 ? 8 : k);
+    // window boundaries of the parts (PA_COMB_SPLIT, e.g. "5" or "2,7": the
+    // first window of every part after the first); "5" (5 + 12 windows)
+    // measured best of the even and two-part splits (profiles/r02_glv_comb.txt)
+    // -- a short first part starts the multiply early, a long second one hides
+    // the rest of the chain and its rows behind the first part's multiply
+    struct Split {
+        int parts = 1, wb[9] = {0};
+    };
+    static const Split split = [] {
+        Split r;
+        const char* v = getenv("PA_COMB_SPLIT");
+        const char* t = v ? v : "5";
+        while (*t && r.parts < 8) {
+            char* end = nullptr;
+            const long w = strtol(t, &end, 10);
+            if (end == t) break;
+            if (w > r.wb[r.parts - 1] && w < kGlvWindows) r.wb[r.parts++] = (int)w;
+            t = *end == ',' ? end + 1 : end;
+        }
+        r.wb[r.parts] = kGlvWindows;
+        return r;
     }();
-    static const int first_w = [] {
-        const char* v = getenv("PA_COMB_FIRST");
-        return v ? atoi(v) : 5;
-    }();
-    int wb[9];
-    for (int p = 0; p <= parts; p++) wb[p] = (kGlvWindows * p + parts - 1) / parts;
-    if (parts > 1 && first_w > 0 && first_w < kGlvWindows - (parts - 2)) {
-        wb[1] = first_w;
-        for (int p = 2; p < parts; p++) wb[p] = first_w + ((kGlvWindows - first_w) * (p - 1) + parts - 2) / (parts - 1);
-    }
-    wb[parts] = kGlvWindows;
+    const int parts = split.parts;
+    const int* wb = split.wb;
     // ev[0]: start; ev[1 + 2p]: chain part p done; ev[2 + 2p]: rows of part p done; ev[1 + 2 parts]: check done
     hipEvent_t ev[2 + 2 * 8] = {};
     int made = 0;
