@@ -106,8 +106,13 @@ static inline uint32_t msm_window_bits(size_t n) {
     int lg = 0;
     while (lg < 40 && ((size_t)1 << (lg + 1)) <= n) lg++;
     int c = lg - 3;
+    static const int cmax = [] {   // A/B knob: PA_MSM_CMAX (default 16)
+        const char* v = getenv("PA_MSM_CMAX");
+        const int k = v ? atoi(v) : 16;
+        return k < 4 ? 4 : (k > 20 ? 20 : k);
+    }();
     if (c < 4) c = 4;
-    if (c > 16) c = 16;
+    if (c > cmax) c = cmax;
     return (uint32_t)c;
 }
 
@@ -120,7 +125,12 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.c = msm_window_bits(n);
     p.W = (257 + p.c - 1) / p.c;
     p.B = 1u << (p.c - 1);
-    p.L = p.B < 8 ? p.B : 8;  // short segments: the running sums are a latency chain per lane
+    static const uint32_t seg = [] {   // A/B knob: PA_MSM_SEG (default 8)
+        const char* v = getenv("PA_MSM_SEG");
+        const int k = v ? atoi(v) : 8;
+        return (uint32_t)(k == 2 || k == 4 || k == 16 || k == 32 ? k : 8);
+    }();
+    p.L = p.B < seg ? p.B : seg;  // short segments: the running sums are a latency chain per lane
     p.items = (size_t)p.W * n;
     const uint64_t sentinel = (uint64_t)p.W * p.B;
     p.key_bits = 1;
@@ -619,7 +629,13 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     uint64_t* src = segs;
     uint64_t* dst = tmp;
     while (count > 1) {
-        const uint32_t group = 4;  // shallow chains: 4 additions per level
+        // shallow chains: 2 additions per level, 2 / 3 / 4 / 8 measured 141.6 / 140.2 / 138.1 / 133.5 M
+        // terms/s at 2^20 (profiles/r02_msm_tuning.txt); PA_MSM_GROUP to A/B
+        static const uint32_t group = [] {
+            const char* v = getenv("PA_MSM_GROUP");
+            const int g = v ? atoi(v) : 2;
+            return (uint32_t)(g < 2 ? 2 : (g > 16 ? 16 : g));
+        }();
         const uint32_t gpw = (count + group - 1) / group;
         hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks((size_t)p.W * gpw, 64)), dim3(64), 0, s, src, count,
                            group, gpw, p.W, dst);
