@@ -300,6 +300,10 @@ def main():
     if rc is not None:
         sys.exit(rc)
     ws, rank, local = dist_env()
+    # under torch.distributed.run (WORLD_SIZE set) every rank joins the RCCL
+    # group and gathers, even at one rank: `torch.distributed.run
+    # --nproc-per-node 1 bench.py` runs the sharded path on a one-GPU box
+    dist_on = ws > 1 or "WORLD_SIZE" in os.environ
     if ws != args.gpus:
         print("bench.py: WORLD_SIZE=%d but --gpus %d; timing %d ranks" % (ws, args.gpus, ws), file=sys.stderr)
     if args.cpu_stub:
@@ -314,11 +318,11 @@ def main():
     if os.environ.get("PA_PAIRING_KERNEL"):
         pairing_amd.set_pairing_kernel(int(os.environ["PA_PAIRING_KERNEL"]))
     dev = torch.device("cuda", local)
-    if ws > 1:
+    if dist_on:
         dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
-        if ws > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -344,7 +348,7 @@ def main():
             pdev.final_exponentiation(scratch, out, None, stream)
             if timed:
                 ev[2].record(stream)
-            if ws > 1:
+            if dist_on:
                 # the path's one exchange: every shard's Fq12 results to rank 0 (RCCL over xGMI)
                 gather_rows_to_root(out, ws * n)
     elif args.workload == "wnaf":
@@ -520,7 +524,7 @@ def main():
             k_ms["b"].append(e[1].elapsed_time(e[2]))
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if ws > 1:
+    if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -536,7 +540,7 @@ def main():
             config = {"workload": "bls12_381 e(P_i,Q_i) batch (fused G2 prepare + Miller loop + final exp)",
                       "kernel_variant": ["gen", "gen2", "coop", "gen"][int(os.environ.get("PA_PAIRING_KERNEL", "0"))],
                       "batch_per_gpu": n, "global_batch": n * ws, "parallelism": "shard%d+rccl_gather" % ws
-                      if ws > 1 else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
+                      if dist_on else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}
         elif args.workload == "wnaf":
             tot_ms, norm_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
@@ -690,7 +694,7 @@ def main():
                 "data": "synthetic (seeded random points k*G)", "config": config,
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
-    if ws > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

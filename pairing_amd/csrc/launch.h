@@ -74,6 +74,9 @@ const char* gen_error_detail();
 // event, so concurrent launches on different streams never share one.
 hipError_t launch_miller_loop_gen(int lanes, const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                   hipStream_t stream);
+// in-place Fq inversion (binary GCD) of Fq 0 of n records `stride` u64 apart
+// (the split final exponentiation's middle step; zero stays zero)
+hipError_t launch_fq_inv_strided(uint64_t* v, size_t stride, size_t n, hipStream_t stream);
 hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
                                 hipStream_t stream);
 // Cooperative kernels (kernels_coop.hip): one WAVE per pairing, for small

@@ -222,3 +222,28 @@ def test_g1_glv_stages_device_match_oracle(gpu, oracle, which):
     assert oracle.g1_eq(np.ascontiguousarray(got1[idx]), exp).all()
     assert oracle.g1_eq(np.ascontiguousarray(got2[idx]), exp).all()
     np.testing.assert_array_equal(oracle.g1_batch_normalization(got1), oracle.g1_batch_normalization(got2))
+
+
+def test_final_exp_split_and_in_place_agree(gpu, oracle):
+    """out apart from in runs the split final exponentiation (norm kernel,
+    binary-GCD inversion, rest); out == in runs the one-kernel form.  Both
+    equal the oracle, including f == 0 (reference None: zero, ok = 0)."""
+    import torch
+    import pairing_amd.device as pdev
+    n = 2300        # above the cooperative kernels' batch limit (PA_COOP_MAX 2048)
+    f = _field_rows(41, n * 12, 6, FQ_TOP, []).reshape(n, 72)
+    f[7] = 0
+    exp, ok_exp = oracle.final_exponentiation(f, _threads())
+    d_in = _dev(f)
+    out = pdev.empty_records(n, 72, "cuda:0")
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    pdev.final_exponentiation(d_in, out, ok)
+    d_same = _dev(f)
+    ok2 = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    pdev.final_exponentiation(d_same, d_same, ok2)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(out), exp)
+    np.testing.assert_array_equal(_host(d_same), exp)
+    np.testing.assert_array_equal(ok.cpu().numpy(), np.asarray(ok_exp, np.uint8))
+    np.testing.assert_array_equal(ok2.cpu().numpy(), np.asarray(ok_exp, np.uint8))
+    assert ok.cpu().numpy()[7] == 0

@@ -201,3 +201,40 @@ def test_fuse_adds_preserves_values():
     Q = dsl.Q
     assert want[0] == (ins[0] + ins[1] + ins[2]) % Q
     assert want[1] == (4 * ins[3] + ins[0] + ins[1] + ins[2]) % Q
+
+
+# ---- round 2: the final exponentiation split around a binary-GCD inversion ----
+def test_dsl_split_final_exp_composes(ref_pair):
+    """norm program -> Fq inverse (R = 2^384 Montgomery records) -> inv program
+    equals the one-kernel final exponentiation and the oracle (mod.rs:104-160)"""
+    _, ml, fe = ref_pair
+    ins = {k: ml[k] for k in range(12)}
+    nrm = dsl.evaluate(kernels.final_exp_prog(lazy="sq", split="norm"), dict(ins))
+    assert sorted(nrm) == [0] and nrm[0] != 0
+    r = 1 << 384
+    ins[12] = r * r * pow(nrm[0], -1, dsl.Q) % dsl.Q
+    out = dsl.evaluate(kernels.final_exp_prog(lazy="sq", split="inv"), ins)
+    assert [out[k] for k in range(12)] == fe
+
+
+def test_split_final_exp_saves_the_fermat_chain():
+    import random
+    g = random.Random(2)
+    ins = {k: g.randrange(dsl.Q) for k in range(13)}
+    macs = {}
+    for split in (None, "norm", "inv"):
+        st = dsl.Stats()
+        dsl.evaluate(kernels.final_exp_prog(lazy="sq", split=split), dict(ins), st)
+        macs[split] = build_gen.macs(st.counts)
+    # the 463-product Fermat chain (~181 k limb MACs) leaves; the norm kernel is ~1 % of the FE
+    assert macs[None] - macs["inv"] > 170000
+    assert macs["norm"] < 0.01 * macs[None]
+
+
+def test_sim_fe_norm_kernel():
+    assert sim_check.check("fen", debug=True)
+
+
+@pytest.mark.slow
+def test_sim_fe_inv_kernel():
+    assert sim_check.check("fei", debug=True)

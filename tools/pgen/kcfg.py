@@ -168,7 +168,9 @@ class MillerLoopCfg(KernelCfg):
 
 class FinalExpCfg(KernelCfg):
     name = "pa_gen_final_exp"
-    records = {k: (0, 576, 48 * k) for k in range(12)}
+    # slot 12 (split final exponentiation, "inv" program): the inverted norm
+    # that the "norm" program stored as Fq 0 of the out record
+    records = {**{k: (0, 576, 48 * k) for k in range(12)}, 12: (1, 576, 0)}
     out_arg = 1
 
     def prologue_masks(self, em, code):

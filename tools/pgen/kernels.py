@@ -199,9 +199,15 @@ def exp_by_x(p, T, V, f, x, tag):
     return T.conj12(V.get12(res))
 
 
-def final_exp_prog(lanes=1, lazy=False, tower_cls=None):
+def final_exp_prog(lanes=1, lazy=False, tower_cls=None, split=None):
     """lazy: False (Tower), True (TowerLazy) or "sq" (TowerLazySq);
-    tower_cls overrides the tower class (coop.py: inversion as one op)"""
+    tower_cls overrides the tower class (coop.py: inversion as one op).
+    split (one lane): the final exponentiation in two kernels around a
+    base-field inversion run elsewhere (binary GCD, bgcd.h) instead of the
+    463-product Fermat chain -- "norm": load f, compute the Fq value that
+    f^-1 needs inverted (fq12.rs:132-148 -> fq6.rs:250-301 -> fq2.rs:138-155)
+    and store it as output slot 0; "inv": the whole final exponentiation with
+    that value's inverse read from input slot 12"""
     p = Prog("final_exp" if lanes == 1 else "final_exp2", lanes,
              use_norm=_norm(lanes) and tower_cls is None)
     if tower_cls is not None:
@@ -212,6 +218,17 @@ def final_exp_prog(lanes=1, lazy=False, tower_cls=None):
         T = {False: Tower, True: TowerLazy, "sq": TowerLazySq}[lazy](p)
     V = _Vars(p, lanes)
     f = V.load12()
+    if split is not None:
+        assert lanes == 1 and split in ("norm", "inv")
+        T.fe_split = split
+    if split == "norm":
+        from tower import NormStop
+        try:
+            T.inv12(f)
+        except NormStop as stop:
+            p.store(0, stop.args[0])
+            return p
+        raise AssertionError("inv12 did not reach the base-field inversion")
     # mod.rs:104-160
     f1 = T.conj12(f)
     f2 = T.inv12(f)

@@ -35,12 +35,16 @@ def check(which, seed=5, lane=3, debug=True):
         sim_lane = 2 * lane
     else:
         sim_lane = lane
-    if which in ("small", "fe", "fe2", "fez"):
+    if which in ("small", "fe", "fe2", "fez", "fen", "fei"):
         ins = [rng.randrange(dsl.Q) for _ in range(12)]
         rec = [0] * (72 * lane) + words(ins)
-        want = dsl.evaluate(prog, {k: ins[k] for k in range(12)}, trace=trace)
+        if which == "fei":   # slot 12: Fq 0 of the out record (any value for the check)
+            ins.append(rng.randrange(dsl.Q))
+        want = dsl.evaluate(prog, {k: ins[k] for k in range(len(ins))}, trace=trace)
         args = [IN, OUT, AUX, lane + 1, WS]
         bufs = {IN: rec}
+        if which == "fei":
+            bufs[OUT] = [0] * (72 * lane) + words(ins[12:])
     else:
         # any field values (the loop does not care whether they are on the curve)
         ins = [rng.randrange(dsl.Q) for _ in range(6)]
@@ -52,10 +56,10 @@ def check(which, seed=5, lane=3, debug=True):
     t = time.time()
     sm = sim.run_lane(code, args, bufs, lane=sim_lane, trace=trace if debug else None, pair=pair)
     got = []
-    for k in range(12):
+    for k in sorted(want):
         base = OUT + 576 * lane + 48 * k
         got.append(sum(sm.mem.get(base + 4 * j, 0) << (32 * j) for j in range(12)))
-    ok = got == [want[k] for k in range(12)]
+    ok = got == [want[k] for k in sorted(want)]
     print("%s lane %d: %s (%d instructions simulated, %.1fs)" % (which, lane, "OK" if ok else "MISMATCH",
                                                               sm.count, time.time() - t))
     if os.environ.get("PGEN_HIST"):

@@ -22,7 +22,17 @@ def _frob_consts():
     return g.FROB_FQ6_C1, g.FROB_FQ6_C2, g.FROB_FQ12_C1
 
 
+class NormStop(Exception):
+    """raised by inv2 in a norm-only program (Tower.fe_split == "norm"):
+    args[0] is the Fq value the base-field inversion would invert"""
+
+
 class Tower:
+    # split final exponentiation (kernels.final_exp_prog(split=...)): "norm"
+    # stops at the base-field value to invert (NormStop), "inv" reads its
+    # inverse from input slot 12 instead of running the Fermat chain
+    fe_split = None
+
     def __init__(self, p):
         self.p = p
 
@@ -251,7 +261,13 @@ class Tower:
 
     def inv2(self, a, tag):  # fq2.rs:138-155
         p = self.p
-        t = self.inv_fq(p.sop(a[0], a[0], a[1], a[1]), tag)
+        if self.fe_split == "inv":
+            t = p.load(12)
+        else:
+            n = p.sop(a[0], a[0], a[1], a[1])
+            if self.fe_split == "norm":
+                raise NormStop(n)
+            t = self.inv_fq(n, tag)
         return (p.mul(a[0], t), p.mul(p.neg(a[1]), t))
 
     def inv6(self, a, tag):  # fq6.rs:250-301
