@@ -596,7 +596,11 @@ def main():
         tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tr_path):
             with open(tr_path) as f:
-                traffic = json.load(f).get(dom_name)
+                # the split final exponentiation has its own entry (the three
+                # kernels' bytes per step); null until measured
+                fe_split = args.workload == "pairing" and dom_name == "final_exponentiation" and \
+                    os.environ.get("PA_FE_SPLIT", "1") != "0"
+                traffic = json.load(f).get(dom_name + ("_split" if fe_split else ""))
         roof = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "bytes_per_unit": dom_bytes, "avg_launch_ms": round(dom_ms, 4)}
@@ -614,7 +618,15 @@ def main():
             # kept alongside
             with open(work_path) as f:
                 work = json.load(f)
-            macs = work["final_exp" if dom_name == "final_exponentiation" else "miller_loop"]["limb_macs"]
+            # the final exponentiation step is, by default, the split form
+            # (gen_launch.hip): norm kernel + binary-GCD inversion + the rest;
+            # its MACs / instructions are the two generated kernels' (the
+            # inversion kernel's integer work is not limb MACs)
+            split = os.environ.get("PA_FE_SPLIT", "1") != "0" and "fe_inv" in work
+            wk = (work["miller_loop"] if dom_name != "final_exponentiation" else
+                  {k: work["fe_norm"][k] + work["fe_inv"][k] for k in ("limb_macs", "instructions")}
+                  if split else work["final_exp"])
+            macs = wk["limb_macs"]
             mac_rate = macs * n / (dom_ms * 1e-3) / 1e12
             roof = {"kernel": dom_name, "bound": "valu", "achieved": round(mac_rate, 3),
                     "peak": round(VALU_MAC_PEAK_T, 3), "unit": "T limb-MAC/s (28x28-bit v_mad_u64_u32)",
@@ -622,7 +634,7 @@ def main():
                     "avg_launch_ms": round(dom_ms, 4),
                     "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS,
                             "bytes_per_unit": dom_bytes}}
-            instr = work["final_exp" if dom_name == "final_exponentiation" else "miller_loop"].get("instructions")
+            instr = wk.get("instructions")
             if instr:
                 rate = instr * n / (dom_ms * 1e-3) / 1e12
                 roof["issue"] = {"achieved": round(rate, 3), "peak": round(ISSUE_PEAK_T, 3),

@@ -46,6 +46,8 @@ for step in "$@"; do
         proffq) run prof_fq 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fq -o run -- python bench.py --workload fq_mul --steps 10 --warmup 2 --no-cpu-baseline ;;
         pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline &&
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+        pmccsv) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline &&
+                run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         pmcsq) run pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES -d gpurun_out/pmc_sq1 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline &&
                run pmc_sq2 600 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR -d gpurun_out/pmc_sq2 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
         pmcsq4) run pmc4_sq1 300 env PA_PAIRING_KERNEL=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES -d gpurun_out/pmc4_sq1 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline &&

@@ -142,7 +142,10 @@ def write_work_json(outdir):
     import random
     rng = random.Random(1)
     out = {}
-    for key, name, nin in (("ml", "miller_loop", 6), ("fe", "final_exp", 12)):
+    for key, name, nin in (("ml", "miller_loop", 6), ("fe", "final_exp", 12), ("fen", "fe_norm", 12),
+                           ("fei", "fe_inv", 13)):
+        if key in ("fen", "fei") and not PROGRAMS[key].cache:
+            continue
         prog = PROGRAMS[key]()[0]
         st = dsl.Stats()
         dsl.evaluate(prog, {k: rng.randrange(dsl.Q) for k in range(nin)}, st)
