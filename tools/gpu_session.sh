@@ -28,6 +28,7 @@ for step in "$@"; do
         sizetests) run pytest_sizes 600 python -u -m pytest tests/test_bench_sizes.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
+        verifybench) run bench_verify 300 python bench.py --workload verify --steps 10 --warmup 2 --no-cpu-baseline ;;
         benchnosplit) run bench_nosplit 600 env PA_FE_SPLIT=0 python bench.py --no-cpu-baseline ;;
         rcclbench) run bench_rccl1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --no-cpu-baseline ;;
         benchgen2) run bench_gen2 600 env PA_PAIRING_KERNEL=1 python bench.py --no-cpu-baseline ;;
