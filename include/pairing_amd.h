@@ -321,6 +321,13 @@ int pa_g1_into_affine_batch_device(const pa_g1 *a, pa_g1_affine *out, size_t n, 
 int pa_g2_into_affine_batch_device(const pa_g2 *a, pa_g2_affine *out, size_t n, void *stream);
 int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
                                       void *stream);
+/* final_exponentiation (mod.rs:104-160) on device records.  With `out` apart
+ * from `in`, batches above PA_COOP_MAX run in three launches on `stream`: the
+ * Fq value f^-1 needs inverted is written to Fq 0 of each `out` record,
+ * inverted there by binary GCD, and read back by the rest of the
+ * exponentiation, which then overwrites `out`; `in` is left unchanged.
+ * in == out (or overlapping) runs the one-kernel form in place.  Same bits
+ * either way; PA_FE_SPLIT=0 in the environment forces the one-kernel form. */
 int pa_final_exponentiation_batch_device(const pa_fq12 *in, pa_fq12 *out, uint8_t *ok, size_t n, void *stream);
 /* pa_multi_pairing on device memory (the verifier's check without host copies); `work` holds n
  * pa_fq12 (the per-pair Miller values, reduced in place to their product) */
