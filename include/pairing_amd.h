@@ -172,6 +172,11 @@ int pa_g2_into_affine_batch(const pa_g2 *a, pa_g2_affine *out, size_t n);
 /* CurveAffine::into_projective, ec.rs:570-582 */
 int pa_g1_into_projective_batch(const pa_g1_affine *a, pa_g1 *out, size_t n);
 int pa_g2_into_projective_batch(const pa_g2_affine *a, pa_g2 *out, size_t n);
+/* PartialEq for the projective types, ec.rs:45-85 (representation independent:
+ * X1 Z2^2 == X2 Z1^2 and Y1 Z2^3 == Y2 Z1^3; zero equals only zero):
+ * eq[i] = 1 if a[i] == b[i], else 0 */
+int pa_g1_eq_batch(const pa_g1 *a, const pa_g1 *b, uint8_t *eq, size_t n);
+int pa_g2_eq_batch(const pa_g2 *a, const pa_g2 *b, uint8_t *eq, size_t n);
 /* G2 CurveProjective::batch_normalization, ec.rs:246-294, in place */
 int pa_g2_batch_normalization(pa_g2 *v, size_t n);
 /* G2 Wnaf::new().base(*base, n).scalar(scalars[i]) (wnaf.rs:93-107, 169-178):
@@ -319,6 +324,8 @@ int pa_g1_add_mixed_batch_device(const pa_g1 *a, const pa_g1_affine *b, pa_g1 *o
 int pa_g2_add_mixed_batch_device(const pa_g2 *a, const pa_g2_affine *b, pa_g2 *out, size_t n, void *stream);
 int pa_g1_into_affine_batch_device(const pa_g1 *a, pa_g1_affine *out, size_t n, void *stream);
 int pa_g2_into_affine_batch_device(const pa_g2 *a, pa_g2_affine *out, size_t n, void *stream);
+int pa_g1_eq_batch_device(const pa_g1 *a, const pa_g1 *b, uint8_t *eq, size_t n, void *stream);
+int pa_g2_eq_batch_device(const pa_g2 *a, const pa_g2 *b, uint8_t *eq, size_t n, void *stream);
 int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
                                       void *stream);
 /* final_exponentiation (mod.rs:104-160) on device records.  With `out` apart

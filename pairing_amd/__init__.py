@@ -32,7 +32,7 @@ __all__ = [
     "fr_mul", "fr_square", "fr_add", "fr_sub", "fr_double", "fr_negate", "fr_inverse",
     "fr_from_repr", "fr_into_repr", "fr_pow", "fr_legendre", "fr_sqrt",
     "g1_affine_mul", "g2_affine_mul", "g1_mul_assign", "g2_mul_assign", "g1_multiexp", "g2_multiexp",
-    "g1_double", "g2_double", "g1_add", "g2_add", "g1_add_mixed", "g2_add_mixed", "g1_negate", "g2_negate",
+    "g1_eq", "g2_eq", "g1_double", "g2_double", "g1_add", "g2_add", "g1_add_mixed", "g2_add_mixed", "g1_negate", "g2_negate",
     "g1_sub", "g2_sub", "g1_into_affine", "g2_into_affine", "g1_into_projective", "g2_into_projective",
     "g2_batch_normalization", "g2_wnaf_fixed_base",
     "g1_recommended_wnaf_for_scalar", "g2_recommended_wnaf_for_scalar",
@@ -496,6 +496,26 @@ def _group_binary(group, op, a, b, b_width):
     out = np.zeros_like(a)
     call("pa_g%d_%s_batch" % (group, op), ptr(a), ptr(b), ptr(out), a.shape[0])
     return out
+
+
+def _group_eq(group, a, b):
+    a = as_rows(a, _JW[group], "a")
+    b = as_rows(b, _JW[group], "b")
+    if a.shape[0] != b.shape[0]:
+        raise ValueError("operand lengths differ: %d vs %d" % (a.shape[0], b.shape[0]))
+    out = np.zeros(a.shape[0], np.uint8)
+    call("pa_g%d_eq_batch" % group, ptr(a), ptr(b), ptr(out), a.shape[0])
+    return out.astype(bool)
+
+
+def g1_eq(a, b):
+    """PartialEq for G1 (ec.rs:45-85): a[i] == b[i] as points, per item."""
+    return _group_eq(1, a, b)
+
+
+def g2_eq(a, b):
+    """PartialEq for G2 (ec.rs:45-85): a[i] == b[i] as points, per item."""
+    return _group_eq(2, a, b)
 
 
 def g1_double(a):

@@ -1011,10 +1011,13 @@ constexpr size_t jac_bytes(int group) { return group == 1 ? sizeof(pa_g1) : size
 constexpr size_t aff_bytes(int group) { return group == 1 ? sizeof(pa_g1_affine) : sizeof(pa_g2_affine); }
 size_t op_in_bytes(int group, int op) { return op == pa::GROUP_FROM_AFFINE ? aff_bytes(group) : jac_bytes(group); }
 size_t op_b_bytes(int group, int op) {
-    if (op == pa::GROUP_ADD || op == pa::GROUP_SUB) return jac_bytes(group);
+    if (op == pa::GROUP_ADD || op == pa::GROUP_SUB || op == pa::GROUP_EQ) return jac_bytes(group);
     return op == pa::GROUP_ADD_MIXED ? aff_bytes(group) : 0;
 }
-size_t op_out_bytes(int group, int op) { return op == pa::GROUP_INTO_AFFINE ? aff_bytes(group) : jac_bytes(group); }
+size_t op_out_bytes(int group, int op) {
+    if (op == pa::GROUP_EQ) return 1;
+    return op == pa::GROUP_INTO_AFFINE ? aff_bytes(group) : jac_bytes(group);
+}
 
 int host_group_op(int group, int op, const void* a, const void* b, void* out, size_t n) {
     if (n == 0) return PA_OK;
@@ -1084,6 +1087,12 @@ int window_for_count(size_t n, const size_t* rec, int m) {
     }                                                                                                           \
     int pa_g##G##_into_affine_batch_device(const JAC* a, AFF* out, size_t n, void* stream) {                    \
         return device_group_op(G, pa::GROUP_INTO_AFFINE, a, nullptr, out, n, stream);                           \
+    }                                                                                                           \
+    int pa_g##G##_eq_batch(const JAC* a, const JAC* b, uint8_t* eq, size_t n) {                                 \
+        return host_group_op(G, pa::GROUP_EQ, a, b, eq, n);                                                     \
+    }                                                                                                           \
+    int pa_g##G##_eq_batch_device(const JAC* a, const JAC* b, uint8_t* eq, size_t n, void* stream) {            \
+        return device_group_op(G, pa::GROUP_EQ, a, b, eq, n, stream);                                           \
     }
 
 PA_GROUP_ENTRIES(1, pa_g1, pa_g1_affine)

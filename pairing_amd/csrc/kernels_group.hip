@@ -2,7 +2,8 @@
 // (src/lib.rs:114-234, the `curve_impl!` macro ec.rs:1-621 instantiated for
 // both groups):
 //   k_group_op          double / add_assign / add_assign_mixed / negate /
-//                       sub_assign / into_affine / into_projective, one item
+//                       sub_assign / into_affine / into_projective /
+//                       PartialEq (a byte per item), one item
 //                       per lane, the reference's exact formula sequence
 //                       (curve.h) so Jacobian words are bit-identical
 //   k_batch_normalize   batch_normalization (ec.rs:246-294) for G2:
@@ -49,6 +50,28 @@ __global__ void __launch_bounds__(64) k_group_op(const uint64_t* __restrict__ a,
         Aff<F> r;
         jac_to_affine(r, p);
         store_aff(out + AW * i, r);
+    } else if constexpr (OP == GROUP_EQ) {
+        // ec.rs:45-85: X1 Z2^2 == X2 Z1^2 and Y1 Z2^3 == Y2 Z1^3; zero equals only zero
+        Jac<F> p, q;
+        load_jac(p, a + JW * i);
+        load_jac(q, b + JW * i);
+        bool eqv;
+        if (jac_is_zero(p) || jac_is_zero(q)) {
+            eqv = jac_is_zero(p) && jac_is_zero(q);
+        } else {
+            F z1, z2, t1, t2;
+            sqr(z1, p.z);
+            sqr(z2, q.z);
+            mul(t1, p.x, z2);
+            mul(t2, q.x, z1);
+            eqv = eq(t1, t2);
+            mul(z1, z1, p.z);
+            mul(z2, z2, q.z);
+            mul(z2, z2, p.y);
+            mul(z1, z1, q.y);
+            eqv = eqv && eq(z1, z2);
+        }
+        reinterpret_cast<uint8_t*>(out)[i] = eqv ? 1 : 0;
     } else if constexpr (OP == GROUP_FROM_AFFINE) {
         Aff<F> p;
         load_aff(p, a + AW * i);
@@ -87,6 +110,7 @@ hipError_t group_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out,
         case GROUP_SUB: hipLaunchKernelGGL((k_group_op<G, GROUP_SUB>), g, bl, 0, s, a, b, out, n); break;
         case GROUP_INTO_AFFINE: hipLaunchKernelGGL((k_group_op<G, GROUP_INTO_AFFINE>), g, bl, 0, s, a, b, out, n); break;
         case GROUP_FROM_AFFINE: hipLaunchKernelGGL((k_group_op<G, GROUP_FROM_AFFINE>), g, bl, 0, s, a, b, out, n); break;
+        case GROUP_EQ: hipLaunchKernelGGL((k_group_op<G, GROUP_EQ>), g, bl, 0, s, a, b, out, n); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -126,6 +126,7 @@ enum GroupOp : int {
     GROUP_SUB,
     GROUP_INTO_AFFINE,
     GROUP_FROM_AFFINE,
+    GROUP_EQ,   // PartialEq (ec.rs:45-85): `out` is one byte per item, 1 = equal
 };
 hipError_t launch_group_op(int group, int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
                            hipStream_t stream);

@@ -99,6 +99,30 @@ def test_group_law_bit_exact(gpu, oracle, group):
     assert eq(G("add")(a, b), G("add")(b, a)).all()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", [1, 2])
+def test_partial_eq_matches_reference(gpu, oracle, group):
+    """PartialEq (ec.rs:45-85) per item: the same point in two Jacobian
+    representations, a point and its negation (same X Z^-2, other Y), zero vs
+    zero (garbage x, y), zero vs nonzero, unrelated points"""
+    n = 130
+    a, _ = _jacobian(oracle, group, 90 + group, n)
+    fw = 6 if group == 1 else 12
+    to_aff, from_aff, add, eq = (oracle.g1_into_affine, oracle.g1_from_affine, oracle.g1_add, oracle.g1_eq) \
+        if group == 1 else (oracle.g2_into_affine, oracle.g2_from_affine, oracle.g2_add, oracle.g2_eq)
+    b = from_aff(to_aff(a))                          # same points, Z = 1 (zero stays zero)
+    b[10:20] = _neg_rows_nonzero(a[10:20], fw)       # negations
+    b[20:30] = add(a[20:30], a[30:40])               # other points
+    b[40] = a[1]                                     # zero vs zero: two garbage encodings
+    b[40, :2 * fw] = np.uint64(5)
+    b[41] = a[1]                                     # zero vs nonzero
+    got = getattr(gpu, "g%d_eq" % group)(a, b)
+    want = eq(a, b)
+    np.testing.assert_array_equal(got, want)
+    assert want[:10].all() and not want[10:30].any() and want[40] and not want[41]
+    assert want[1] and want[n // 3]                  # a zero against its own copy
+
+
 def _neg_rows_nonzero(rows, fw):
     out = rows.copy()
     nz = rows[:, 2 * fw:3 * fw].any(axis=1)
