@@ -416,6 +416,7 @@ template <> struct GroupAbi<1> {
     static constexpr auto sub = &pa_g1_sub_batch;
     static constexpr auto to_affine = &pa_g1_into_affine_batch;
     static constexpr auto from_affine = &pa_g1_into_projective_batch;
+    static constexpr auto eq = &pa_g1_eq_batch;
     static constexpr auto normalize = &pa_g1_batch_normalization;
     static constexpr auto mul_assign = &pa_g1_mul_assign_batch;
     static constexpr auto affine_mul = &pa_g1_affine_mul_batch;
@@ -436,6 +437,7 @@ template <> struct GroupAbi<2> {
     static constexpr auto sub = &pa_g2_sub_batch;
     static constexpr auto to_affine = &pa_g2_into_affine_batch;
     static constexpr auto from_affine = &pa_g2_into_projective_batch;
+    static constexpr auto eq = &pa_g2_eq_batch;
     static constexpr auto normalize = &pa_g2_batch_normalization;
     static constexpr auto mul_assign = &pa_g2_mul_assign_batch;
     static constexpr auto affine_mul = &pa_g2_affine_mul_batch;
@@ -480,8 +482,9 @@ public:
         return a;
     }
     bool operator==(const Projective& o) const {
-        if (is_zero() || o.is_zero()) return is_zero() && o.is_zero();
-        return into_affine() == o.into_affine();
+        uint8_t r = 0;
+        check(Abi::eq(&v, &o.v, &r, 1), "PartialEq");
+        return r != 0;
     }
     bool operator!=(const Projective& o) const { return !(*this == o); }
 
@@ -497,6 +500,13 @@ public:
         std::vector<Projective> out(a.size());
         if (!a.empty()) check(Abi::dbl(&a[0].v, &out[0].v, a.size()), "double_batch");
         return out;
+    }
+    // PartialEq per item (ec.rs:45-85) in one ABI call
+    static std::vector<bool> eq_batch(const std::vector<Projective>& a, const std::vector<Projective>& b) {
+        if (a.size() != b.size()) throw std::invalid_argument("eq_batch: operand lengths differ");
+        std::vector<uint8_t> r(a.size());
+        if (!a.empty()) check(Abi::eq(&a[0].v, &b[0].v, r.data(), a.size()), "eq_batch");
+        return std::vector<bool>(r.begin(), r.end());
     }
     static std::vector<Projective> add_batch(const std::vector<Projective>& a, const std::vector<Projective>& b) {
         same_size(a.size(), b.size());

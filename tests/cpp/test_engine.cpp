@@ -297,6 +297,20 @@ static void curve_tests(int iters) {
             EXPECT(v[k].is_normalized());
             EXPECT(v[k].into_affine() == expect[k]);
         }
+        // PartialEq in one batch (ec.rs:45-85): normalized == original, != its double
+        std::vector<P> orig, other;
+        for (size_t k = 0; k < v.size(); k++) {
+            orig.push_back(expect[k].into_projective());
+            P d = v[k];
+            d.double_();
+            other.push_back(d);
+        }
+        auto same = P::eq_batch(v, orig);
+        auto diff = P::eq_batch(v, other);
+        for (size_t k = 0; k < v.size(); k++) {
+            EXPECT(same[k]);
+            EXPECT(diff[k] == v[k].is_zero());   // only zero equals its double
+        }
     }
     {   // wNAF (curve.rs:68-179): fixed base and fixed scalar == mul_assign
         const P g = rand_point<P>(rng);
