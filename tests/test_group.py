@@ -113,7 +113,8 @@ def test_partial_eq_matches_reference(gpu, oracle, group):
     b = from_aff(to_aff(a))                          # same points, Z = 1 (zero stays zero)
     b[10:20] = _neg_rows_nonzero(a[10:20], fw)       # negations
     b[20:30] = add(a[20:30], a[30:40])               # other points
-    b[40] = a[1]                                     # zero vs zero: two garbage encodings
+    a[40] = a[1]                                     # zero vs zero: two garbage encodings
+    b[40] = a[1]
     b[40, :2 * fw] = np.uint64(5)
     b[41] = a[1]                                     # zero vs nonzero
     got = getattr(gpu, "g%d_eq" % group)(a, b)
