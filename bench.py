@@ -59,6 +59,8 @@ def parse():
                     default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layout", choices=["aos", "soa"], default="aos",
+                    help="fq_mul: device layout of the operands (SURVEY.md 8(d) config 2 names SoA)")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="launcher test only: gloo ranks on the CPU, the oracle as the per-rank compute "
                          "(tests/test_bench_launcher.py); not a measurement")
@@ -495,14 +497,21 @@ def main():
         n = args.batch if args.batch != (1 << 16) else (1 << 20)
         a_np = random_fq(g, 4096)[np.arange(n) % 4096]
         b_np = random_fq(g, 4096)[(np.arange(n) * 7 + 3) % 4096]
-        a = torch.from_numpy(a_np.view(np.int64)).to(dev)
-        b = torch.from_numpy(b_np.view(np.int64)).to(dev)
-        out = pdev.empty_records(n, 6, dev)
+        if args.layout == "soa":
+            a = torch.from_numpy(np.ascontiguousarray(a_np.T).view(np.int64)).to(dev)
+            b = torch.from_numpy(np.ascontiguousarray(b_np.T).view(np.int64)).to(dev)
+            out = torch.empty((6, n), dtype=torch.int64, device=dev)
+            mul = pdev.fq_mul_soa
+        else:
+            a = torch.from_numpy(a_np.view(np.int64)).to(dev)
+            b = torch.from_numpy(b_np.view(np.int64)).to(dev)
+            out = pdev.empty_records(n, 6, dev)
+            mul = pdev.fq_mul
 
         def step(timed):
             if timed:
                 ev[0].record(stream)
-            pdev.fq_mul(a, b, out, stream)
+            mul(a, b, out, stream)
             if timed:
                 ev[1].record(stream)
 
@@ -589,7 +598,7 @@ def main():
             dom_name, dom_ms, dom_bytes = "fq_mul_batch", float(np.mean(k_ms["a"])), 144
             value = ws * n * args.steps / elapsed
             metric, unit = "Fq::mul_assign per second at batch 2^20", "muls/s"
-            config = {"workload": "2^20 Fq Montgomery multiplications (AoS 6x u64)", "batch_per_gpu": n,
+            config = {"workload": "2^20 Fq Montgomery multiplications (%s 6x u64)" % args.layout.upper(), "batch_per_gpu": n,
                       "global_batch": n * ws}
         achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9
         traffic = None

@@ -302,6 +302,9 @@ int pa_g1_fixed_base_glv_mul_device(const pa_g1 *base, const uint64_t *table, co
 int pa_g1_wnaf_fixed_base_device(const pa_g1 *base, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
                                  uint64_t *table, uint64_t *workspace, void *stream);
 int pa_fq_mul_batch_device(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n, void *stream);
+/* Fq::mul_assign (fq.rs:909-960) on the SoA device layout of SURVEY.md 8(d) config 2: u64 word j
+ * (0..5, little-endian, Montgomery, < q) of element i at a[j * n + i]; same bits as the AoS form */
+int pa_fq_mul_batch_soa_device(const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, void *stream);
 int pa_fr_mul_batch_device(const pa_fr *a, const pa_fr *b, pa_fr *out, size_t n, void *stream);
 int pa_g1_multiexp_device(const pa_g1_affine *bases, const pa_fr_repr *s, size_t n, pa_g1 *out, void *workspace,
                           size_t workspace_bytes, void *stream);

@@ -102,6 +102,7 @@ _SIGS = {
     "pa_g1_fixed_base_glv_table_device": [_P, _P, _P, _P],
     "pa_g1_fixed_base_glv_mul_device": [_P, _P, _P, _P, _P, _N, _P],
     "pa_fq_mul_batch_device": [_P, _P, _P, _N, _P],
+    "pa_fq_mul_batch_soa_device": [_P, _P, _P, _N, _P],
     "pa_miller_loop_fused_batch_device": [_P, _P, _P, _N, _P],
     "pa_final_exponentiation_batch_device": [_P, _P, _P, _N, _P],
     "pa_pairing_batch_device": [_P, _P, _P, _P, _N, _P],
@@ -141,11 +142,11 @@ _SIGS = {
 for _g in (1, 2):
     for _op in ("double", "negate", "into_affine", "into_projective"):
         _SIGS["pa_g%d_%s_batch" % (_g, _op)] = [_P, _P, _N]
-    for _op in ("add", "add_mixed", "sub"):
+    for _op in ("add", "add_mixed", "sub", "eq"):
         _SIGS["pa_g%d_%s_batch" % (_g, _op)] = [_P, _P, _P, _N]
     for _op in ("double", "into_affine"):
         _SIGS["pa_g%d_%s_batch_device" % (_g, _op)] = [_P, _P, _N, _P]
-    for _op in ("add", "add_mixed"):
+    for _op in ("add", "add_mixed", "eq"):
         _SIGS["pa_g%d_%s_batch_device" % (_g, _op)] = [_P, _P, _P, _N, _P]
     _SIGS["pa_g%d_recommended_wnaf_for_scalar" % _g] = [_P]
     _SIGS["pa_g%d_recommended_wnaf_for_num_scalars" % _g] = [_N]

@@ -833,6 +833,11 @@ int pa_fq_mul_batch_device(const pa_fq* a, const pa_fq* b, pa_fq* out, size_t n,
            "kernel launch");
     return PA_OK;
 }
+int pa_fq_mul_batch_soa_device(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, void* stream) {
+    if (n && (!a || !b || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_fq_mul_batch_soa(a, b, out, n, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
 int pa_miller_loop_fused_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n,
                                       void* stream) {
     if (n && (!p || !q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");

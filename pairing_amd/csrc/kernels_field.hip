@@ -114,6 +114,40 @@ __global__ void __launch_bounds__(256) k_fq_mul_batch_fl(const uint64_t* __restr
     fq_store(out + 6 * i, fl_pack_canon(z));
 }
 
+// Config 2 with the device layout SURVEY.md section 8(d) names (SoA): word j of
+// element i at a[j n + i], so each of the six 8-byte loads / stores of a wave
+// is one contiguous 512-byte run.  Same product and canonicalization as
+// k_fq_mul_batch_fl.
+__global__ void __launch_bounds__(256) k_fq_mul_batch_soa(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
+                                                           uint64_t* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fq x, y;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const uint64_t u = a[j * n + i], v = b[j * n + i];
+        x.w[2 * j] = (uint32_t)u;
+        x.w[2 * j + 1] = (uint32_t)(u >> 32);
+        y.w[2 * j] = (uint32_t)v;
+        y.w[2 * j + 1] = (uint32_t)(v >> 32);
+    }
+    const F<1> xs = fl_split_shl8(x), ys = fl_split(y);
+    F<1> z;
+    fl_mul_leaf(z.w, xs.w, ys.w);
+    const Fq r = fl_pack_canon(z);
+#pragma unroll
+    for (int j = 0; j < 6; j++) out[j * n + i] = (uint64_t)r.w[2 * j] | ((uint64_t)r.w[2 * j + 1] << 32);
+}
+hipError_t launch_fq_mul_batch_soa(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    static const unsigned lds = [] {
+        const char* e = getenv("PA_FQ_LDS");
+        return e ? (unsigned)atoi(e) : 27000u;
+    }();
+    hipLaunchKernelGGL(k_fq_mul_batch_soa, dim3(blocks_for(n, 256)), dim3(256), lds, stream, a, b, out, n);
+    return hipGetLastError();
+}
+
 // Probe for config 2 (PA_FQ_VARIANT=9, not the product path): the same record
 // traffic with no multiply (z = x ^ y), i.e. the access-pattern bound: 25.0 us at
 // 2^20 against 29.0 us with the multiply (profiles/r02_fq_variants_s7.txt; a

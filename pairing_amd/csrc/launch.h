@@ -59,6 +59,8 @@ inline StreamCfg stream_cfg() {
 }
 
 // Fq::mul_assign batch, 6 x u64 AoS in and out (config 2 kernel)
+// config 2 on the SoA device layout: word j of element i at a[j n + i]
+hipError_t launch_fq_mul_batch_soa(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, hipStream_t stream);
 hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
                                hipStream_t stream);
 

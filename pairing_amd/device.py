@@ -36,6 +36,19 @@ def fq_mul(a, b, out, stream=None):
          _stream_ptr(stream))
 
 
+def fq_mul_soa(a, b, out, stream=None):
+    """Fq::mul_assign on the SoA device layout: (6, n) int64 planes, word j of
+    element i at [j, i]."""
+    for t, name in ((a, "a"), (b, "b"), (out, "out")):
+        if not t.is_cuda or not t.is_contiguous() or t.dtype != torch.int64 or t.dim() != 2 or t.shape[0] != 6:
+            raise ValueError("%s must be a contiguous (6, n) int64 CUDA tensor" % name)
+    n = a.shape[1]
+    if b.shape[1] != n or out.shape[1] != n:
+        raise ValueError("operand lengths differ")
+    call("pa_fq_mul_batch_soa_device", ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+         ctypes.c_void_p(out.data_ptr()), n, _stream_ptr(stream))
+
+
 def miller_loop(p, q, out, stream=None):
     """Fused-prepare single-pair Miller loops: out[i] = miller_loop([(p[i], q[i].prepare())])."""
     call("pa_miller_loop_fused_batch_device", _dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"),

@@ -247,3 +247,20 @@ def test_final_exp_split_and_in_place_agree(gpu, oracle):
     np.testing.assert_array_equal(ok.cpu().numpy(), np.asarray(ok_exp, np.uint8))
     np.testing.assert_array_equal(ok2.cpu().numpy(), np.asarray(ok_exp, np.uint8))
     assert ok.cpu().numpy()[7] == 0
+
+
+@pytest.mark.parametrize("n", [1 << 20, (1 << 20) + 37])
+def test_fq_mul_soa_device_bit_exact(gpu, oracle, n):
+    """config 2 on the SoA device layout: every element
+    against the oracle, words transposed on the host"""
+    import torch
+    import pairing_amd.device as pdev
+    a = _fq_rows(7, n)
+    b = _fq_rows(8, n)[::-1].copy()
+    da = torch.from_numpy(np.ascontiguousarray(a.T).view(np.int64)).to("cuda:0")
+    db = torch.from_numpy(np.ascontiguousarray(b.T).view(np.int64)).to("cuda:0")
+    out = torch.empty((6, n), dtype=torch.int64, device="cuda:0")
+    pdev.fq_mul_soa(da, db, out)
+    torch.cuda.synchronize()
+    got = np.ascontiguousarray(out.cpu().numpy().view(np.uint64).T)
+    np.testing.assert_array_equal(got, oracle.fq_mul(a, b))
