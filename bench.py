@@ -608,7 +608,7 @@ def main():
                 # the split final exponentiation has its own entry (the three
                 # kernels' bytes per step); null until measured
                 fe_split = args.workload == "pairing" and dom_name == "final_exponentiation" and \
-                    os.environ.get("PA_FE_SPLIT", "1") != "0"
+                    os.environ.get("PA_FE_SPLIT", "0") == "1"
                 traffic = json.load(f).get(dom_name + ("_split" if fe_split else ""))
         roof = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -627,11 +627,14 @@ def main():
             # kept alongside
             with open(work_path) as f:
                 work = json.load(f)
-            # the final exponentiation step is, by default, the split form
-            # (gen_launch.hip): norm kernel + binary-GCD inversion + the rest;
-            # its MACs / instructions are the two generated kernels' (the
-            # inversion kernel's integer work is not limb MACs)
-            split = os.environ.get("PA_FE_SPLIT", "1") != "0" and "fe_inv" in work
+            # the final exponentiation step is one generated kernel (round 3:
+            # in-kernel binary-GCD inversions, compressed squarings); with
+            # PA_FE_SPLIT=1 round 2's split form: norm kernel + binary-GCD
+            # inversion kernel + the rest, whose MACs / instructions are the two
+            # generated kernels' (the inversion kernel's integer work is not
+            # limb MACs).  The in-kernel binary GCD's instructions are counted,
+            # its 64-bit approximation steps are not limb MACs either.
+            split = os.environ.get("PA_FE_SPLIT", "0") == "1" and "fe_inv" in work
             wk = (work["miller_loop"] if dom_name != "final_exponentiation" else
                   {k: work["fe_norm"][k] + work["fe_inv"][k] for k in ("limb_macs", "instructions")}
                   if split else work["final_exp"])

@@ -197,16 +197,16 @@ hipError_t launch_miller_loop_gen(int lanes, const uint64_t* p_aff, const uint64
                                   hipStream_t stream) {
     return launch(lanes == 2 ? 2 : 0, p_aff, q_aff, out, n, stream);
 }
-// One lane: by default the split form -- norm kernel (Fq 0 of out), binary-GCD
-// inversion in place, then the final exponentiation reading that inverse
-// instead of running its 463-product Fermat chain.  It needs `out` apart from
-// `in` (the norm lands in out while the last kernel still reads in); an
-// overlapping call and PA_FE_SPLIT=0 run the one-kernel form.
+// One lane: the one-kernel final exponentiation (round 3: its inversions run
+// in the kernel by binary GCD and exp_by_x squares compressed, Karabina;
+// tools/pgen/kernels.py).  PA_FE_SPLIT=1 selects round 2's split form -- norm
+// kernel (Fq 0 of out), binary-GCD inversion in place, then the Granger-Scott
+// exponentiation reading that inverse -- which needs `out` apart from `in`.
 hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
                                 hipStream_t stream) {
     static const bool split = [] {
         const char* e = getenv("PA_FE_SPLIT");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     const bool apart = out + 72 * n <= in || in + 72 * n <= out;
     if (lanes == 2 || !split || !apart) return launch(lanes == 2 ? 3 : 1, in, out, ok, n, stream);

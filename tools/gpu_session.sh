@@ -28,6 +28,8 @@ for step in "$@"; do
         sizetests) run pytest_sizes 600 python -u -m pytest tests/test_bench_sizes.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
+        benchnc) run bench_nc 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+        benchsplit) run bench_split 300 env PA_FE_SPLIT=1 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         verifybench) run bench_verify 300 python bench.py --workload verify --steps 10 --warmup 2 --no-cpu-baseline ;;
         fqsoa) run bench_fq_soa 300 python bench.py --workload fq_mul --layout soa --steps 20 --warmup 3 --no-cpu-baseline ;;
         proffqsoa) run prof_fq_soa 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fq_soa -o run -- python bench.py --workload fq_mul --layout soa --steps 10 --warmup 2 --no-cpu-baseline ;;

@@ -181,10 +181,34 @@ class Prog:
     def inv(self, a):
         """a^-1 in the Fl domain (0 -> 0) as ONE op.  The cooperative kernels
         (coop.py, kernels_coop.hip) run it on the 12-word core's binary GCD
-        (bgcd.h); the one-lane generated kernels use Tower.inv_fq's Fermat
-        chain instead."""
+        (bgcd.h); the one-lane generated kernels use binv() (or Tower.inv_fq's
+        Fermat chain with PGEN_BINV=0)."""
         self._full(a)
         return self._op("inv", [a], 1)
+
+    def binv(self, a):
+        """a^-1 in the Fl domain (0 -> 0) by the in-kernel binary GCD of the
+        one-lane generated kernels (emit.Emitter.emit_binv; exact output limbs:
+        binv_limbs below).  u = 1, value < 2q, not canonical."""
+        self._full(a)
+        assert a.vb <= VB_RED, "binv value bound %d" % a.vb
+        return self._op("binv", [a], 1)
+
+    def selz(self, tests, a, b):
+        """a where every test value is 0 mod q, else b (lane-wise select).  The
+        tests must be fully reduced (u = vb = 1: limbs < 2^28, value < 2q, so
+        zero mod q means the limbs are those of 0 or of q)."""
+        self._full(a, b, *tests)
+        assert all(t.u == 1 and t.vb == 1 for t in tests), "selz tests must be reduced"
+        return self._op("selz", list(tests) + [a, b], max(a.u, b.u), imm=len(tests), vb=max(a.vb, b.vb))
+
+    def red_full(self, a):
+        """the full reduction (value < 2q, limbs < 2^28) whatever the value bound"""
+        self._full(a)
+        if a.u == 1 and a.vb == 1:
+            return a
+        assert a.vb <= VB_RED, "red value bound %d" % a.vb
+        return self._cse("red", [a], 1, vb=1)
 
     # ---- wide (double-width, unreduced) values: lazy reduction ----
     def wsop(self, *args):
@@ -556,6 +580,67 @@ def red_limbs(x):
     return tuple(r)
 
 
+# ---- the in-kernel binary GCD (emit.Emitter.emit_binv), limb-exact ----
+# T. Pornin, "Optimized Binary GCD for Modular Inversion" (eprint 2020/972),
+# Algorithm 2 with k - 1 = 28: BINV_OUTER outer steps of 28 inner steps on
+# 58-bit approximations (the low 28 bits = limb 0, the top 30 bits of
+# max(len a, len b, 58)); the update (u, v) <- (u f + v g) / 2^28 is one
+# Montgomery digit, so u, v stay signed 14-limb integers below (t + 1) q in
+# magnitude and are never reduced inside the loop.  28 x 28 = 784 >= 2 * 381 - 1.
+BINV_OUTER = 28
+BINV_PAD = 32          # v + 32 q >= 0 before the final product
+BINV_C = pow(2, 3 * LB * NL, Q)       # R'^3: (y^-1) R'^3 / R' = a^-1 R' for y = a R'
+
+
+def binv_core(y):
+    """y (0 <= y < q) -> the signed integer v the emitted loop leaves (v = y^-1
+    mod q, or 0 for y = 0), following the emitted limb arithmetic exactly"""
+    A, B, U, W = y, Q, 1, 0
+    m28 = MASK
+    for _ in range(BINV_OUTER):
+        n = max((A | B).bit_length(), 58)
+        p = n - 30
+        xa = (((A >> p) & ((1 << 30) - 1)) << 28) | (A & m28)
+        xb = (((B >> p) & ((1 << 30) - 1)) << 28) | (B & m28)
+        f0, g0, f1, g1 = 1, 0, 0, 1
+        for _ in range(28):
+            odd = xa & 1
+            sw = odd and xa < xb
+            if sw:
+                xa, xb, f0, f1, g0, g1 = xb, xa, f1, f0, g1, g0
+            if odd:
+                xa, f0, g0 = xa - xb, f0 - f1, g0 - g1
+            xa >>= 1
+            f1, g1 = 2 * f1, 2 * g1
+        na, nb = A * f0 + B * g0, A * f1 + B * g1
+        assert na % (1 << 28) == 0 and nb % (1 << 28) == 0
+        na >>= 28
+        nb >>= 28
+        if na < 0:
+            na, f0, g0 = -na, -f0, -g0
+        if nb < 0:
+            nb, f1, g1 = -nb, -f1, -g1
+        tu, tw = U * f0 + W * g0, U * f1 + W * g1
+        ku = (tu * QINV28) & m28
+        kw = (tw * QINV28) & m28
+        tu, tw = tu + ku * Q, tw + kw * Q
+        assert tu % (1 << 28) == 0 and tw % (1 << 28) == 0
+        A, B, U, W = na, nb, tu >> 28, tw >> 28
+    assert A == 0 and B in (1, Q), "binary GCD did not converge"
+    return W
+
+
+def binv_limbs(x):
+    """limbs the emitted binv leaves for input limbs x: red, canonical y,
+    the loop, v + 32 q normalized, times R'^3 (one Montgomery product)"""
+    r = red_limbs(x)
+    y = val_of(r)
+    y = y - Q if y >= Q else y
+    w = binv_core(y) + BINV_PAD * Q
+    assert 0 <= w < (1 << 387)
+    return mont_sop([(tuple(gen_fl.limbs(w)), tuple(gen_fl.limbs(BINV_C)))])
+
+
 def evaluate(prog, inputs, stats=None, trace=None):
     """inputs: dict slot -> canonical ABI integer (R = 2^384 Montgomery value,
     i.e. the integer held in the record).  Returns dict slot -> output integer.
@@ -610,6 +695,11 @@ def evaluate(prog, inputs, stats=None, trace=None):
         if k == "inv":
             v = val_of(s[0]) % Q
             return tuple(gen_fl.limbs(R * R * pow(v, -1, Q) % Q if v else 0))
+        if k == "binv":
+            return binv_limbs(s[0])
+        if k == "selz":
+            nt = op.imm
+            return s[nt] if all(val_of(t) % Q == 0 for t in s[:nt]) else s[nt + 1]
         raise ValueError(k)
 
     def step(op):

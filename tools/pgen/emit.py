@@ -26,7 +26,8 @@ for constants, or label strings; see render.py / sim.py.
 """
 import os
 
-from dsl import Loop, If, Op, SUBC, NL, MASK, QL, QINV28, KQ
+import gen_fl
+from dsl import Loop, If, Op, SUBC, NL, MASK, QL, QINV28, KQ, Q, BINV_OUTER, BINV_PAD, BINV_C
 
 A_BASE, S_BASE = 256, 512
 VCC = S_BASE + 106
@@ -246,8 +247,7 @@ class Emitter:
                 continue
             vs = self.vslot[k]
             nu = self.next_use(vs, pos) - pos
-            clean = len(vs.locs) > 1
-            score = nu * (3 if clean else 1)
+            score = nu * self.drop_weight(vs)
             if score > best:
                 best, bk = score, k
         if bk is None:
@@ -256,6 +256,17 @@ class Emitter:
             self.wait_pending([bk])
         self.evict(bk, pos)
         return bk
+
+    # Belady weights: dropping a value with a copy in an AGPR costs 14 moves to
+    # reload, in LDS 7 loads, in the HBM workspace 7 loads + latency + traffic;
+    # a value without a copy costs a spill first (PGEN_DROP_W: A/B experiments)
+    DROP_W = tuple(float(x) for x in os.environ.get("PGEN_DROP_W", "3,3,3,1").split(","))
+
+    def drop_weight(self, vs):
+        kinds = {l[0] for l in vs.locs if l[0] != "V"}
+        if not kinds:
+            return self.DROP_W[3]
+        return max(self.DROP_W["ALM".index(k)] for k in kinds)
 
     def evict(self, k, pos):
         vs = self.vslot[k]
@@ -595,6 +606,213 @@ class Emitter:
         for i in range(NL):
             self.i("v_mov_b32", d + i, K(limbs[i]))
 
+    # ---- zero-test select (dsl.Prog.selz) ----
+    def emit_selz(self, tests, a, b, d):
+        """d = a where every test (limbs < 2^28, value < 2q) is 0 or q, else b.
+        Masks: s[32:33] / s[34:35] / s[38:39] (free outside record I/O and
+        binv), the final one in VCC by SALU; a VALU read of an SGPR a VALU
+        wrote needs two wait states on gfx950 (only SALU reads follow the
+        compares here)."""
+        pairs = ((S(32), S(34)), (S(38), S(34)))
+        for n, t in enumerate(tests):
+            self.i("v_or3_b32", 0, t, t + 1, t + 2)
+            for i in range(3, NL, 2):
+                if i + 1 < NL:
+                    self.i("v_or3_b32", 0, 0, t + i, t + i + 1)
+                else:
+                    self.i("v_or_b32", 0, 0, t + i)
+            for i in range(NL):
+                self.i("v_xor_b32", 2 + i, S(SQ + i), t + i)
+            self.i("v_or3_b32", 1, 2, 3, 4)
+            for i in range(5, 2 + NL, 2):
+                if i + 1 < 2 + NL:
+                    self.i("v_or3_b32", 1, 1, i, i + 1)
+                else:
+                    self.i("v_or_b32", 1, 1, i)
+            za, zq = pairs[n]
+            self.i("v_cmp_eq_u32_e64", za, K(0), 0)
+            self.i("v_cmp_eq_u32_e64", zq, K(0), 1)
+            self.i("s_or_b64", za, za, zq)
+        if len(tests) == 1:
+            self.i("s_mov_b64", VCC, S(32))
+        else:
+            self.i("s_and_b64", VCC, S(32), S(38))
+        for i in range(NL):
+            self.i("v_cndmask_b32", d + i, b + i, a + i)
+
+    # ---- in-kernel binary GCD inversion (dsl.Prog.binv, dsl.binv_limbs) ----
+    def emit_binv(self, x, d, scratch):
+        """d = x^-1 (Fl domain, 0 -> 0) by T. Pornin's optimized binary GCD
+        (eprint 2020/972, Algorithm 2) on 28-bit limbs -- the same algorithm as
+        pairing_amd/csrc/bgcd.h with k - 1 = 28 so that the exact update's
+        division by 2^28 drops one limb.  Exact semantics: dsl.binv_limbs.
+
+        Registers: a, b, u, w = four scratch V slots; work area v0..v15
+        (v16 = the lane offset, v17 are kept); s[32:33] s[34:35] s[38:39] VCC
+        masks; the outer loop counter at S_CNT + depth.  Every VALU read of an
+        SGPR a VALU wrote comes at least two instructions after the write."""
+        a, b, u, w = (self.vbase(k) for k in scratch)
+        MK = K(MASK)
+        # y = x mod q, canonical, into a
+        self.emit_red(x, a)
+        for li in range(NL):
+            self.i("v_subrev_u32", li, K(QL[li]), a + li)
+            if li:
+                self.i("v_add_u32", li, li, 14)
+            self.i("v_ashrrev_i32", 14, K(28), li)
+            self.i("v_and_b32", li, MK, li)
+        for li in range(NL):
+            self.i("v_bfi_b32", a + li, 14, a + li, li)     # a < q ? a : a - q
+        for i in range(NL):
+            self.i("v_mov_b32", b + i, S(SQ + i))
+            self.i("v_mov_b32", u + i, K(1 if i == 0 else 0))
+            self.i("v_mov_b32", w + i, K(0))
+        cnt = S(S_CNT + self.depth)
+        top = self.label()
+        self.i("s_mov_b32", cnt, K(BINV_OUTER - 1))
+        self.i("label", top)
+        w0 = self.weight
+        self.weight = w0 * BINV_OUTER
+        # -- n = max(len(a | b), 58): top nonzero limb (index v13, value v12),
+        #    limbs 2..13 (below limb 2 the max with 58 decides anyway)
+        masks = (S(32), S(34), S(38))
+        self.i("v_mov_b32", 12, K(1))
+        self.i("v_mov_b32", 13, K(1))
+        for i in range(2, NL):
+            self.i("v_or_b32", i - 2, a + i, b + i)
+        # compares rotate over three SGPR pairs so each select is >= 2 wait states after its compare
+        order = list(range(2, NL))
+        for n, i in enumerate(order):
+            self.i("v_cmp_eq_u32_e64", masks[n % 3], K(0), i - 2)
+            if n >= 2:
+                j = order[n - 2]
+                m = masks[(n - 2) % 3]
+                self.i("v_cndmask_b32_e64", 12, j - 2, 12, m)      # zero ? old : limb
+                self.i("v_cndmask_b32_e64", 13, K(j), 13, m)       # zero ? old : index
+        for n in (len(order) - 2, len(order) - 1):
+            j = order[n]
+            m = masks[n % 3]
+            self.i("v_cndmask_b32_e64", 12, j - 2, 12, m)
+            self.i("v_cndmask_b32_e64", 13, K(j), 13, m)
+        self.i("v_ffbh_u32", 14, 12)
+        self.i("v_sub_u32", 15, K(32), 14)
+        self.i("v_mad_u32_u24", 15, 13, K(28), 15)           # n = 28 idx + bitlen(limb)
+        self.i("v_max_u32", 15, K(58), 15)
+        self.i("v_subrev_u32", 15, K(30), 15)                # p = n - 30 >= 28
+        self.i("v_mul_u32_u24", 14, K(9363), 15)
+        self.i("v_lshrrev_b32", 14, K(18), 14)               # j = p / 28 (exact for p < 392)
+        self.i("v_mul_u32_u24", 13, K(28), 14)
+        self.i("v_sub_u32", 15, 15, 13)                      # s = p - 28 j
+        # -- barrel masks of j: s[32:33] bit 8, s[34:35] bit 4, s[38:39] bit 2, VCC bit 1
+        bm = (S(32), S(34), S(38), VCC)
+        for bit, m in zip((8, 4, 2, 1), bm):
+            self.i("v_and_b32", 12, K(bit), 14)
+            if m == VCC:
+                self.i("v_cmp_ne_u32", K(0), 12)
+            else:
+                self.i("v_cmp_ne_u32_e64", m, K(0), 12)
+        # -- approximations: xa = v[10:11], xb = v[12:13]
+        for src, dst in ((a, 10), (b, 12)):
+            for i in range(10):
+                self.i("v_cndmask_b32_e64", i, src + i, (src + i + 8) if i + 8 < NL else K(0), bm[0])
+            for st, m, cntn in ((4, bm[1], 6), (2, bm[2], 4), (1, bm[3], 3)):
+                for i in range(cntn):
+                    self.i("v_cndmask_b32_e64", i, i, i + st, m)
+            self.i("v_lshl_or_b32", 4, 1, K(28), 0)
+            self.i("v_lshrrev_b32", 5, K(4), 1)
+            self.i("v_lshl_or_b32", 5, 2, K(24), 5)
+            self.i("v_lshrrev_b64", 4, 15, 4)
+            self.i("v_and_b32", 4, K((1 << 30) - 1), 4)
+            self.i("v_lshl_or_b32", dst, 4, K(28), src)
+            self.i("v_lshrrev_b32", dst + 1, K(4), 4)
+        # -- 28 inner steps: f0 v6, g0 v7, f1 v8, g1 v9
+        for r, v in ((6, 1), (7, 0), (8, 0), (9, 1)):
+            self.i("v_mov_b32", r, K(v))
+        for _ in range(28):
+            self.i("v_and_b32", 0, K(1), 10)
+            self.i("v_cmp_lt_u64_e64", S(38), 10, 12)          # lt
+            self.i("v_cmp_ne_u32_e64", S(34), K(0), 0)          # odd
+            self.i("s_and_b64", VCC, S(34), S(38))              # swap = odd & lt
+            self.i("v_cndmask_b32", 0, 10, 12)                  # XA = swap ? xb : xa
+            self.i("v_cndmask_b32", 1, 11, 13)
+            self.i("v_cndmask_b32", 12, 12, 10)                 # xb' = swap ? xa : xb
+            self.i("v_cndmask_b32", 13, 13, 11)
+            self.i("v_cndmask_b32", 4, 6, 8)                    # FA = swap ? f1 : f0
+            self.i("v_cndmask_b32", 8, 8, 6)                    # FB
+            self.i("v_cndmask_b32", 5, 7, 9)                    # GA
+            self.i("v_cndmask_b32", 9, 9, 7)                    # GB
+            self.i("v_sub_co_u32", 2, 0, 12)                    # XA - XB (borrow in VCC)
+            self.i("v_sub_u32", 14, 4, 8)
+            self.i("v_sub_u32", 15, 5, 9)
+            self.i("v_subb_co_u32", 3, 1, 13)
+            self.i("v_cndmask_b32_e64", 6, 4, 14, S(34))        # f0' = odd ? FA - FB : FA
+            self.i("v_cndmask_b32_e64", 7, 5, 15, S(34))
+            self.i("v_lshlrev_b32", 8, K(1), 8)                 # f1' = 2 FB
+            self.i("v_lshlrev_b32", 9, K(1), 9)
+            self.i("v_cndmask_b32_e64", 10, 0, 2, S(34))        # xa' = (odd ? XA - XB : XA) / 2
+            self.i("v_cndmask_b32_e64", 11, 1, 3, S(34))
+            self.i("v_lshrrev_b64", 10, K(1), 10)
+        # -- (a, b) <- ((a f0 + b g0), (a f1 + b g1)) / 2^28, in place (column i -> limb i - 1)
+        self.comb_columns(((a, 6, b, 7, None), (b, 9, a, 8, None)))
+        # -- negative results: negate the limbs and the factor row
+        for src, mreg in ((a, 10), (b, 11)):
+            self.i("v_ashrrev_i32", mreg, K(31), src + NL - 1)
+            self.i("v_and_b32", 12, MK, mreg)
+            self.i("v_lshrrev_b32", 13, K(31), src + NL - 1)
+            for i in range(NL - 1):
+                self.i("v_xad_u32", 15, src + i, 12, 13)
+                self.i("v_and_b32", src + i, MK, 15)
+                self.i("v_lshrrev_b32", 13, K(28), 15)
+            self.i("v_xad_u32", src + NL - 1, src + NL - 1, mreg, 13)
+        for r, mreg in ((6, 10), (7, 10), (8, 11), (9, 11)):
+            self.i("v_xor_b32", r, r, mreg)
+            self.i("v_sub_u32", r, r, mreg)
+        # -- (u, w) <- ((u f0 + w g0), (u f1 + w g1)) / 2^28 mod q (one Montgomery digit each)
+        self.comb_columns(((u, 6, w, 7, 4), (w, 9, u, 8, 5)))
+        self.weight = w0
+        self.i("s_sub_u32", cnt, cnt, K(1))
+        self.i("s_cmp_ge_i32", cnt, K(0))
+        self.i("long_cbranch_scc1", top)
+        # -- w + 32 q >= 0, normalized; times R'^3 (one Montgomery product)
+        pad = gen_fl.limbs(BINV_PAD * Q)
+        for i in range(NL):
+            self.i("v_add_u32", 1, K(pad[i]), w + i)
+            if i == NL - 1:
+                self.i("v_add_u32", w + i, 1, 0)
+                break
+            if i:
+                self.i("v_add_u32", 1, 1, 0)
+            self.i("v_and_b32", w + i, MK, 1)
+            self.i("v_lshrrev_b32", 0, K(28), 1)
+        self.emit_const(gen_fl.limbs(BINV_C), a)
+        self.emit_sop([(w, a)], d)
+
+    def comb_columns(self, rows):
+        """two signed linear combinations of the 14-limb values, divided by
+        2^28 in place: for each row (x, fx, y, fy, kreg) the accumulator gets
+        x_i f + y_i g (+ k q_i when kreg names the VGPR of the Montgomery digit,
+        k = -(column 0) q^-1 mod 2^28); column i's low 28 bits replace limb
+        i - 1 of x, the final carry is limb 13 (signed).  Accumulators v[0:1],
+        v[2:3]; the rows' x must be the two values being replaced, each row
+        reading both before either is written."""
+        accs = (0, 2)
+        for i in range(NL):
+            for (x, fx, y, fy, kreg), acc in zip(rows, accs):
+                self.i("v_mad_i64_i32", acc, x + i, fx, K(0) if i == 0 else acc)
+                self.i("v_mad_i64_i32", acc, y + i, fy, acc)
+                if kreg is not None:
+                    if i == 0:
+                        self.i("v_mul_lo_u32", kreg, acc, S(SQINV))
+                        self.i("v_and_b32", kreg, K(MASK), kreg)
+                    self.i("v_mad_i64_i32", acc, kreg, S(SQ + i), acc)
+            if i:
+                for (x, _, _, _, _), acc in zip(rows, accs):
+                    self.i("v_and_b32", x + i - 1, K(MASK), acc)
+            for acc in accs:
+                self.i("v_ashrrev_i64", acc, K(28), acc)
+        for (x, _, _, _, _), acc in zip(rows, accs):
+            self.i("v_mov_b32", x + NL - 1, acc)
+
     # ---------------- blocks ----------------
     def analyse(self, block):
         """ValStates + use positions for the values defined in `block`"""
@@ -818,6 +1036,12 @@ class Emitter:
             self.wait_pending([dk2])
         if dk is not None:
             self.pinned.add(dk)
+        scratch = []
+        if k == "binv":
+            for _ in range(4):
+                kk = self.get_vslot(pos, avoid=self.pinned)
+                self.pinned.add(kk)
+                scratch.append(kk)
         self.prefetch(pos)
         base = [self.vbase(x) for x in sk]
         d = self.vbase(dk) if dk is not None else None
@@ -858,6 +1082,11 @@ class Emitter:
             self.emit_swap(base[0], d)
         elif k == "sel":
             self.emit_sel(base[0], base[1], d)
+        elif k == "selz":
+            nt = op.imm
+            self.emit_selz(base[:nt], base[nt], base[nt + 1], d)
+        elif k == "binv":
+            self.emit_binv(base[0], d, scratch)
         elif k == "load_raw":
             self.cfg.emit_load(self, op.imm, d)
         elif k == "store_raw":
@@ -886,7 +1115,8 @@ class Emitter:
 
     # ---------------- prefetch ----------------
     COST = {"sop": None, "sqr": 460, "red": 62, "norm": 39, "add": 14, "add3": 14, "shladd": 14, "shl": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
-            "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14}
+            "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14,
+            "selz": 80, "binv": 33000}
     # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
     AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}
     WINDOW = 2500

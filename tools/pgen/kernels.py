@@ -12,7 +12,7 @@ lane selects done by the emitted prologue/epilogue, outside the DSL.
 import os
 
 from dsl import Prog
-from tower import Tower, TowerLazy, TowerLazySq, X_ABS, declare12, get12, set12
+from tower import Tower, TowerLazy, TowerLazySq, X_ABS, declare12, get12, set12  # noqa: F401
 from tower2 import Tower2
 
 ML_MASK = (X_ABS >> 1) & ((1 << 62) - 1)  # bits 61..0 below the leading one of |x| >> 1
@@ -199,6 +199,124 @@ def exp_by_x(p, T, V, f, x, tag):
     return T.conj12(V.get12(res))
 
 
+def exp_by_x_karabina(p, T, V, xv, L, first_skip, tag="k"):
+    """exp_by_x (mod.rs:116-121) in place on the Fq12 variable `xv`, as
+    f^|x| = prod f^(2^i) over the set bits i of |x| = 0xd201000000010000
+    (16, 48, 57, 60, 62, 63), then conjugation (x < 0).  The powers up to
+    bit 57 come from ONE run of compressed (Karabina) squarings, saved at bits
+    16 and 48; those three are decompressed with one shared inversion
+    (Tower.batch_inv2 -> the in-kernel binary GCD); the 6 squarings between the
+    top bits run uncompressed (Granger-Scott) from f^(2^57), since another
+    decompression would cost more than they do.  Inside the hard part's loop
+    over its five calls (final_exp_prog): when bit `first_skip` of the loop
+    counter L is set the first run is one squaring shorter, which is the
+    exp_by_x(x >> 1) call (bits 15, 47, 56, 59, 61, 62)."""
+    bits = [i for i in range(X_ABS.bit_length()) if (X_ABS >> i) & 1]
+    res, top = "kr%s_" % tag, "kt%s_" % tag
+    # the compressed state's homes are those of the later GS state's first 8
+    # coordinates (the two never live at once)
+    kn = ["%s%d_%d" % (top, j // 2, j % 2) for j in range(8)]
+    for n in kn:
+        p.var(n, 1, os.environ.get("PGEN_KC_HOME", "A"))
+    (_, a1, a2), (b0, _, b2) = V.get12(xv)
+    for n, v in zip(kn, [*a1, *a2, *b0, *b2]):
+        p.set(n, v)
+
+    def getg(names):
+        g = [p.get(n) for n in names]
+        return ((g[0], g[1]), (g[2], g[3]), (g[4], g[5]), (g[6], g[7]))
+
+    def ksqr_state():
+        for n, v in zip(kn, [c for x2 in T.ksqr(getg(kn)) for c in x2]):
+            p.set(n, v)
+
+    saved, prev = [], 0
+    for k, b in enumerate(bits[:3]):
+        n = b - prev
+        if k == 0:
+            n -= 1
+        with p.loop(n):
+            ksqr_state()
+        if k == 0:
+            with p.if_bit(((1 << 8) - 1) & ~(1 << first_skip), L):
+                ksqr_state()
+        prev = b
+        if k < 2:
+            sn = ["ks%s%d_%d" % (tag, k, i) for i in range(8)]
+            for n in sn:
+                p.var(n, 1, os.environ.get("PGEN_KS_HOME", "M"))
+            for n, v in zip(sn, [p.get(m) for m in kn]):
+                p.set(n, v)
+            saved.append(sn)
+    saved.append(kn)
+    gs = [getg(sn) for sn in saved]
+    nds = [T.kdec_numden(g) for g in gs]
+    idens = T.batch_inv2([d for _, d in nds], tag)
+    F = [T.kdec_finish(g, nd[0], iv) for g, nd, iv in zip(gs, nds, idens)]
+    # top: the GS state reuses the 8 compressed-state homes (dead by now) plus
+    # four more; res: 6 + 6 coordinates in AGPRs + the workspace
+    V.declare12(res, os.environ.get("PGEN_KR_HOME", "AAAAAAMMMMMM"))
+    for i in range(6):
+        for c in (0, 1):
+            j = 2 * i + c
+            if j >= 8:
+                p.var("%s%d_%d" % (top, i, c), 1, os.environ.get("PGEN_KT_HOME", "A"))
+    V.set12(top, F[2])
+    V.set12(res, T.mul12(T.mul12(F[0], F[1]), F[2]))
+    # the top bits: squarings 1..6 above bit 57, multiply after squarings 3, 5, 6
+    # (loop counter 5..0 -> bits 3, 1, 0 of the mask)
+    assert [b - bits[2] for b in bits[3:]] == [3, 5, 6]
+    with p.loop(6) as L2:
+        V.set12(top, T.cyc_sqr(V.get12(top)))
+        with p.if_bit(0b1011, L2):
+            V.set12(res, T.mul12(V.get12(res), V.get12(top)))
+    V.set12(xv, T.conj12(V.get12(res)))
+
+
+def hard_part_loop(p, T, V, r):
+    """mod.rs:125-156 with the five exp_by_x calls as ONE loop body (counter
+    4..0 = calls a..e; the code between calls runs in branches on the counter),
+    so the final exponentiation's code holds one copy of exp_by_x.  Returns y1.
+        a: y1 = E(y0)                b: y2 = E'(y1)  (x >> 1)
+           y1 = conj(y1 conj(r)) y2  c: y2 = E(y1)   d: y3 = E(y2)
+           y1 = frob3(conj(conj(y1) ...)) ... (see below)    e: y2 = E(y3)"""
+    H = os.environ.get("PGEN_HP_HOME", "M")
+    for n in ("hr", "y0", "y1", "y2", "x"):
+        V.declare12(n, H)
+    V.set12("hr", r)
+    y0 = T.cyc_sqr(r)
+    V.set12("y0", y0)
+    V.set12("x", y0)
+    with p.loop(5) as L:
+        exp_by_x_karabina(p, T, V, "x", L, first_skip=3)
+        with p.if_bit(1 << 4, L):          # after a: y1 = E(y0)
+            V.set12("y1", V.get12("x"))
+        with p.if_bit(1 << 3, L):          # after b: y2 = E'(y1); y1 = conj(y1 conj(r)) y2
+            y2 = V.get12("x")
+            y1 = T.mul12(T.conj12(T.mul12(V.get12("y1"), T.conj12(V.get12("hr")))), y2)
+            V.set12("y1", y1)
+            V.set12("x", y1)
+        with p.if_bit(1 << 2, L):          # after c: y2 = E(y1)
+            V.set12("y2", V.get12("x"))
+        with p.if_bit(1 << 1, L):          # after d: y3 = E(y2) (stays in x)
+            y3 = V.get12("x")
+            y1 = V.get12("y1")
+            y1c = T.conj12(y1)
+            y3 = T.mul12(y3, y1c)
+            y1 = T.mul12(T.frob12(y1, 3), T.frob12(V.get12("y2"), 2))
+            V.set12("y1", y1)
+            V.set12("y2", y3)              # y2 holds y3 until the end
+            V.set12("x", y3)
+    # after e: x = E(y3); y3 is in y2
+    y2 = T.mul12(T.mul12(V.get12("x"), V.get12("y0")), V.get12("hr"))
+    y1 = T.mul12(V.get12("y1"), y2)
+    return T.mul12(y1, T.frob12(V.get12("y2"), 1))
+
+
+def _karabina():
+    return os.environ.get("PGEN_KARABINA", "1") == "1"
+
+
 def final_exp_prog(lanes=1, lazy=False, tower_cls=None, split=None):
     """lazy: False (Tower), True (TowerLazy) or "sq" (TowerLazySq);
     tower_cls overrides the tower class (coop.py: inversion as one op).
@@ -217,6 +335,11 @@ def final_exp_prog(lanes=1, lazy=False, tower_cls=None, split=None):
     else:
         T = {False: Tower, True: TowerLazy, "sq": TowerLazySq}[lazy](p)
     V = _Vars(p, lanes)
+    # one-lane programs invert in the kernel by binary GCD (emit.emit_binv) and
+    # exponentiate by x with compressed squarings; PGEN_KARABINA=0: Fermat +
+    # Granger-Scott (round 2)
+    kara = lanes == 1 and tower_cls is None and split is None and _karabina()
+    p.binv_ok = kara
     f = V.load12()
     if split is not None:
         assert lanes == 1 and split in ("norm", "inv")
@@ -235,6 +358,9 @@ def final_exp_prog(lanes=1, lazy=False, tower_cls=None, split=None):
     r = T.mul12(f1, f2)
     f2 = r
     r = T.mul12(T.frob12(r, 2), f2)
+    if kara:
+        V.store12(hard_part_loop(p, T, V, r))
+        return p
     x = X_ABS
     y0 = T.cyc_sqr(r)
     y1 = exp_by_x(p, T, V, y0, x, "a")

@@ -13,7 +13,8 @@ W64 = {  # operand positions that are 64-bit register pairs, per mnemonic
     "global_load_dwordx2": (0, 1), "global_load_dword": (1,), "global_store_dwordx2": (0, 1),
     "global_store_byte": (0,), "global_store_dwordx2_s": (1, 2), "global_load_dwordx2_s": (0, 2),
     "s_load_dwordx2": (0, 1), "s_mov_b64": (0, 1), "s_and_saveexec_b64": (0,), "s_bitcmp1_b64": (0,),
-    "s_cmp_eq_u64": (0,),
+    "s_cmp_eq_u64": (0,), "v_cmp_eq_u32_e64": (0,), "v_cmp_ne_u32_e64": (0,),
+    "v_cmp_lt_u64_e64": (0, 1, 2), "s_and_b64": (0, 1, 2), "s_or_b64": (0, 1, 2),
 }
 
 
@@ -80,8 +81,14 @@ class Renderer:
             return self.jump(a[0], "s_cbranch_execnz")
         if m in ("v_mad_u64_u32", "v_mad_i64_i32"):
             return ["%s %s, vcc, %s, %s, %s" % (m, o[0], o[1], o[2], o[3])]
+        if m.startswith("v_cmp_") and m.endswith("_e64"):
+            return ["%s %s, %s, %s" % (m, o[0], o[1], o[2])]
         if m.startswith("v_cmp_"):
             return ["%s vcc, %s, %s" % (m, o[0], o[1])]
+        if m == "v_sub_co_u32":
+            return ["v_sub_co_u32_e32 %s, vcc, %s, %s" % (o[0], o[1], o[2])]
+        if m == "v_subb_co_u32":
+            return ["v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (o[0], o[1], o[2])]
         if m == "v_cndmask_b32":
             return ["v_cndmask_b32 %s, %s, %s, vcc" % (o[0], o[1], o[2])]
         if m == "v_cndmask_b32_e64":

@@ -42,6 +42,43 @@ class Sim:
         self.count = 0
         self.hist = {}
         self.trace = None
+        self.ws = 0              # wait-state clock: +1 per instruction, +N+1 per s_nop N
+        self.sgpr_vwrite = {}    # SGPR number -> wait-state clock of its last VALU write
+
+    # gfx950: a VALU read of an SGPR (mask, carry-in or operand) must come two
+    # wait states after a VALU instruction wrote it (LLVM inserts s_nop 1 there)
+    VALU_SW = {"v_mad_u64_u32": "vcc", "v_mad_i64_i32": "vcc", "v_sub_co_u32": "vcc", "v_subb_co_u32": "vcc"}
+    VALU_SR = {"v_cndmask_b32": "vcc", "v_subb_co_u32": "vcc"}
+
+    def hazard(self, t):
+        m, a = t[0], t[1:]
+        if not m.startswith("v_"):
+            return
+        reads = set()
+        if m in self.VALU_SR:
+            reads.add(106)
+        if m.startswith("v_cmp") and not m.endswith("_e64"):
+            srcs = a
+        elif m.startswith("v_cmp"):
+            srcs = a[1:]
+        else:
+            srcs = a[1:]
+        for x in srcs:
+            if isinstance(x, int) and x >= 512:
+                reads.add(x - 512)
+        for r in reads:
+            for rr in (r, r + 1):
+                w = self.sgpr_vwrite.get(rr)
+                if w is not None and self.ws - w - 1 < 2:
+                    raise AssertionError("VALU read of s%d %d wait states after a VALU write (instr %d: %r)" % (
+                        rr, self.ws - w - 1, self.count, t))
+        writes = []
+        if m in self.VALU_SW or (m.startswith("v_cmp") and not m.endswith("_e64")):
+            writes.append(106)
+        elif m.startswith("v_cmp"):
+            writes.append(a[0] - 512)
+        for r in writes:
+            self.sgpr_vwrite[r] = self.sgpr_vwrite[r + 1] = self.ws
 
     # ---------- operand access ----------
     def chk(self, x):
@@ -99,6 +136,18 @@ class Sim:
         m = self.s[106] | (self.s[107] << 32)
         return (m >> (self.lane % 64)) & 1
 
+    def set_mask(self, sreg, bit):
+        """lane bit of a 64-bit SGPR-pair mask (sreg: operand number >= 512)"""
+        n = sreg - 512
+        m = self.s[n] | (self.s[n + 1] << 32)
+        b = self.lane % 64
+        m = (m & ~(1 << b)) | (int(bool(bit)) << b)
+        self.s[n], self.s[n + 1] = m & M32, m >> 32
+
+    def mask_bit(self, sreg):
+        n = sreg - 512
+        return ((self.s[n] | (self.s[n + 1] << 32)) >> (self.lane % 64)) & 1
+
     def async_wr(self, kind, x, val):
         if self.inflight:
             self.chk(x)
@@ -133,6 +182,8 @@ class Sim:
                 raise RuntimeError("step limit")
             m = t[0]
             self.hist[m] = self.hist.get(m, 0) + 1
+            self.hazard(t)
+            self.ws += (t[1] + 1) if m == "s_nop" else 1
             if m.startswith("ds_"):
                 self.seq["lgkm"] += 1
             elif m.startswith("global_"):
@@ -214,6 +265,37 @@ class Sim:
             wr(a[0], rd(a[1]))
         elif m == "v_mov_b64":
             wr64(a[0], rd64(a[1]))
+        elif m == "v_cmp_eq_u32_e64":
+            self.set_mask(a[0], rd(a[1]) == rd(a[2]))
+        elif m == "v_cmp_ne_u32_e64":
+            self.set_mask(a[0], rd(a[1]) != rd(a[2]))
+        elif m == "v_cmp_lt_u64_e64":
+            self.set_mask(a[0], rd64(a[1]) < rd64(a[2]))
+        elif m == "s_and_b64":
+            wr64(a[0], rd64(a[1]) & rd64(a[2]))
+        elif m == "s_or_b64":
+            wr64(a[0], rd64(a[1]) | rd64(a[2]))
+        elif m == "v_sub_co_u32":
+            r = rd(a[1]) - rd(a[2])
+            wr(a[0], r)
+            self.set_vcc(r < 0)
+        elif m == "v_subb_co_u32":
+            r = rd(a[1]) - rd(a[2]) - self.vcc()
+            wr(a[0], r)
+            self.set_vcc(r < 0)
+        elif m == "v_xad_u32":
+            wr(a[0], (rd(a[1]) ^ rd(a[2])) + rd(a[3]))
+        elif m == "v_xor_b32":
+            wr(a[0], rd(a[1]) ^ rd(a[2]))
+        elif m == "v_or3_b32":
+            wr(a[0], rd(a[1]) | rd(a[2]) | rd(a[3]))
+        elif m == "v_ffbh_u32":
+            x = rd(a[1])
+            wr(a[0], 32 - x.bit_length() if x else M32)
+        elif m == "v_max_u32":
+            wr(a[0], max(rd(a[1]), rd(a[2])))
+        elif m == "v_mad_u32_u24":
+            wr(a[0], (rd(a[1]) & 0xffffff) * (rd(a[2]) & 0xffffff) + rd(a[3]))
         elif m == "v_cmp_gt_u32":
             self.set_vcc(rd(a[0]) > rd(a[1]))
         elif m == "v_cmp_eq_u32":

@@ -196,12 +196,97 @@ class Tower:
         c02 = t.red2(t.add2(t.dbl2(t.sub2(t4, a2)), t4))
         return ((c00, c01, c02), (c10, c11, c12))
 
+    # ---------------- compressed cyclotomic squaring (Karabina) ----------------
+    # f = (a0 + a1 v + a2 v^2) + (b0 + b1 v + b2 v^2) w in the cyclotomic subgroup
+    # is determined by g = (a1, a2, b0, b2) (S. Karabina, "Squaring in cyclotomic
+    # subgroups", eprint 2010/542; the formulas of Aranha-Karabina-Longa-Gebotys-
+    # Lopez, eprint 2010/526, section 5, in this tower's coordinates).  Squaring
+    # g costs 6 Fq2 squarings against Granger-Scott's 9 on all of f; recovering
+    # a0, b1 costs one Fq2 division, so a run of squarings stays compressed and
+    # only the powers that are multiplied are decompressed, their divisions
+    # sharing one inversion (Montgomery's trick).  Checked against the Python
+    # model in tests/test_pgen.py (test_karabina_*).
+    def ksqr(self, g):
+        """g -> g^2 compressed:  a1' = 3(b0^2 + xi a2^2) - 2 a1,
+        a2' = 3(a1^2 + xi b2^2) - 2 a2,  b0' = 6 xi a1 b2 + 2 b0,  b2' = 6 a2 b0 + 2 b2"""
+        t = self
+        a1, a2, b0, b2 = g
+
+        def half(x, y, z, zy, xi_on_cross):
+            # x^2 + xi y^2 and 2 x y = (x + y)^2 - x^2 - y^2, then
+            # z' = 3 (x^2 + xi y^2) - 2 z  and  zy' = 6 [xi] x y + 2 zy
+            sx, sy = t.sqr2(x), t.sqr2(y)
+            sxy = t.sqr2(t.lim2(t.add2(x, y)))
+            s = t.red2(t.add2(sx, t.xi(sy)))
+            c = t.red2(t.sub2(sxy, t.add2(sx, sy)))
+            if xi_on_cross:
+                c = t.red2(t.xi(c))
+            nz = t.red2(t.add2(t.dbl2(t.sub2(s, z)), s))
+            nzy = t.red2(t.add2(t.dbl2(t.add2(c, zy)), c))
+            return nz, nzy
+
+        na2, nb0 = half(a1, b2, a2, b0, True)
+        na1, nb2 = half(b0, a2, a1, b2, False)
+        return (na1, na2, nb0, nb2)
+
+    def kdec_numden(self, g):
+        """the division that recovers b1 = num / den:  b0 != 0: (3 a1^2 - 2 a2 +
+        xi b2^2) / (4 b0);  b0 == 0: 2 a1 b2 / a2 (lane-wise select).  Only the
+        identity has b0 = a2 = 0 (then num = den = 0, and the shared inversion's
+        0 -> 0 gives b1 = 0, a0 = 1: the identity)."""
+        t, p = self, self.p
+        a1, a2, b0, b2 = g
+        s1 = t.sqr2(a1)
+        num1 = t.red2(t.sub2(t.add2(t.add2(t.dbl2(s1), s1), t.xi(t.sqr2(b2))), t.dbl2(a2)))
+        den1 = t.red2(t.dbl2(t.dbl2(b0)))
+        num2 = t.red2(t.dbl2(t.mul2(a1, b2)))
+        den2 = t.red2(a2)
+        z = [p.red_full(b0[0]), p.red_full(b0[1])]
+        num = (p.selz(z, num2[0], num1[0]), p.selz(z, num2[1], num1[1]))
+        den = (p.selz(z, den2[0], den1[0]), p.selz(z, den2[1], den1[1]))
+        return num, den
+
+    def kdec_finish(self, g, num, iden):
+        """b1 = num iden, a0 = xi (2 b1^2 + b0 b2 - 3 a1 a2) + 1"""
+        t = self
+        a1, a2, b0, b2 = g
+        b1 = t.mul2(num, iden)
+        m = t.mul2(a1, a2)
+        s = t.red2(t.sub2(t.add2(t.dbl2(t.sqr2(b1)), t.mul2(b0, b2)), t.add2(t.dbl2(m), m)))
+        a0 = t.red2(t.add2(t.xi(s), t.one2()))
+        return ((a0, a1, a2), (b0, b1, b2))
+
+    def inv2_direct(self, a, tag):
+        """Fq2 inverse (fq2.rs:138-155) with the base-field inversion as one op"""
+        p = self.p
+        n = p.sop(a[0], a[0], a[1], a[1])
+        i = self.inv_fq(n, tag)
+        return (p.mul(a[0], i), p.mul(p.neg(a[1]), i))
+
+    def batch_inv2(self, ds, tag):
+        """Montgomery's trick over Fq2 values: 3 (n - 1) products + one inverse"""
+        t = self
+        pre = [ds[0]]
+        for d in ds[1:]:
+            pre.append(t.mul2(pre[-1], d))
+        acc = t.inv2_direct(pre[-1], tag)
+        out = [None] * len(ds)
+        for k in range(len(ds) - 1, 0, -1):
+            out[k] = t.mul2(acc, pre[k - 1])
+            acc = t.mul2(acc, ds[k])
+        out[0] = acc
+        return out
+
     # ---------------- inversion ----------------
     def inv_fq(self, a, tag):
         """a^(q-2) (Fermat; the same value as fq.rs:849-902's Euclid for a != 0):
         a sliding window of 4 bits over the constant exponent -- 8 odd powers,
         then 380 squarings and 78 multiplications (463 products against 608 for
-        bitwise square-and-multiply); PGEN_INV_W=0 selects the bitwise form"""
+        bitwise square-and-multiply); PGEN_INV_W=0 selects the bitwise form.
+        One-lane programs with binary GCD (Prog.binv_ok): the in-kernel binary
+        GCD instead (~37 k instructions against ~300 k)."""
+        if getattr(self.p, "binv_ok", False):
+            return self.p.binv(self.p.red_full(a))
         W = int(os.environ.get("PGEN_INV_W", "4"))
         if W:
             return self._inv_fq_window(a, tag, W)
