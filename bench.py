@@ -34,10 +34,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# v_mad_u64_u32 issue ceiling, measured (profiles/r01_clock_probe.txt): 5.13
-# shader clocks per wave-instruction per SIMD at a sustained 2.39 GHz,
-# 1024 SIMDs x 64 lanes -> limb multiply-accumulates per second
-VALU_MAC_PEAK_T = 1024 * 64 / 5.13 * 2.39e9 / 1e12
+# v_mad_u64_u32 issue ceiling, measured at 1, 2, 4 and 8 waves per SIMD
+# (tools/valu_peak.hip, profiles/r03_valu_peak.txt): the best sustained rate,
+# 8 waves per SIMD, 8 independent chains -> limb multiply-accumulates per
+# second.  The pairing kernels run ONE wave per SIMD at batch 2^16 (2^16 lanes
+# = 1024 waves = the chip's 1024 SIMDs), whose own ceiling is VALU_MAC_1WAVE_T.
+VALU_MAC_PEAK_T = 35.96
+VALU_MAC_1WAVE_T = 21.32
 # issue ceiling of the one-wave-per-SIMD pairing kernels: one wave issues at most
 # one instruction per 4 clk (SQ: one ACTIVE_INST quad-cycle per instruction), at
 # the 2.33 GHz the chip holds under them (GRBM_GUI_ACTIVE, profiles/r02_cyc_probe.txt)
@@ -55,6 +58,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 16, help="pairings per GPU per step")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="pairing workload: a fixed global batch split over the ranks (contiguous shards, "
+                         "pairing_amd/shard.py) instead of --batch per GPU; BASELINE config 5 is "
+                         "--gpus 8 --global-batch 1048576")
+    ap.add_argument("--stub-echo", action="store_true",
+                    help="with --cpu-stub: each rank echoes its shard instead of computing pairings "
+                         "(plumbing test of large shapes)")
     ap.add_argument("--workload", choices=["pairing", "fq_mul", "fr_mul", "wnaf", "decode", "msm", "verify"],
                     default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
@@ -103,12 +113,17 @@ def dist_env():
     return ws, rank, local
 
 
-def make_pairs(n, rank, seed=0):
+def make_pairs(n, rank, seed=0, span=None):
     """2^16 pairs tiled from a pool of 256 x 256 distinct point combinations,
-    1/128 of them with an infinity side (mod.rs:50-54)."""
+    1/128 of them with an infinity side (mod.rs:50-54).  Rows rank*n ..
+    rank*n + n of the global sequence, or rows span = (start, stop) (a rank's
+    shard of a --global-batch): each rank builds only its own rows."""
     d = np.load(os.path.join(ROOT, "tests", "golden", "bench_points.npz"))
     g1, g2 = d["g1"], d["g2"]
-    idx = np.arange(n, dtype=np.int64) + rank * n + seed
+    if span is not None:
+        idx = np.arange(span[0], span[1], dtype=np.int64) + seed
+    else:
+        idx = np.arange(n, dtype=np.int64) + rank * n + seed
     p = g1[idx % 256].copy()
     q = g2[(idx // 256 + idx * 7) % 256].copy()
     inf = np.nonzero(idx % 128 == 5)[0]
@@ -262,15 +277,26 @@ def main_cpu_stub(args, ws, rank):
     import torch.distributed as dist
     from oracle import binding as oracle
     from pairing_amd.shard import gather_rows_to_root
+    from pairing_amd.shard import shard_range
     if ws > 1:
         dist.init_process_group("gloo")
-    n = args.batch
-    p_np, q_np = make_pairs(n, rank)
+    if args.global_batch:
+        span = shard_range(args.global_batch, ws, rank)
+        n, n_global = span[1] - span[0], args.global_batch
+    else:
+        span, n, n_global = None, args.batch, args.batch * ws
+    p_np, q_np = make_pairs(n, rank, span=span)
 
     def step():
-        out = torch.from_numpy(oracle.pairing(p_np, q_np, 1).view(np.int64))
+        if args.stub_echo:
+            out = torch.zeros((n, 72), dtype=torch.int64)
+            out[:, :13] = torch.from_numpy(p_np.view(np.int64))
+        else:
+            out = torch.from_numpy(oracle.pairing(p_np, q_np, 1).view(np.int64))
         if ws > 1:
-            gather_rows_to_root(out, ws * n)
+            res = gather_rows_to_root(out, n_global)
+            if rank == 0 and res.shape[0] != n_global:
+                raise RuntimeError("gathered %d rows, global batch %d" % (res.shape[0], n_global))
 
     for _ in range(args.warmup):
         step()
@@ -286,11 +312,11 @@ def main_cpu_stub(args, ws, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     if rank == 0:
-        print(json.dumps({"metric": "launcher test (cpu stub)", "value": ws * n * args.steps / elapsed,
+        print(json.dumps({"metric": "launcher test (cpu stub)", "value": n_global * args.steps / elapsed,
                           "unit": "pairings/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
                           "vs_baseline": None, "dtype": "u64", "data": "cpu stub: oracle per rank, gloo gather",
-                          "config": {"workload": "cpu stub", "batch_per_gpu": n, "global_batch": n * ws,
+                          "config": {"workload": "cpu stub", "batch_per_gpu": n, "global_batch": n_global,
                                      "parallelism": "shard%d+gather" % ws if ws > 1 else "single"}}), flush=True)
     if ws > 1:
         dist.destroy_process_group()
@@ -333,8 +359,16 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     k_ms = {"a": [], "b": [], "c": []}
 
+    n_global = n * ws
     if args.workload == "pairing":
-        p_np, q_np = make_pairs(n, rank)
+        span = None
+        if args.global_batch:
+            # config 5 shape: a fixed global batch in contiguous shards, each
+            # rank building and staging only its own rows
+            from pairing_amd.shard import shard_range
+            span = shard_range(args.global_batch, ws, rank)
+            n, n_global = span[1] - span[0], args.global_batch
+        p_np, q_np = make_pairs(n, rank, span=span)
         p = torch.from_numpy(p_np.view(np.int64)).to(dev)
         q = torch.from_numpy(q_np.view(np.int64)).to(dev)
         out = pdev.empty_records(n, 72, dev)
@@ -352,7 +386,7 @@ def main():
                 ev[2].record(stream)
             if dist_on:
                 # the path's one exchange: every shard's Fq12 results to rank 0 (RCCL over xGMI)
-                gather_rows_to_root(out, ws * n)
+                gather_rows_to_root(out, n_global)
     elif args.workload == "wnaf":
         # config 3: Wnaf::new().base(g, 2^18).scalar(s_i) + G1::batch_normalization
         n = args.batch if args.batch != (1 << 16) else (1 << 18)
@@ -544,11 +578,15 @@ def main():
             fe = float(np.mean(k_ms["b"]))
             dom_name, dom_ms, dom_bytes = ("final_exponentiation", fe, FE_BYTES) if fe >= ml else \
                 ("miller_loop_fused", ml, ML_BYTES)
-            value = ws * n * args.steps / elapsed
+            value = n_global * args.steps / elapsed
             metric, unit = "BLS12-381 pairings/sec at batch 2^16", "pairings/s"
-            config = {"workload": "bls12_381 e(P_i,Q_i) batch (fused G2 prepare + Miller loop + final exp)",
+            wl = "bls12_381 e(P_i,Q_i) batch (fused G2 prepare + Miller loop + final exp)"
+            if args.global_batch:
+                wl += "; fixed global batch %d in %d contiguous shards (BASELINE config 5 at 2^20 over 8)" % (
+                    n_global, ws)
+            config = {"workload": wl,
                       "kernel_variant": ["gen", "gen2", "coop", "gen"][int(os.environ.get("PA_PAIRING_KERNEL", "0"))],
-                      "batch_per_gpu": n, "global_batch": n * ws, "parallelism": "shard%d+rccl_gather" % ws
+                      "batch_per_gpu": n, "global_batch": n_global, "parallelism": "shard%d+rccl_gather" % ws
                       if dist_on else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}
         elif args.workload == "wnaf":
@@ -644,6 +682,7 @@ def main():
                     "peak": round(VALU_MAC_PEAK_T, 3), "unit": "T limb-MAC/s (28x28-bit v_mad_u64_u32)",
                     "frac": mac_rate / VALU_MAC_PEAK_T, "traffic": traffic, "macs_per_unit": macs,
                     "avg_launch_ms": round(dom_ms, 4),
+                    "peak_one_wave_per_simd": VALU_MAC_1WAVE_T, "frac_one_wave": mac_rate / VALU_MAC_1WAVE_T,
                     "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS,
                             "bytes_per_unit": dom_bytes}}
             instr = wk.get("instructions")

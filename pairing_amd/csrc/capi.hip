@@ -530,6 +530,8 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
     hipEvent_t* h2d = c->ev;        // [k]: chunk's inputs copied (pinned in[k] free again)
     hipEvent_t* done = c->ev + 2;   // [k]: chunk's kernels finished (device in[k], ml[k] free)
     hipEvent_t* d2h = c->ev + 4;    // [k * kPieces + j]: piece j of the chunk's results in pinned out[k]
+    hipEvent_t* outk = c->ev + 12;  // [k]: every piece of the chunk's results copied (device out[k] free);
+                                    // recorded after the piece loop, so an empty last piece cannot leave it stale
     auto piece = [&](size_t cnt, size_t j, size_t* lo) {
         const size_t per = (cnt + kPieces - 1) / kPieces;
         *lo = per * j < cnt ? per * j : cnt;
@@ -573,7 +575,7 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
         PA_TRY(hipEventRecord(h2d[k], c->copy), "event");
         stamp("staged in", ci);
         PA_TRY(hipStreamWaitEvent(ks, h2d[k], 0), "stream wait");
-        if (ci >= 2) PA_TRY(hipStreamWaitEvent(ks, d2h[k * kPieces + kPieces - 1], 0), "stream wait");
+        if (ci >= 2) PA_TRY(hipStreamWaitEvent(ks, outk[k], 0), "stream wait");
         PA_TRY(ml_launch((const uint64_t*)dev_p, (const uint64_t*)dev_q, dev_ml, cnt, ks), "kernel launch");
         // Engine::pairing unwraps: a Miller-loop value is never zero, ok is not reported
         PA_TRY(fe_launch(dev_ml, dev_out, nullptr, cnt, ks), "kernel launch");
@@ -588,6 +590,7 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
                    "D2H copy");
             PA_TRY(hipEventRecord(d2h[k * kPieces + j], c->copy_out), "event");
         }
+        PA_TRY(hipEventRecord(outk[k], c->copy_out), "event");
         stamp("enqueued", ci);
         if (ci >= 1) {
             const int rc = drain(ci - 1);

@@ -10,10 +10,10 @@
 // device keeps a pool of workspaces; a workspace records the stream and an
 // event of its last launch and is handed to a new launch only if that launch
 // is on the same stream (stream order serializes them) or the event has
-// completed.  Otherwise a new workspace is allocated, so concurrent callers
-// on different streams (pairing_amd.h: every entry point is reentrant) each
-// get their own.  The pool only grows to the number of launches in flight at
-// once.
+// completed (acquire() below).  Otherwise a new workspace is allocated, so
+// concurrent callers on different streams (pairing_amd.h: every entry point is
+// reentrant) each get their own.  The pool only grows to the number of
+// launches in flight at once.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
@@ -121,19 +121,33 @@ size_t wave_bytes() {
 }
 
 // A workspace of at least `need` bytes that no unfinished launch on another
-// stream uses (caller holds g_mu).
+// stream uses (caller holds g_mu).  Reuse is decided by the completion event;
+// an unfinished workspace of the same stream handle is also reused, with the
+// new launch made to wait for that event: on the same stream the wait changes
+// nothing (stream order), and if the handle now names another stream (a
+// destroyed stream's handle reused, hipStreamPerThread from two threads) it
+// keeps the two launches apart.  A finished workspace that is too small is
+// grown in place, whatever stream used it.
 hipError_t acquire(GenDevice& d, size_t need, hipStream_t stream, Workspace** out) {
     Workspace* idle_small = nullptr;
+    Workspace* same = nullptr;
     for (auto& w : d.pool) {
-        const bool free_now = w.last == stream || hipEventQuery(w.done) == hipSuccess;
-        if (!free_now) continue;
-        if (w.bytes >= need) {
-            *out = &w;
-            return hipSuccess;
+        if (hipEventQuery(w.done) == hipSuccess) {
+            if (w.bytes >= need) {
+                *out = &w;
+                return hipSuccess;
+            }
+            if (!idle_small) idle_small = &w;
+        } else if (w.last == stream && w.bytes >= need && !same) {
+            same = &w;
         }
-        if (!idle_small && w.last != stream) idle_small = &w;
     }
     hipError_t e;
+    if (same) {
+        if ((e = hipStreamWaitEvent(stream, same->done, 0)) != hipSuccess) return e;
+        *out = same;
+        return hipSuccess;
+    }
     if (idle_small) {  // its last launch has finished: grow it in place
         if ((e = hipFree(idle_small->p)) != hipSuccess) return e;
         idle_small->p = nullptr;

@@ -15,8 +15,8 @@
 // = at most 33 mixed additions (madd-2007-bl) per scalar and no doublings,
 // against ~255 doublings + 16 additions for wNAF.
 //
-// batch_normalization.  Montgomery's trick over chunks of CHUNK points per
-// lane with one Fermat inversion per chunk; zero and already-normalized points
+// batch_normalization.  Montgomery's trick over chunks of kNormChunk points per
+// lane with one binary-GCD inversion per chunk (bgcd.h); zero and already-normalized points
 // are left bit-for-bit untouched, as in the reference (ec.rs:255-257, 271, 285).
 #include <mutex>
 
@@ -39,9 +39,9 @@ constexpr int kNormChunk = 8;         // points per lane in batch_normalization 
 //   s P = rem P + q (x^2 P) = rem P + q psi(P),  psi(x, y) = (beta x, -y),
 // rem < 2^128, q < 2^129: 17 windows of each over rows T[0..16] and their
 // psi images T[17..33], after a base chain of 128 doublings instead of 256.
-// A base outside G1 (or off the curve) takes the plain 33-window comb; both
-// paths are launched, each kernel reading the membership flag and returning
-// at once when it is not its path's.
+// A base outside G1 (or off the curve) takes a 256-bit double-and-add ladder
+// (k_g1_fixed_base_ladder); both paths are launched, each kernel reading the
+// membership flag and returning at once when it is not its path's.
 constexpr int kGlvWindows = 17;
 constexpr int kTableRows = 2 * kGlvWindows;   // >= kCombWindows
 static_assert(kTableRows >= kCombWindows, "table rows");
@@ -536,8 +536,8 @@ hipError_t launch_g1_glv_mul(const uint64_t* base, const uint64_t* table_fl, con
 // doubles toward part p + 1's bases while side stream 1 builds part p's rows
 // and their phi images and the caller's stream multiplies part p.  Side
 // stream 2 runs the membership check from the start; after the last GLV
-// multiply the caller's stream waits for it and runs the plain 33-window comb
-// (table + multiply), whose kernels return at once unless the check failed.
+// multiply the caller's stream waits for it and runs the double-and-add ladder
+// (k_g1_fixed_base_ladder), which returns at once unless the check failed.
 // Equal as points to launch_g1_comb_table + launch_g1_comb_mul.
 hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
                                 uint64_t* table_fl, uint64_t* workspace, hipStream_t stream) {
@@ -614,7 +614,7 @@ hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, u
                                wb[p], wb[p + 1], p == 0 ? 1 : 0, nullptr);
             ck(hipGetLastError());
         }
-        // fallback: the plain comb, live only when the base failed the check
+        // fallback: the double-and-add ladder, live only when the base failed the check
         if (err == hipSuccess && ck(hipStreamWaitEvent(mul, ev[1 + 2 * parts], 0)))
             ck(glv_fallback(base, workspace, scalars, out, n, mul));
     }

@@ -25,6 +25,33 @@ def _dptr(t, width, name):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _rows(t, n, name):
+    """t holds at least the n records the call writes or reads"""
+    if t.shape[0] < n:
+        raise ValueError("%s has %d rows, the call needs %d" % (name, t.shape[0], n))
+
+
+def _flags(ok, n, name="ok"):
+    """a contiguous uint8 CUDA tensor of at least n flags, or None"""
+    if ok is None:
+        return ctypes.c_void_p(0)
+    if not ok.is_cuda or not ok.is_contiguous() or ok.dtype != torch.uint8 or ok.numel() < n:
+        raise ValueError("%s must be a contiguous uint8 CUDA tensor of >= %d elements" % (name, n))
+    return ctypes.c_void_p(ok.data_ptr())
+
+
+def _words(t, need, name):
+    """a contiguous int64 CUDA buffer of at least `need` 8-byte words"""
+    if not t.is_cuda or not t.is_contiguous() or t.dtype != torch.int64 or t.numel() < need:
+        raise ValueError("%s must be a contiguous int64 CUDA tensor of >= %d words" % (name, need))
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _fb_table(table, ws):
+    return (_words(table, int(_lib.pa_g1_fixed_base_table_words()), "table"),
+            _words(ws, int(_lib.pa_g1_fixed_base_workspace_words()), "ws"))
+
+
 def empty_records(n, width, device):
     return torch.empty((n, width), dtype=torch.int64, device=device)
 
@@ -32,8 +59,10 @@ def empty_records(n, width, device):
 def fq_mul(a, b, out, stream=None):
     """Fq::mul_assign over a batch resident in HBM (BASELINE config 2)."""
     n = a.shape[0]
-    call("pa_fq_mul_batch_device", _dptr(a, W_FQ, "a"), _dptr(b, W_FQ, "b"), _dptr(out, W_FQ, "out"), n,
-         _stream_ptr(stream))
+    args = (_dptr(a, W_FQ, "a"), _dptr(b, W_FQ, "b"), _dptr(out, W_FQ, "out"))
+    _rows(b, n, "b")
+    _rows(out, n, "out")
+    call("pa_fq_mul_batch_device", *args, n, _stream_ptr(stream))
 
 
 def fq_mul_soa(a, b, out, stream=None):
@@ -51,28 +80,39 @@ def fq_mul_soa(a, b, out, stream=None):
 
 def miller_loop(p, q, out, stream=None):
     """Fused-prepare single-pair Miller loops: out[i] = miller_loop([(p[i], q[i].prepare())])."""
-    call("pa_miller_loop_fused_batch_device", _dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"),
-         _dptr(out, W_FQ12, "out"), p.shape[0], _stream_ptr(stream))
+    n = p.shape[0]
+    args = (_dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"), _dptr(out, W_FQ12, "out"))
+    _rows(q, n, "q")
+    _rows(out, n, "out")
+    call("pa_miller_loop_fused_batch_device", *args, n, _stream_ptr(stream))
 
 
 def final_exponentiation(f, out, ok=None, stream=None):
-    okp = ctypes.c_void_p(ok.data_ptr()) if ok is not None else ctypes.c_void_p(0)
-    call("pa_final_exponentiation_batch_device", _dptr(f, W_FQ12, "f"), _dptr(out, W_FQ12, "out"), okp,
-         f.shape[0], _stream_ptr(stream))
+    n = f.shape[0]
+    args = (_dptr(f, W_FQ12, "f"), _dptr(out, W_FQ12, "out"), _flags(ok, n))
+    _rows(out, n, "out")
+    call("pa_final_exponentiation_batch_device", *args, n, _stream_ptr(stream))
 
 
 def pairing(p, q, out, scratch, stream=None):
     """out[i] = e(p[i], q[i]) for a batch resident in HBM (BASELINE config 4)."""
-    call("pa_pairing_batch_device", _dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"), _dptr(out, W_FQ12, "out"),
-         _dptr(scratch, W_FQ12, "scratch"), p.shape[0], _stream_ptr(stream))
+    n = p.shape[0]
+    args = (_dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"), _dptr(out, W_FQ12, "out"), _dptr(scratch, W_FQ12, "scratch"))
+    for t, name in ((q, "q"), (out, "out"), (scratch, "scratch")):
+        _rows(t, n, name)
+    call("pa_pairing_batch_device", *args, n, _stream_ptr(stream))
 
 
 def multi_pairing(p, q, out, ok, work, stream=None):
     """final_exponentiation(miller_loop(pairs)) over pairs resident in HBM (the verifier's
     batch check, mod.rs:40-160): out (1, 72), ok (1,) uint8, work (n, 72) scratch."""
-    call("pa_multi_pairing_device", _dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"), p.shape[0],
-         _dptr(out, W_FQ12, "out"), ctypes.c_void_p(ok.data_ptr()), _dptr(work, W_FQ12, "work"),
-         _stream_ptr(stream))
+    n = p.shape[0]
+    args = (_dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"))
+    _rows(q, n, "q")
+    _rows(out, 1, "out")
+    _rows(work, n, "work")   # the per-pair Miller values and the product tree
+    call("pa_multi_pairing_device", *args, n, _dptr(out, W_FQ12, "out"), _flags(ok, 1),
+         _dptr(work, W_FQ12, "work"), _stream_ptr(stream))
 
 
 def g1_fixed_base_table(base, stream=None):
@@ -87,30 +127,36 @@ def g1_fixed_base_table(base, stream=None):
 
 def g1_fixed_base_mul(table, scalars, out, stream=None):
     """out[i] = scalars[i] * base (config 3), scalars (n,4) int64 FrRepr."""
-    call("pa_g1_fixed_base_mul_device", ctypes.c_void_p(table.data_ptr()), _dptr(scalars, 4, "scalars"),
-         _dptr(out, W_G1, "out"), scalars.shape[0], _stream_ptr(stream))
+    n = scalars.shape[0]
+    args = (_words(table, int(_lib.pa_g1_fixed_base_table_words()), "table"), _dptr(scalars, 4, "scalars"),
+            _dptr(out, W_G1, "out"))
+    _rows(out, n, "out")
+    call("pa_g1_fixed_base_mul_device", *args, n, _stream_ptr(stream))
 
 
 def g1_fixed_base_glv_table(base, table, ws, stream=None):
     """GLV stage 1: table rows, their phi images and the membership flag (ws)."""
-    call("pa_g1_fixed_base_glv_table_device", _dptr(base, W_G1, "base"), ctypes.c_void_p(table.data_ptr()),
-         ctypes.c_void_p(ws.data_ptr()), _stream_ptr(stream))
+    call("pa_g1_fixed_base_glv_table_device", _dptr(base, W_G1, "base"), *_fb_table(table, ws),
+         _stream_ptr(stream))
 
 
 def g1_fixed_base_glv_mul(base, table, ws, scalars, out, stream=None):
-    """GLV stage 2: out[i] = scalars[i] * base (plain-comb fallback inside)."""
-    call("pa_g1_fixed_base_glv_mul_device", _dptr(base, W_G1, "base"), ctypes.c_void_p(table.data_ptr()),
-         ctypes.c_void_p(ws.data_ptr()), _dptr(scalars, 4, "scalars"), _dptr(out, W_G1, "out"), scalars.shape[0],
-         _stream_ptr(stream))
+    """GLV stage 2: out[i] = scalars[i] * base (for a base outside G1 the
+    double-and-add ladder k_g1_fixed_base_ladder takes over inside)."""
+    n = scalars.shape[0]
+    args = (_dptr(base, W_G1, "base"), *_fb_table(table, ws), _dptr(scalars, 4, "scalars"), _dptr(out, W_G1, "out"))
+    _rows(out, n, "out")
+    call("pa_g1_fixed_base_glv_mul_device", *args, n, _stream_ptr(stream))
 
 
 def g1_wnaf_fixed_base(base, scalars, out, table, ws, stream=None):
     """out[i] = scalars[i] * base with the table built in the same call (its
     serial base chain overlapped with the multiply); table / ws as returned by
     fixed_base_buffers()."""
-    call("pa_g1_wnaf_fixed_base_device", _dptr(base, W_G1, "base"), _dptr(scalars, 4, "scalars"),
-         _dptr(out, W_G1, "out"), scalars.shape[0], ctypes.c_void_p(table.data_ptr()),
-         ctypes.c_void_p(ws.data_ptr()), _stream_ptr(stream))
+    n = scalars.shape[0]
+    args = (_dptr(base, W_G1, "base"), _dptr(scalars, 4, "scalars"), _dptr(out, W_G1, "out"))
+    _rows(out, n, "out")
+    call("pa_g1_wnaf_fixed_base_device", *args, n, *_fb_table(table, ws), _stream_ptr(stream))
 
 
 def fixed_base_buffers(dev):
@@ -137,16 +183,21 @@ def g2_fixed_base_buffers(dev):
 
 def g2_wnaf_fixed_base(base, scalars, out, table, ws, stream=None):
     """out[i] = scalars[i] * base for G2 (base a (1,36) Jacobian record)."""
-    call("pa_g2_wnaf_fixed_base_device", _dptr(base, W_G2, "base"), _dptr(scalars, 4, "scalars"),
-         _dptr(out, W_G2, "out"), scalars.shape[0], ctypes.c_void_p(table.data_ptr()),
-         ctypes.c_void_p(ws.data_ptr()), _stream_ptr(stream))
+    n = scalars.shape[0]
+    args = (_dptr(base, W_G2, "base"), _dptr(scalars, 4, "scalars"), _dptr(out, W_G2, "out"))
+    _rows(out, n, "out")
+    call("pa_g2_wnaf_fixed_base_device", *args, n,
+         _words(table, int(_lib.pa_g2_fixed_base_table_words()), "table"),
+         _words(ws, int(_lib.pa_g2_fixed_base_workspace_words()), "ws"), _stream_ptr(stream))
 
 
 def group_add(group, a, b, out, stream=None):
     """CurveProjective::add_assign over Jacobian rows in HBM: out = a + b (group 1 or 2)."""
     w = W_G1 if group == 1 else W_G2
-    call("pa_g%d_add_batch_device" % group, _dptr(a, w, "a"), _dptr(b, w, "b"), _dptr(out, w, "out"),
-         a.shape[0], _stream_ptr(stream))
+    args = (_dptr(a, w, "a"), _dptr(b, w, "b"), _dptr(out, w, "out"))
+    _rows(b, a.shape[0], "b")
+    _rows(out, a.shape[0], "out")
+    call("pa_g%d_add_batch_device" % group, *args, a.shape[0], _stream_ptr(stream))
 
 
 def decode(group, enc, compressed, checked, out, status, stream=None):
@@ -167,8 +218,10 @@ def decode(group, enc, compressed, checked, out, status, stream=None):
 
 def fr_mul(a, b, out, stream=None):
     """Fr::mul_assign (fr.rs:438-465) over a batch resident in HBM, rows (n, 4)."""
-    call("pa_fr_mul_batch_device", _dptr(a, 4, "a"), _dptr(b, 4, "b"), _dptr(out, 4, "out"), a.shape[0],
-         _stream_ptr(stream))
+    args = (_dptr(a, 4, "a"), _dptr(b, 4, "b"), _dptr(out, 4, "out"))
+    _rows(b, a.shape[0], "b")
+    _rows(out, a.shape[0], "out")
+    call("pa_fr_mul_batch_device", *args, a.shape[0], _stream_ptr(stream))
 
 
 def multiexp_workspace(group, n, device):

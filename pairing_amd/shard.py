@@ -48,17 +48,24 @@ def gather_rows_to_root(local, n_global, root=0, group=None):
     return torch.cat([bufs[r][:sizes[r]] for r in range(world)], dim=0)
 
 
-def sharded_batch(p, q, compute, root=0, group=None):
-    """out[i] = compute(p, q)[i] over the global batch, sharded across ranks.
-
-    p, q: the full global batch on every rank (each rank reads only its
-    shard), compute: (p_shard, q_shard) -> (n_shard, w) tensor on this rank's
-    device.  Returns the (n, w) result on root, None elsewhere."""
+def sharded_batch_from(load, n, compute, root=0, group=None):
+    """out[i] over a global batch of n pairings, sharded across ranks, where
+    each rank stages ONLY its own shard: load(start, stop) -> (p_shard,
+    q_shard) (from a file, a memmap or a generator), compute: (p_shard,
+    q_shard) -> (n_shard, w) tensor on this rank's device.  Returns the (n, w)
+    result on root, None elsewhere."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    a, b = shard_range(p.shape[0], world, rank)
-    local = compute(p[a:b], q[a:b])
-    return gather_rows_to_root(local, p.shape[0], root=root, group=group)
+    a, b = shard_range(n, world, rank)
+    local = compute(*load(a, b))
+    return gather_rows_to_root(local, n, root=root, group=group)
+
+
+def sharded_batch(p, q, compute, root=0, group=None):
+    """sharded_batch_from over indexable p, q (arrays, memmaps, tensors): each
+    rank slices its own rows, so a memmap'd global batch is read only shard by
+    shard."""
+    return sharded_batch_from(lambda a, b: (p[a:b], q[a:b]), p.shape[0], compute, root=root, group=group)
 
 
 def sharded_product(p, q, local_product, combine, root=0, group=None):

@@ -92,3 +92,46 @@ def test_errors_are_reported_not_aborted():
     rc = lib.pa_fq_mul_batch(None, None, None, 5)
     assert rc == -1
     assert b"null" in lib.pa_last_error()
+
+
+def test_device_layer_rejects_undersized_buffers():
+    """pairing_amd.device validates what the kernels would write past (ADVICE
+    r02): row counts of q / out / work against p, the ok flags' dtype and
+    size, and the fixed-base table / workspace sizes -- before any device call,
+    so these checks run without a GPU on CPU tensors shaped like the real ones"""
+    import pytest
+    import torch
+    import pairing_amd.device as pdev
+
+    class FakeCuda:
+        """shape/dtype/contiguity of a tensor, reporting is_cuda"""
+        def __init__(self, t):
+            self.t = t
+            self.is_cuda = True
+            self.shape, self.dtype = t.shape, t.dtype
+
+        def is_contiguous(self):
+            return True
+
+        def dim(self):
+            return self.t.dim()
+
+        def numel(self):
+            return self.t.numel()
+
+        def data_ptr(self):
+            return 0
+
+    f = lambda *s, dt=torch.int64: FakeCuda(torch.zeros(*s, dtype=dt))  # noqa: E731
+    with pytest.raises(ValueError, match="work"):
+        pdev.multi_pairing(f(4, 13), f(4, 25), f(1, 72), f(1, dt=torch.uint8), f(3, 72))
+    with pytest.raises(ValueError, match="q"):
+        pdev.multi_pairing(f(4, 13), f(3, 25), f(1, 72), f(1, dt=torch.uint8), f(4, 72))
+    with pytest.raises(ValueError, match="ok"):
+        pdev.multi_pairing(f(4, 13), f(4, 25), f(1, 72), f(1, dt=torch.int64), f(4, 72))
+    with pytest.raises(ValueError, match="ok"):
+        pdev.final_exponentiation(f(5, 72), f(5, 72), f(4, dt=torch.uint8))
+    with pytest.raises(ValueError, match="out"):
+        pdev.miller_loop(f(5, 13), f(5, 25), f(4, 72))
+    with pytest.raises(ValueError, match="table"):
+        pdev.g1_wnaf_fixed_base(f(1, 18), f(8, 4), f(8, 18), f(3), f(10 ** 6))

@@ -49,3 +49,28 @@ def test_bench_fails_when_fewer_devices_than_gpus():
     r = _run(["--gpus", str(max(n, 2)), "--steps", "1", "--warmup", "0"])
     assert r.returncode == 2
     assert "visible" in r.stderr
+
+
+def test_bench_config5_shape_global_batch():
+    """BASELINE config 5 (2^20 pairings over 8 GPUs) as the launcher runs it:
+    `bench.py --gpus 8 --global-batch 1048576` starts 8 ranks, each builds
+    only its 2^17-row shard (make_pairs(span=...)), and the root gathers all
+    2^20 result rows (checked inside the stub).  Here with gloo ranks that echo
+    their shard instead of computing pairings (plumbing only)."""
+    r = _run(["--gpus", "8", "--steps", "1", "--warmup", "0", "--global-batch", str(1 << 20),
+              "--cpu-stub", "--stub-echo"], timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_lines(r.stdout)[0]
+    assert line["n_gpus"] == 8
+    assert line["config"]["global_batch"] == 1 << 20
+    assert line["config"]["batch_per_gpu"] == 1 << 17
+    assert line["config"]["parallelism"] == "shard8+gather"
+
+
+def test_bench_global_batch_ragged_shards():
+    """a global batch that does not divide: shards differ by one row, the
+    root still gathers exactly the global batch (oracle compute, 2 ranks)"""
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--global-batch", "7", "--cpu-stub"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_lines(r.stdout)[0]
+    assert line["config"]["global_batch"] == 7 and line["config"]["batch_per_gpu"] == 4

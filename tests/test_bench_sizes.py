@@ -159,6 +159,30 @@ def test_pairing_host_pipeline_chunks_and_threads(gpu, oracle, monkeypatch):
     np.testing.assert_array_equal(np.concatenate(res), exp)
 
 
+def test_pairing_host_pipeline_pieces_with_empty_last_piece(oracle):
+    """the pipelined host path cut into pieces (PA_PIPELINE_PIECES=4, read once
+    per process, hence a child process) with chunks of 5 pairs: the last piece
+    of every chunk is empty (per = 2: 2 + 2 + 1 + 0), so the kernels' wait for
+    the D2H of chunk ci-2 must not hang on that piece's event (ADVICE r02,
+    capi.hip: one 'chunk copied out' event after the piece loop)"""
+    import subprocess
+    import sys
+    code = ("import numpy as np, sys; sys.path[:0] = [%r, %r]; import bench, pairing_amd; "
+            "p, q = bench.make_pairs(23, 0, seed=9); np.save(sys.argv[1], pairing_amd.pairing(p, q))"
+            % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+               os.path.dirname(os.path.abspath(__file__))))
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "out.npy")
+        env = dict(os.environ, PA_PIPELINE_CHUNK="5", PA_PIPELINE_PIECES="4")
+        r = subprocess.run([sys.executable, "-c", code, path], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        got = np.load(path)
+    import bench
+    p, q = bench.make_pairs(23, 0, seed=9)
+    np.testing.assert_array_equal(got, oracle.pairing(p, q, _threads()))
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 5])
 def test_multi_pairing_device_matches_oracle(gpu, oracle, n):
     """bench.py --workload verify: pa_multi_pairing_device (cooperative Miller
@@ -264,3 +288,62 @@ def test_fq_mul_soa_device_bit_exact(gpu, oracle, n):
     torch.cuda.synchronize()
     got = np.ascontiguousarray(out.cpu().numpy().view(np.uint64).T)
     np.testing.assert_array_equal(got, oracle.fq_mul(a, b))
+
+
+def _config3_inputs(n):
+    """bench.py --workload wnaf's inputs (config 3): the G1 base of
+    tests/golden/bench_points.npz with z = 1 and the tiled scalars"""
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bench_points.npz"))
+    base = np.zeros((1, 18), np.uint64)
+    base[0, :12] = d["g1"][0, :12]
+    base[0, 12:18] = np.array([0x760900000002fffd, 0xebf4000bc40c0002, 0x5f48985753c758ba,
+                               0x77ce585370525745, 0x5c071a97a256ec6d, 0x15f65ec3fa80e493], np.uint64)
+    s = np.ascontiguousarray(d["s1"][np.arange(n) % 256])
+    s[:, 0] ^= np.arange(n, dtype=np.uint64) << np.uint64(8)
+    return base, s
+
+
+def test_config3_full_size_bit_exact(gpu, oracle):
+    """config 3 exactly as bench.py times it -- pa_g1_wnaf_fixed_base_device then
+    pa_g1_batch_normalization_device on the bench's 2^18 scalars -- against
+    the oracle's Wnaf::base(g, 2^18).scalar(s_i) (wnaf.rs:93-107, 169-178)
+    followed by G1::batch_normalization (ec.rs:246-294): every output, bit
+    for bit (the normalized records are canonical)."""
+    import torch
+    import pairing_amd.device as pdev
+    n = 1 << 18
+    base_np, s_np = _config3_inputs(n)
+    base, scal = _dev(base_np), _dev(s_np)
+    out = pdev.empty_records(n, 18, "cuda:0")
+    table, ws = pdev.fixed_base_buffers("cuda:0")
+    pdev.g1_wnaf_fixed_base(base, scal, out, table, ws)
+    pdev.g1_batch_normalization(out)
+    torch.cuda.synchronize()
+    exp = oracle.g1_batch_normalization(oracle.g1_wnaf_fixed_base(base_np, s_np, _threads()))
+    np.testing.assert_array_equal(_host(out), exp)
+
+
+def test_fixed_base_wrapping_reprs_documented_divergence(gpu, oracle):
+    """the one documented divergence of pa_g1_wnaf_fixed_base (pairing_amd.h):
+    for raw 256-bit reprs within 2^w of 2^256 the reference's wnaf_form wraps in
+    add_nocarry (wnaf.rs:30-35) -- s = 2^256 - 1 becomes the digit string [-1],
+    i.e. -g -- while the GPU multiplies exactly, s g = (s mod r) g.  No
+    Fr::into_repr output is that large.  Pinned here on both sides."""
+    import torch
+    import pairing_amd.device as pdev
+    base_np, _ = _config3_inputs(1)
+    s = np.array([limbs((1 << 256) - 1, 4), limbs((1 << 256) - 2, 4), limbs(R_ORDER - 1, 4)], np.uint64)
+    out = pdev.empty_records(3, 18, "cuda:0")
+    table, ws = pdev.fixed_base_buffers("cuda:0")
+    pdev.g1_wnaf_fixed_base(_dev(base_np), _dev(s), out, table, ws)
+    torch.cuda.synchronize()
+    got = _host(out)
+    ref = oracle.g1_wnaf_fixed_base(base_np, s)
+    exact = oracle.g1_mul(np.repeat(base_np, 3, axis=0),
+                          np.array([limbs(((1 << 256) - 1) % R_ORDER, 4), limbs(((1 << 256) - 2) % R_ORDER, 4),
+                                    limbs(R_ORDER - 1, 4)], np.uint64))
+    assert oracle.g1_eq(got, exact).all()
+    neg_g = oracle.g1_mul(base_np, np.array([limbs(R_ORDER - 1, 4)], np.uint64))
+    assert oracle.g1_eq(ref[:1], neg_g).all()          # the reference's wrap: -g
+    assert not oracle.g1_eq(got[:1], ref[:1]).any()     # ... which the GPU does not reproduce
+    assert oracle.g1_eq(got[2:], ref[2:]).all()         # r - 1 is an ordinary repr: equal

@@ -146,3 +146,41 @@ def test_sharded_pairing_world2_hip(tmp_path, oracle, n):
     fe, ok = oracle.final_exponentiation(single.reshape(1, 72).copy())
     assert ok[0] == 1
     np.testing.assert_array_equal(prod[1], fe[0])
+
+
+def _shard_from_worker(rank, world, path, n, out_path):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(path[1]))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pairing_amd.shard import sharded_batch_from
+    seen = []
+
+    def load(a, b):        # each rank materializes only rows a..b
+        seen.append((a, b))
+        rows = np.arange(a, b, dtype=np.int64)[:, None] * np.ones((1, 3), np.int64)
+        return torch.from_numpy(rows), torch.from_numpy(rows + 1)
+    out = sharded_batch_from(load, n, lambda p, q: p + q)
+    if rank == 0:
+        np.save(out_path, out.numpy())
+    dist.destroy_process_group()
+    assert len(seen) == 1
+
+
+def test_sharded_batch_from_stages_only_the_shard(tmp_path):
+    """pairing_amd.shard.sharded_batch_from: every rank loads only its own
+    contiguous rows (ragged world-3 split) and the root gathers all n"""
+    import numpy as np
+    import socket
+    import torch.multiprocessing as mp
+    sck = socket.socket()
+    sck.bind(("127.0.0.1", 0))
+    port = sck.getsockname()[1]
+    sck.close()
+    n = 11
+    out_path = str(tmp_path / "out.npy")
+    mp.spawn(_shard_from_worker, args=(3, ("x", port), n, out_path), nprocs=3, join=True)
+    got = np.load(out_path)
+    want = (2 * np.arange(n) + 1)[:, None] * np.ones((1, 3), np.int64)
+    np.testing.assert_array_equal(got, want)

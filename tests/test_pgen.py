@@ -217,18 +217,28 @@ def test_dsl_split_final_exp_composes(ref_pair):
     assert [out[k] for k in range(12)] == fe
 
 
-def test_split_final_exp_saves_the_fermat_chain():
+def test_split_final_exp_saves_the_fermat_chain(monkeypatch):
+    """round 2's split form against round 2's one-kernel form (Fermat
+    inversion, Granger-Scott exp_by_x: PGEN_KARABINA=0), and round 3's
+    one-kernel form (in-kernel binary GCD, compressed squarings) below both"""
     import random
     g = random.Random(2)
     ins = {k: g.randrange(dsl.Q) for k in range(13)}
     macs = {}
     for split in (None, "norm", "inv"):
         st = dsl.Stats()
+        monkeypatch.setenv("PGEN_KARABINA", "0")
         dsl.evaluate(kernels.final_exp_prog(lazy="sq", split=split), dict(ins), st)
         macs[split] = build_gen.macs(st.counts)
+    monkeypatch.setenv("PGEN_KARABINA", "1")
+    st = dsl.Stats()
+    dsl.evaluate(kernels.final_exp_prog(lazy="sq"), dict(ins), st)
+    kara = build_gen.macs(st.counts)
     # the 463-product Fermat chain (~181 k limb MACs) leaves; the norm kernel is ~1 % of the FE
     assert macs[None] - macs["inv"] > 170000
     assert macs["norm"] < 0.01 * macs[None]
+    # compressed squarings: ~17 % fewer limb MACs than the split form
+    assert kara < 0.85 * macs["inv"]
 
 
 def test_sim_fe_norm_kernel():
@@ -238,3 +248,159 @@ def test_sim_fe_norm_kernel():
 @pytest.mark.slow
 def test_sim_fe_inv_kernel():
     assert sim_check.check("fei", debug=True)
+
+
+# ---- round 3: compressed squaring, in-kernel binary GCD, zero-test select ----
+def _cyclotomic(seed):
+    """a random element of the cyclotomic subgroup (the easy part of the final
+    exponentiation applied to a random Fq12), Python model"""
+    import pymodel as pm
+    g = random.Random(seed)
+    f = tuple(tuple((g.randrange(dsl.Q), g.randrange(dsl.Q)) for _ in range(3)) for _ in range(2))
+    t = pm.f12mul(pm.f12conj(f), pm.f12inv(f))
+    return pm.f12mul(pm.f12pow(t, dsl.Q * dsl.Q), t)
+
+
+def _b0_zero_element():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "karabina_b0zero.json")) as fh:
+        f = json.load(fh)["f"]
+    return tuple(tuple((x[0], x[1]) for x in c) for c in f)
+
+
+def _model_ksqr(g):
+    import pymodel as pm
+
+    def sc(k, a):
+        return ((k * a[0]) % dsl.Q, (k * a[1]) % dsl.Q)
+    a1, a2, b0, b2 = g
+    sq = lambda x: pm.f2mul(x, x)  # noqa: E731
+    return (pm.f2sub(sc(3, pm.f2add(sq(b0), pm.f2xi(sq(a2)))), sc(2, a1)),
+            pm.f2sub(sc(3, pm.f2add(sq(a1), pm.f2xi(sq(b2)))), sc(2, a2)),
+            pm.f2add(sc(6, pm.f2xi(pm.f2mul(a1, b2))), sc(2, b0)),
+            pm.f2add(sc(6, pm.f2mul(b0, a2)), sc(2, b2)))
+
+
+def test_karabina_formulas_on_the_model():
+    """tower.Tower.ksqr's formulas square the compressed coordinates of
+    cyclotomic elements (against full squaring in the Python model), and the
+    element with b0 = 0 (tests/golden/karabina_b0zero.json) is really in the
+    cyclotomic subgroup and satisfies the b0 = 0 decompression identity
+    b1 a2 = 2 a1 b2 that kdec_numden's select relies on"""
+    import pymodel as pm
+    for f in (_cyclotomic(1), _cyclotomic(2), _b0_zero_element()):
+        assert pm.f12mul(f, pm.f12conj(f)) == pm.F12ONE
+        g = (f[0][1], f[0][2], f[1][0], f[1][2])
+        for _ in range(3):
+            f = pm.f12mul(f, f)
+            g = _model_ksqr(g)
+            assert g == (f[0][1], f[0][2], f[1][0], f[1][2])
+    z = _b0_zero_element()
+    (a0, a1, a2), (b0, b1, b2) = z
+    assert b0 == (0, 0) and a2 != (0, 0)
+    assert pm.f2mul(b1, a2) == pm.f2add(pm.f2mul(a1, b2), pm.f2mul(a1, b2))
+
+
+def _dec_prog():
+    import unit_progs
+    return unit_progs.dec_prog()
+
+
+def _abi_words(f):
+    """plain Fq12 -> the 12 canonical Montgomery (R = 2^384) integers, ABI order"""
+    R384 = (1 << 384) % dsl.Q
+    return [(x * R384) % dsl.Q for c6 in f for c2 in c6 for x in c2]
+
+
+@pytest.mark.parametrize("which", ["random", "b0_zero", "identity"])
+def test_dsl_karabina_decompression(which):
+    """the DSL decompression (both branches of the b0 == 0 select, and the
+    identity whose inversion input is 0) rebuilds the element exactly"""
+    import pymodel as pm
+    f = {"random": lambda: _cyclotomic(3), "b0_zero": _b0_zero_element, "identity": lambda: pm.F12ONE}[which]()
+    ins = _abi_words(f)
+    out = dsl.evaluate(_dec_prog(), {k: ins[k] for k in range(12)})
+    assert [out[k] for k in range(12)] == ins
+
+
+def test_binv_model_is_the_inverse():
+    """dsl.binv_limbs (the emitted binary GCD's exact limbs) is a^-1 R' for
+    aR' = x, 0 for x = 0 mod q, over random lazy inputs and edge values"""
+    g = random.Random(4)
+    R = dsl.R
+    vals = [0, dsl.Q, 1, dsl.Q - 1, dsl.Q + 1, 2 * dsl.Q - 1, R % dsl.Q, (1 << 380)] + \
+        [g.randrange(2 * dsl.Q) for _ in range(200)]
+    for v in vals:
+        out = dsl.val_of(dsl.binv_limbs(tuple(dsl.gen_fl.limbs(v))))
+        assert out < 2 * dsl.Q
+        a = v * pow(R, -1, dsl.Q) % dsl.Q
+        assert out % dsl.Q == (pow(a, -1, dsl.Q) * R % dsl.Q if a else 0)
+
+
+def _unit_prog():
+    import unit_progs
+    return unit_progs.unit_prog()
+
+
+def _sim_run(prog, ins, lane=3):
+    import kcfg
+    import sim
+    cfg = kcfg.FinalExpCfg()
+    cfg.name = prog.name
+    code, _ = kcfg.build(prog, cfg, debug=True)
+    trace = []
+    want = dsl.evaluate(prog, {k: ins[k] for k in range(12)}, trace=trace)
+    IN, OUT, AUX, WS = 0x100000, 0x200000, 0x300000, 0x400000
+    sm = sim.run_lane(code, [IN, OUT, AUX, lane + 1, WS], {IN: [0] * (72 * lane) + sim_check.words(ins)},
+                      lane=lane, trace=trace)
+    got = [sum(sm.mem.get(OUT + 576 * lane + 48 * k + 4 * j, 0) << (32 * j) for j in range(12)) for k in range(12)]
+    return got, [want[k] for k in range(12)]
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_sim_binv_and_selz(case):
+    """the emitted binary GCD and zero-test select, run by the simulator (with
+    its gfx950 VALU-SGPR wait-state check), equal the DSL model limb for limb:
+    random inputs, zero tests true for (0, 0), inverses of 0 and of q"""
+    g = random.Random(7 + case)
+    ins = [g.randrange(dsl.Q) for _ in range(12)]
+    if case == 1:
+        ins[4] = ins[5] = ins[6] = 0
+    if case == 2:
+        ins[0] = 0
+        ins[4] = 0
+    if case == 3:
+        ins[2] = dsl.Q - ins[3]
+        ins[6] = 0
+    got, want = _sim_run(_unit_prog(), ins)
+    assert got == want
+    assert got[4] == ((1 << 384) % dsl.Q if ins[0] and ins[1] else 0)
+
+
+def test_sim_karabina_decompression_b0_zero():
+    """the emitted decompression on the b0 = 0 element (the select's rare
+    branch) equals the DSL model and the element itself"""
+    ins = _abi_words(_b0_zero_element())
+    got, want = _sim_run(_dec_prog(), ins)
+    assert got == want == ins
+
+
+def test_local_homes_free_dead_variables():
+    """emit.Emitter.index_vars: a variable written first inside a loop body and
+    used only there gets its home only in that body (round 3's looped hard
+    part relies on it to reuse AGPR homes between its phases)"""
+    import emit
+    import kcfg
+    p = dsl.Prog("t", use_norm=True)
+    x = p.load(0)
+    p.var("outer", 1, "A")
+    p.set("outer", x)
+    with p.loop(3):
+        p.var("inner", 1, "A")
+        p.set("inner", p.mul(p.get("outer"), p.get("outer")))
+        p.set("outer", p.get("inner"))
+    p.store(0, p.get("outer"))
+    em = emit.Emitter(p, kcfg.FinalExpCfg())
+    em.run_block(p.root, top=True)
+    loop_body = [it for it in p.root.items if isinstance(it, dsl.Loop)][0].body
+    assert em.local_vars.get(id(loop_body)) == {"inner"}

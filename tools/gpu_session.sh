@@ -23,8 +23,10 @@ run() {  # name limit cmd...
 for step in "$@"; do
     case $step in
         valu) run valu 120 ./tools/valu_rates ;;
+        valupeak) run valu_peak 120 ./tools/valu_peak ;;
         tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
         alltests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
+        unittests) run pytest_units 300 python -u -m pytest tests/test_gen_units.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         sizetests) run pytest_sizes 600 python -u -m pytest tests/test_bench_sizes.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;

@@ -92,6 +92,9 @@ PROGRAMS = {
     "fen": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="norm"), kcfg.FinalExpCfg, "pa_gen_fe_norm"),
     "fei": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="inv"), kcfg.FinalExpCfg, "pa_gen_fe_inv"),
     "ml2": _mk(lambda: kernels.miller_loop_prog(lanes=2), kcfg.MillerLoopCfg2, "pa_gen_miller_loop2"),
+    # test-only kernels (tools/pgen/unit_progs.py, tests/test_gen_units.py)
+    "tdec": _mk(lambda: __import__("unit_progs").dec_prog(), kcfg.FinalExpCfg, "pa_gen_tdec"),
+    "tunit": _mk(lambda: __import__("unit_progs").unit_prog(), kcfg.FinalExpCfg, "pa_gen_tunit"),
     "fe2": _mk(lambda: kernels.final_exp_prog(lanes=2), kcfg.FinalExpCfg2, "pa_gen_final_exp2"),
     # lazy reduction (tower.TowerLazy): wide products, one reduction per output Fq
     # (measured slower; built only on request for A/B runs)
@@ -101,7 +104,8 @@ PROGRAMS = {
 FILES = {"small": "pa_gen_small.hsaco", "cyc": "pa_gen_cyc.hsaco", "ml": "pa_gen_miller_loop.hsaco", "fe": "pa_gen_final_exp.hsaco",
          "fen": "pa_gen_fe_norm.hsaco", "fei": "pa_gen_fe_inv.hsaco",
          "ml2": "pa_gen_miller_loop2.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
-         "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco"}
+         "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco",
+         "tdec": "test/pa_gen_tdec.hsaco", "tunit": "test/pa_gen_tunit.hsaco"}
 
 
 def build(which, outdir):
@@ -113,6 +117,7 @@ def build(which, outdir):
     asm = render.kernel_asm(kname, code, em.lds_bytes, lanes=prog.lanes,
                             nvgpr=256 if prog.lanes == 1 else min(256, -(-(emit.VSLOT0 + 14 * em.NV) // 4) * 4))
     out = os.path.join(outdir, FILES[which])
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     render.assemble(asm, out, os.path.join(ROOT, "build", "pgen"))
     nv = sum(1 for t in code if t[0].startswith("v_"))
     print("%s: %d instructions (%d VALU), %d M slots, %.1fs  %s" % (

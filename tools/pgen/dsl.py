@@ -172,6 +172,14 @@ class Prog:
         assert a.vb * b.vb + c.vb * d.vb <= VB_PROD, "sop value bound"
         return self._op("sop", [a, b, c, d], 1)
 
+    def sopn(self, args):
+        """sum a_i b_i over the pairs (a0, b0, a1, b1, ...): one product leaf"""
+        self._full(*args)
+        assert len(args) % 2 == 0 and args
+        assert sum(a.u * b.u for a, b in zip(args[0::2], args[1::2])) <= COL_BOUND, "sopn bound"
+        assert sum(a.vb * b.vb for a, b in zip(args[0::2], args[1::2])) <= VB_PROD, "sopn value bound"
+        return self._op("sop", list(args), 1)
+
     def sqr(self, a):
         self._full(a)
         assert a.u <= 3, "sqr bound %d" % a.u

@@ -897,21 +897,26 @@ class Emitter:
         self.local_ids = self.block_vals(block)
         saved_items = self.items
         self.items = block.items
-        vr = self.var_ranges(block) if top else {}
+        if top:
+            self.index_vars(block)
+            vr = self.var_ranges(block)
+        else:
+            # variables that live only inside this block, written before any
+            # read in each pass: their homes exist only over their range here
+            loc = self.local_vars.get(id(block), ())
+            vr = {n: r for n, r in self.var_ranges(block).items() if n in loc}
         for pos, it in enumerate(block.items):
-            if top:
-                for name, (f, _) in vr.items():
-                    if f == pos and name not in self.home:
-                        self.alloc_home(name, pos)
+            for name, (f, _) in vr.items():
+                if f == pos and name not in self.home:
+                    self.alloc_home(name, pos)
             if isinstance(it, (Loop, If)):
                 self.park(block, pos)
                 self.run_construct(it)
             else:
                 self.run_op(it, pos)
-            if top:
-                for name, (_, l) in vr.items():
-                    if l == pos and name in self.home:
-                        self.free_home(name, pos)
+            for name, (_, l) in vr.items():
+                if l == pos and name in self.home:
+                    self.free_home(name, pos)
         # everything defined here is dead now
         self.wait_pending()
         self.items = saved_items
@@ -920,6 +925,81 @@ class Emitter:
             if vs is not None and vs.val.id in self.local_ids:
                 self.kill(vs)
         self.local_ids = saved_ids
+
+    def index_vars(self, root):
+        """self.local_vars: block id -> the variables whose every access lies in
+        that block's subtree and whose first access there is a setvar directly
+        in the block (so no value crosses a back edge of an enclosing loop);
+        the innermost such block gets the variable (PGEN_LOCAL_HOMES=0: every
+        home lives at the top level, round 2)"""
+        self.local_vars = {}
+        if os.environ.get("PGEN_LOCAL_HOMES", "1") != "1":
+            return
+        parent, where, first = {}, {}, {}
+
+        def walk(block, par):
+            parent[id(block)] = par
+            for it in block.items:
+                if isinstance(it, (Loop, If)):
+                    walk(it.body, id(block))
+                elif it.kind in ("getvar", "setvar"):
+                    where.setdefault(it.imm, set()).add(id(block))
+                    first.setdefault((id(block), it.imm), it.kind)
+        walk(root, None)
+
+        def ancestors(b):
+            out = []
+            while b is not None:
+                out.append(b)
+                b = parent[b]
+            return out
+
+        for name, blocks in where.items():
+            common = None
+            for b in blocks:
+                a = ancestors(b)
+                common = a if common is None else [x for x in common if x in a]
+            # innermost common ancestor whose own first access is a setvar and
+            # that holds the first access of the subtree
+            for b in common:
+                if b == id(root):
+                    break
+                if first.get((b, name)) == "setvar" and self._first_access_here(b, name):
+                    self.local_vars.setdefault(b, set()).add(name)
+                    break
+
+    def _first_access_here(self, bid, name):
+        """the first access of `name` in block bid's subtree (program order) is
+        one of bid's own items"""
+        blk = self._block_by_id(bid)
+        for it in blk.items:
+            if isinstance(it, (Loop, If)):
+                if self._touches(it.body, name):
+                    return False
+            elif it.kind in ("getvar", "setvar") and it.imm == name:
+                return it.kind == "setvar"
+        return False
+
+    def _touches(self, block, name):
+        for it in block.items:
+            if isinstance(it, (Loop, If)):
+                if self._touches(it.body, name):
+                    return True
+            elif it.kind in ("getvar", "setvar") and it.imm == name:
+                return True
+        return False
+
+    def _block_by_id(self, bid):
+        if not hasattr(self, "_blocks"):
+            self._blocks = {}
+
+            def walk(b):
+                self._blocks[id(b)] = b
+                for it in b.items:
+                    if isinstance(it, (Loop, If)):
+                        walk(it.body)
+            walk(self.prog.root)
+        return self._blocks[bid]
 
     def block_vals(self, block):
         ids = {it.dst.id for it in block.items if isinstance(it, Op) and it.dst is not None}

@@ -249,10 +249,9 @@ def exp_by_x_karabina(p, T, V, xv, L, first_skip, tag="k"):
                 p.set(n, v)
             saved.append(sn)
     saved.append(kn)
-    gs = [getg(sn) for sn in saved]
-    nds = [T.kdec_numden(g) for g in gs]
-    idens = T.batch_inv2([d for _, d in nds], tag)
-    F = [T.kdec_finish(g, nd[0], iv) for g, nd, iv in zip(gs, nds, idens)]
+    nds = [T.kdec_numden(getg(sn)) for sn in saved]
+    idens = T.batch_inv2([nd[1] for nd in nds], tag)
+    F = [T.kdec_finish(getg(sn), nd[0], iv, nd[2]) for sn, nd, iv in zip(saved, nds, idens)]
     # top: the GS state reuses the 8 compressed-state homes (dead by now) plus
     # four more; res: 6 + 6 coordinates in AGPRs + the workspace
     V.declare12(res, os.environ.get("PGEN_KR_HOME", "AAAAAAMMMMMM"))

@@ -233,7 +233,9 @@ class Tower:
         """the division that recovers b1 = num / den:  b0 != 0: (3 a1^2 - 2 a2 +
         xi b2^2) / (4 b0);  b0 == 0: 2 a1 b2 / a2 (lane-wise select).  Only the
         identity has b0 = a2 = 0 (then num = den = 0, and the shared inversion's
-        0 -> 0 gives b1 = 0, a0 = 1: the identity)."""
+        0 -> 0 gives b1 = 0, a0 = 1: the identity).  Also returns
+        w = 3 a1 a2 - b0 b2 (a0 = xi (2 b1^2 - w) + 1), formed now so that the
+        finish does not read g again."""
         t, p = self, self.p
         a1, a2, b0, b2 = g
         s1 = t.sqr2(a1)
@@ -244,15 +246,21 @@ class Tower:
         z = [p.red_full(b0[0]), p.red_full(b0[1])]
         num = (p.selz(z, num2[0], num1[0]), p.selz(z, num2[1], num1[1]))
         den = (p.selz(z, den2[0], den1[0]), p.selz(z, den2[1], den1[1]))
-        return num, den
+        # w = 3 a1 a2 - b0 b2 as two 4-term products:
+        #   re = 3 a1r a2r + 3 (-a1i) a2i + (-b0r) b2r + b0i b2i
+        #   im = 3 a1r a2i + 3 a1i a2r + (-b0r) b2i + (-b0i) b2r
+        a13 = (t.lim2(t.add2(t.dbl2(a1), a1)))
+        nb0 = (p.neg(b0[0]), p.neg(b0[1]))
+        w = (p.sopn([a13[0], a2[0], p.neg(a13[1]), a2[1], nb0[0], b2[0], b0[1], b2[1]]),
+             p.sopn([a13[0], a2[1], a13[1], a2[0], nb0[0], b2[1], nb0[1], b2[0]]))
+        return num, den, w
 
-    def kdec_finish(self, g, num, iden):
-        """b1 = num iden, a0 = xi (2 b1^2 + b0 b2 - 3 a1 a2) + 1"""
+    def kdec_finish(self, g, num, iden, w):
+        """b1 = num iden, a0 = xi (2 b1^2 - w) + 1"""
         t = self
         a1, a2, b0, b2 = g
         b1 = t.mul2(num, iden)
-        m = t.mul2(a1, a2)
-        s = t.red2(t.sub2(t.add2(t.dbl2(t.sqr2(b1)), t.mul2(b0, b2)), t.add2(t.dbl2(m), m)))
+        s = t.red2(t.sub2(t.dbl2(t.sqr2(b1)), w))
         a0 = t.red2(t.add2(t.xi(s), t.one2()))
         return ((a0, a1, a2), (b0, b1, b2))
 
@@ -559,6 +567,29 @@ class TowerLazy(Tower):
         t2 = t.w_sqr2(t.lim1(t.add2(a, b)))
         r1 = t.w_red2(t.w_sub2(t2, t.w_add2(t0, t1)))
         return t.lim1(r0), t.lim1(r1)
+
+    def ksqr(self, g):
+        """Tower.ksqr with each half's x^2 + xi y^2 and 2 x y formed from wide
+        squares, one reduction per output Fq (PGEN_KSQR_LAZY=0: Tower.ksqr)"""
+        if os.environ.get("PGEN_KSQR_LAZY", "1") != "1":
+            return Tower.ksqr(self, g)
+        t = self
+        a1, a2, b0, b2 = g
+
+        def half(x, y, z, zy, xi_on_cross):
+            sx, sy = t.w_sqr2(x), t.w_sqr2(y)
+            s = t.lim1(t.w_red2(t.w_add2(sx, t.w_xi(sy))))
+            sxy = t.w_sqr2(t.lim1(t.add2(x, y)))
+            c = t.lim1(t.w_red2(t.w_sub2(sxy, t.w_add2(sx, sy))))
+            if xi_on_cross:
+                c = t.red2(t.xi(c))
+            nz = t.red2(t.add2(t.dbl2(t.sub2(s, z)), s))
+            nzy = t.red2(t.add2(t.dbl2(t.add2(c, zy)), c))
+            return nz, nzy
+
+        na2, nb0 = half(a1, b2, a2, b0, True)
+        na1, nb2 = half(b0, a2, a1, b2, False)
+        return (na1, na2, nb0, nb2)
 
 
 class TowerLazySq(TowerLazy):
