@@ -225,13 +225,20 @@ def final_exponentiation(f):
     return out, ok.astype(bool)
 
 
-def pairing(p, q):
-    """Engine::pairing (lib.rs:101-109) for n independent (G1Affine, G2Affine) pairs."""
+def pairing(p, q, out=None):
+    """Engine::pairing (lib.rs:101-109) for n independent (G1Affine, G2Affine) pairs.
+    `out`: an optional (n, 72) uint64 C-contiguous array to write into -- a caller
+    that reuses it saves the first-touch page faults of a fresh 37.7 MB result
+    per 2^16 pairs (tools/pcie_rate.py measures both)."""
     p = as_rows(p, W_G1A, "p")
     q = as_rows(q, W_G2A, "q")
     if p.shape[0] != q.shape[0]:
         raise ValueError("p and q lengths differ")
-    out = np.empty((p.shape[0], W_FQ12), np.uint64)
+    if out is None:
+        out = np.empty((p.shape[0], W_FQ12), np.uint64)
+    elif (not isinstance(out, np.ndarray) or out.dtype != np.uint64 or out.shape != (p.shape[0], W_FQ12)
+          or not out.flags.c_contiguous or not out.flags.writeable):
+        raise ValueError("out must be a writeable C-contiguous (%d, %d) uint64 array" % (p.shape[0], W_FQ12))
     call("pa_pairing_batch", ptr(p), ptr(q), ptr(out), p.shape[0])
     return out
 

@@ -519,12 +519,14 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
             fprintf(stderr, "[pipeline] chunk %zu %-10s %8.3f ms\n", ci, what,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     };
-    // Within a chunk the staging copies and the DMA may run in kPieces pieces
-    // (PA_PIPELINE_PIECES, 1..4), so the host copy of piece j overlaps the DMA
-    // of piece j - 1 (in) / j + 1 (out).
+    // Within a chunk the staging copies and the DMA run in kPieces pieces
+    // (PA_PIPELINE_PIECES, 1..4, default 2), so the host copy of piece j
+    // overlaps the DMA of piece j - 1 (in) / j + 1 (out): one caller at 2^16,
+    // reused result buffer, 19.19 ms with 1 piece, 18.89 with 2, 18.84 with 4
+    // (profiles/r03_host_boundary.txt).
     static const size_t kPieces = [] {
         const char* e = getenv("PA_PIPELINE_PIECES");
-        const long v = e ? strtol(e, nullptr, 10) : 1;
+        const long v = e ? strtol(e, nullptr, 10) : 2;
         return (size_t)(v < 1 ? 1 : (v > 4 ? 4 : v));
     }();
     hipEvent_t* h2d = c->ev;        // [k]: chunk's inputs copied (pinned in[k] free again)

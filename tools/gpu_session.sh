@@ -24,6 +24,11 @@ for step in "$@"; do
     case $step in
         valu) run valu 120 ./tools/valu_rates ;;
         valupeak) run valu_peak 120 ./tools/valu_peak ;;
+        issue) run issue_probe 120 ./tools/issue_probe ;;
+        hostrate) run host_rate1 300 python tools/pcie_rate.py &&
+                  run host_rate2 300 env PA_PIPELINE_PIECES=2 python tools/pcie_rate.py &&
+                  run host_rate4 300 env PA_PIPELINE_PIECES=4 python tools/pcie_rate.py &&
+                  run host_trace 300 env PA_PIPELINE_TRACE=1 python tools/pcie_rate.py ;;
         tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
         alltests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
         unittests) run pytest_units 300 python -u -m pytest tests/test_gen_units.py -m gpu -x -v --timeout 120 --timeout-method thread ;;

@@ -32,11 +32,19 @@ n = 1 << 16
 p, q = bench.make_pairs(2 * n, 0)
 out = np.empty((2 * n, 72), np.uint64)
 pairing_amd.pairing(p[:1024], q[:1024])  # warm-up (code objects, contexts)
+pieces = os.environ.get("PA_PIPELINE_PIECES", "1")
 for m in (n, 2 * n):
     pairing_amd.pairing(p[:m], q[:m])
     t = median_time(lambda: pairing_amd.pairing(p[:m], q[:m]))
-    print("one caller, n=%d: median %.2f ms -> %.0f pairings/s (bytes in %d, out %d)"
-          % (m, t * 1e3, m / t, p[:m].nbytes + q[:m].nbytes, m * 576), flush=True)
+    print("one caller, n=%d, fresh result array: median %.2f ms -> %.0f pairings/s (bytes in %d, out %d; pieces %s)"
+          % (m, t * 1e3, m / t, p[:m].nbytes + q[:m].nbytes, m * 576, pieces), flush=True)
+    o = out[:m]
+    pairing_amd.pairing(p[:m], q[:m], out=o)
+    t = median_time(lambda: pairing_amd.pairing(p[:m], q[:m], out=o))
+    print("one caller, n=%d, reused result array: median %.2f ms -> %.0f pairings/s (pieces %s)"
+          % (m, t * 1e3, m / t, pieces), flush=True)
+    if os.environ.get("PA_PIPELINE_TRACE") == "1":
+        break
 
 
 def worker(k, reps):

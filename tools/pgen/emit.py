@@ -637,8 +637,10 @@ class Emitter:
             self.i("s_mov_b64", VCC, S(32))
         else:
             self.i("s_and_b64", VCC, S(32), S(38))
+        # the e64 form: back-to-back VOP2 v_cndmask_b32 (implicit VCC) issue at
+        # 19 clk on a lone wave, the e64 form at 6 (profiles/r03_issue_probe.txt)
         for i in range(NL):
-            self.i("v_cndmask_b32", d + i, b + i, a + i)
+            self.i("v_cndmask_b32_e64", d + i, b + i, a + i, VCC)
 
     # ---- in-kernel binary GCD inversion (dsl.Prog.binv, dsl.binv_limbs) ----
     def emit_binv(self, x, d, scratch):
@@ -733,14 +735,14 @@ class Emitter:
             self.i("v_cmp_lt_u64_e64", S(38), 10, 12)          # lt
             self.i("v_cmp_ne_u32_e64", S(34), K(0), 0)          # odd
             self.i("s_and_b64", VCC, S(34), S(38))              # swap = odd & lt
-            self.i("v_cndmask_b32", 0, 10, 12)                  # XA = swap ? xb : xa
-            self.i("v_cndmask_b32", 1, 11, 13)
-            self.i("v_cndmask_b32", 12, 12, 10)                 # xb' = swap ? xa : xb
-            self.i("v_cndmask_b32", 13, 13, 11)
-            self.i("v_cndmask_b32", 4, 6, 8)                    # FA = swap ? f1 : f0
-            self.i("v_cndmask_b32", 8, 8, 6)                    # FB
-            self.i("v_cndmask_b32", 5, 7, 9)                    # GA
-            self.i("v_cndmask_b32", 9, 9, 7)                    # GB
+            self.i("v_cndmask_b32_e64", 0, 10, 12, VCC)  # XA = swap ? xb : xa
+            self.i("v_cndmask_b32_e64", 1, 11, 13, VCC)
+            self.i("v_cndmask_b32_e64", 12, 12, 10, VCC)  # xb' = swap ? xa : xb
+            self.i("v_cndmask_b32_e64", 13, 13, 11, VCC)
+            self.i("v_cndmask_b32_e64", 4, 6, 8, VCC)  # FA = swap ? f1 : f0
+            self.i("v_cndmask_b32_e64", 8, 8, 6, VCC)  # FB
+            self.i("v_cndmask_b32_e64", 5, 7, 9, VCC)  # GA
+            self.i("v_cndmask_b32_e64", 9, 9, 7, VCC)  # GB
             self.i("v_sub_co_u32", 2, 0, 12)                    # XA - XB (borrow in VCC)
             self.i("v_sub_u32", 14, 4, 8)
             self.i("v_sub_u32", 15, 5, 9)
@@ -1199,7 +1201,7 @@ class Emitter:
             "selz": 80, "binv": 33000}
     # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
     AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}
-    WINDOW = 2500
+    WINDOW = int(os.environ.get("PGEN_WINDOW", 2500))
 
     def op_cost(self, op):
         if op.kind == "sop":
