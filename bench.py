@@ -707,6 +707,23 @@ def main():
                     "avg_launch_ms": round(dom_ms, 4),
                     "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS,
                             "bytes_per_unit": dom_bytes}}
+        valu_path = os.path.join(ROOT, "profiles", "pmc_valu.json")
+        if args.workload == "decode" and os.path.exists(valu_path):
+            # VALU-issue bound (square roots = Fq exponentiations, the r*P check =
+            # 63/126 doublings): one record per lane, so the wave's VALU
+            # instruction count (SQ_INSTS_VALU / SQ_WAVES, profiles/pmc_valu.json,
+            # a fixed function of the seeded batch) is the lane-instructions per
+            # record; timed live here
+            with open(valu_path) as f:
+                ipr = json.load(f).get(dom_name, {}).get("valu_instructions_per_wave")
+            if ipr:
+                rate = ipr * n / (dom_ms * 1e-3) / 1e12
+                roof = {"kernel": dom_name, "bound": "valu_issue", "achieved": round(rate, 3),
+                        "peak": round(ISSUE_PEAK_T, 3), "unit": "T lane-instructions/s (VALU, 1 per 4 clk per SIMD)",
+                        "frac": rate / ISSUE_PEAK_T, "traffic": traffic, "instructions_per_unit": ipr,
+                        "avg_launch_ms": round(dom_ms, 4),
+                        "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS,
+                                "bytes_per_unit": dom_bytes}}
         if args.workload == "msm":
             # VALU view: every term enters W = 17 windows; each entry is one mixed
             # addition into a bucket (madd-2007-bl on the lazy core: 7 products + 4

@@ -16,8 +16,11 @@
 //   1. k_msm_digits: signed c-bit digits per window (|d| <= 2^(c-1)); item
 //      (window, |d|) -> sort key, (i | sign<<31) -> value.   c*W >= 257 so any
 //      256-bit FrRepr (also >= r, as the reference's BitIterator allows) fits.
-//   2. hipcub radix sort of the W*n (key, value) pairs: each bucket's points
-//      become contiguous (stable, so the result is deterministic).
+//   2. a stable LSD counting sort of the items by bucket, 8 bits per pass
+//      (k_sort_hist / k_sort_scan / k_sort_scatter, ceil((c-1)/8) passes):
+//      each bucket's points become contiguous in term order, windows stay
+//      apart, zero digits are dropped.  Same order as a stable sort of the
+//      (w*B + |d|-1) keys, so the result is deterministic.
 //   3. k_msm_bucket_bounds: [start, end) per bucket from the sorted keys.
 //   4. k_msm_chunk_acc: one lane per 32 sorted items, mixed additions
 //      (madd-2007-bl) of the affine bases gathered from HBM (y negated for
@@ -28,10 +31,11 @@
 //   6. k_msm_group_sum (repeated): segment results -> one sum per window.
 //   7. k_msm_horner: one wave, sum_w 2^(c*w) S_w (doublings over three lanes).
 // Work: n*W mixed additions + ~2*W*2^(c-1) additions + ~256 doublings.
-#include <hipcub/hipcub.hpp>
 
 #include "curve_fl.h"
 #include "launch_msm.h"
+
+#include <utility>
 
 namespace pa {
 
@@ -95,11 +99,12 @@ __global__ void __launch_bounds__(64) k_proj_mul(const uint64_t* __restrict__ p,
 // ---------------- MSM ----------------
 struct MsmPlan {
     uint32_t c, W, B, L;        // window bits, windows, buckets per window, segment length
-    uint32_t key_bits;          // radix-sort key width
+    uint32_t passes;            // counting-sort passes over the c-1 magnitude bits
+    uint32_t tpw;               // sort tiles per window
     size_t items;               // W * n
     size_t off_keys_in, off_keys_out, off_vals_in, off_vals_out, off_start, off_end;
-    size_t off_buckets, off_segs, off_tmp, off_sort, off_cont, off_basefl;
-    size_t sort_bytes, total;
+    size_t off_buckets, off_segs, off_tmp, off_hist, off_wtot, off_cont, off_basefl;
+    size_t total;
 };
 
 static inline uint32_t msm_window_bits(size_t n) {
@@ -118,6 +123,9 @@ static inline uint32_t msm_window_bits(size_t n) {
 
 // items (sorted (bucket, term) pairs) per lane of the bucket accumulation
 constexpr uint32_t kMsmChunk = 32;
+// counting sort: a tile is 16 rounds of one item per thread of a 256-thread block
+constexpr uint32_t kSortIpt = 16;
+constexpr uint32_t kSortTile = 256 * kSortIpt;
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -132,9 +140,8 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     }();
     p.L = p.B < seg ? p.B : seg;  // short segments: the running sums are a latency chain per lane
     p.items = (size_t)p.W * n;
-    const uint64_t sentinel = (uint64_t)p.W * p.B;
-    p.key_bits = 1;
-    while (((uint64_t)1 << p.key_bits) <= sentinel) p.key_bits++;
+    p.passes = (p.c - 1 + 7) / 8;
+    p.tpw = (uint32_t)((n + kSortTile - 1) / kSortTile);
     const size_t jw = 8 * (size_t)(group == 1 ? Grp<1>::JW : Grp<2>::JW);
     const size_t nb = (size_t)p.W * p.B;
     const size_t nseg = (size_t)p.W * (p.B / p.L);
@@ -150,12 +157,8 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.off_tmp = off; off = align256(off + jw * nseg);
     p.off_cont = off; off = align256(off + jw * ((p.items + kMsmChunk - 1) / kMsmChunk));
     p.off_basefl = off; off = align256(off + (group == 1 ? 4 * 28 * n : 0));
-    p.sort_bytes = 0;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, p.sort_bytes, (const uint32_t*)nullptr,
-                                                      (uint32_t*)nullptr, (const uint32_t*)nullptr,
-                                                      (uint32_t*)nullptr, (int)p.items, 0, (int)p.key_bits);
-    if (e != hipSuccess) return e;
-    p.off_sort = off; off = align256(off + p.sort_bytes);
+    p.off_hist = off; off = align256(off + 4 * (size_t)p.W * 256 * p.tpw);
+    p.off_wtot = off; off = align256(off + 4 * (size_t)p.W);
     p.total = off;
     return hipSuccess;
 }
@@ -210,6 +213,206 @@ __global__ void __launch_bounds__(256) k_msm_bucket_bounds(const uint32_t* __res
     if (k >= sentinel) return;
     if (j == 0 || keys[j - 1] != k) start[k] = (uint32_t)j;
     if (j + 1 == items || keys[j + 1] != k) end[k] = (uint32_t)(j + 1);
+}
+
+// ---- the bucketing sort (step 2) ----
+// Items are (key, value) = (w*B + |d|-1, term | sign<<31).  Pass k orders the
+// items of each window by the 8-bit digit ((key & (B-1)) >> 8k), stably; the
+// first pass reads the window-major digit output (window w at [w*n, w*n + n),
+// zero digits carry key >= sentinel and are skipped), every pass writes the
+// windows compacted (window w at [wbase(w), wbase(w) + wtot[w])).  A window's
+// source range is cut in tiles of kSortTile items; hist[w][digit][tile] holds
+// the tile's digit counts, and after k_sort_scan the exclusive prefix over
+// (digit, tile) in that order -- where the tile's run of each digit starts.
+
+// window w's first item in the compacted layout
+PA_DEV uint32_t sort_wbase(const uint32_t* __restrict__ wtot, uint32_t w) {
+    uint32_t b = 0;
+    for (uint32_t k = 0; k < w; k++) b += wtot[k];
+    return b;
+}
+
+struct SortPass {
+    uint32_t shift, bmask, sentinel, tpw, first;
+    size_t n;
+};
+
+// window w's source range [base, base + count); tile t is its items
+// [t kSortTile, (t + 1) kSortTile) clipped to count
+PA_DEV void sort_window(const SortPass& sp, const uint32_t* __restrict__ wtot, uint32_t w, size_t& base,
+                        uint32_t& count) {
+    if (sp.first) {
+        base = (size_t)w * sp.n;
+        count = (uint32_t)sp.n;
+    } else {
+        base = sort_wbase(wtot, w);
+        count = wtot[w];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sort_hist(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ wtot,
+                                                   SortPass sp, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    const uint32_t tid = threadIdx.x, w = blockIdx.x / sp.tpw, t = blockIdx.x % sp.tpw;
+    h[tid] = 0;
+    __syncthreads();
+    size_t base;
+    uint32_t count;
+    sort_window(sp, wtot, w, base, count);
+    const uint32_t lo = t * kSortTile;
+    uint32_t key[kSortIpt];  // the whole tile's loads in flight at once
+#pragma unroll
+    for (uint32_t r = 0; r < kSortIpt; r++) {
+        const uint32_t k = lo + r * 256 + tid;
+        key[r] = k < count ? keys[base + k] : 0xffffffffu;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kSortIpt; r++)
+        if (key[r] < sp.sentinel) atomicAdd(&h[((key[r] & sp.bmask) >> sp.shift) & 0xff], 1u);
+    __syncthreads();
+    hist[((size_t)w * 256 + tid) * sp.tpw + t] = h[tid];
+}
+
+// exclusive prefix over one window's 256 x tpw counts (digit-major), in place;
+// the window's item count into wtot[w].  One 1024-thread block per window,
+// segments of 1024 x 64 counters: each thread's 64 as 16 uint4 loads in
+// flight, a block scan of the 1024 thread sums, then the prefixed writes.
+__global__ void __launch_bounds__(1024) k_sort_scan(uint32_t* __restrict__ hist, uint32_t tpw,
+                                                    uint32_t* __restrict__ wtot) {
+    __shared__ uint32_t s[2][1024];
+    const uint32_t tid = threadIdx.x;
+    uint32_t* a = hist + (size_t)blockIdx.x * 256 * tpw;
+    const uint32_t len = 256 * tpw;  // a multiple of 4
+    uint32_t carry = 0;
+    for (uint32_t seg = 0; seg < len; seg += 1024 * 64) {
+        const uint32_t b0 = seg + tid * 64;
+        uint4 v[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+            v[q] = b0 + 4 * q < len ? *reinterpret_cast<const uint4*>(a + b0 + 4 * q) : make_uint4(0, 0, 0, 0);
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) sum += v[q].x + v[q].y + v[q].z + v[q].w;
+        s[0][tid] = sum;
+        __syncthreads();
+        int cur = 0;
+        for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
+            s[cur ^ 1][tid] = s[cur][tid] + (tid >= d ? s[cur][tid - d] : 0u);
+            cur ^= 1;
+            __syncthreads();
+        }
+        uint32_t run = carry + s[cur][tid] - sum;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            uint4 o;
+            o.x = run;
+            o.y = (run += v[q].x);
+            o.z = (run += v[q].y);
+            o.w = (run += v[q].z);
+            run += v[q].w;
+            if (b0 + 4 * q < len) *reinterpret_cast<uint4*>(a + b0 + 4 * q) = o;
+        }
+        carry += s[cur][1023];
+        __syncthreads();  // s is rewritten by the next segment
+    }
+    if (tid == 0) wtot[blockIdx.x] = carry;
+}
+
+// One block per tile: rank the tile's items by digit, stably, stage them
+// digit-sorted in LDS, then write each digit's run to its place --
+// consecutive threads write consecutive addresses of a few runs instead of
+// one scattered word each.  Wave q owns the tile's items [q 1024, (q+1) 1024),
+// 64 consecutive ones per round, and counts digits in its own LDS row, so the
+// ranking needs no block barrier: source order = (wave, round, lane).
+__global__ void __launch_bounds__(256) k_sort_scatter(const uint32_t* __restrict__ keys_in,
+                                                      const uint32_t* __restrict__ vals_in,
+                                                      const uint32_t* __restrict__ hist,
+                                                      const uint32_t* __restrict__ wtot, SortPass sp,
+                                                      uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out) {
+    __shared__ uint32_t gbase[256], loff[256], wcnt[4][256], scan[2][256];
+    __shared__ uint32_t sk[kSortTile], sv[kSortTile];
+    __shared__ uint32_t wb_s;
+    const uint32_t tid = threadIdx.x, w = blockIdx.x / sp.tpw, t = blockIdx.x % sp.tpw;
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    size_t base;
+    uint32_t count;
+    sort_window(sp, wtot, w, base, count);
+    const uint32_t lo = t * kSortTile + wave * (64 * kSortIpt);
+    uint32_t keyr[kSortIpt], valr[kSortIpt];  // the wave's loads in flight at once
+#pragma unroll
+    for (uint32_t r = 0; r < kSortIpt; r++) {
+        const uint32_t k = lo + r * 64 + lane;
+        keyr[r] = 0xffffffffu;
+        valr[r] = 0;
+        if (k < count) {
+            keyr[r] = keys_in[base + k];
+            valr[r] = vals_in[base + k];
+        }
+    }
+    if (tid == 0) wb_s = sort_wbase(wtot, w);
+    // this tile's digit counts from the prefix: next entry (digit-major) minus this one
+    const size_t flat = (size_t)tid * sp.tpw + t, len = (size_t)256 * sp.tpw;
+    const uint32_t* hw = hist + (size_t)w * len;
+    const uint32_t off = hw[flat];
+    const uint32_t cnt = (flat + 1 < len ? hw[flat + 1] : wtot[w]) - off;
+    scan[0][tid] = cnt;
+#pragma unroll
+    for (int q = 0; q < 4; q++) wcnt[q][tid] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+    uint32_t slot[kSortIpt];  // rank among the wave's items of the same digit
+#pragma unroll
+    for (uint32_t r = 0; r < kSortIpt; r++) {
+        const bool valid = keyr[r] < sp.sentinel;
+        const uint32_t d = valid ? ((keyr[r] & sp.bmask) >> sp.shift) & 0xff : 0;
+        // lanes of this wave holding the same digit (8 ballots)
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint64_t m = __ballot((d >> b) & 1);
+            peers &= ((d >> b) & 1) ? m : ~m;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        const uint32_t before = valid ? wcnt[wave][d] : 0;  // read by all peers before the leader's write
+        slot[r] = before + rank;
+        if (valid && rank == 0) wcnt[wave][d] = before + (uint32_t)__popcll(peers);
+    }
+    int cur = 0;
+    for (uint32_t d = 1; d < 256; d <<= 1) {  // tile-local digit starts (the barrier also publishes wcnt)
+        scan[cur ^ 1][tid] = scan[cur][tid] + (tid >= d ? scan[cur][tid - d] : 0u);
+        cur ^= 1;
+        __syncthreads();
+    }
+    const uint32_t tile_items = scan[cur][255];
+    loff[tid] = scan[cur][tid] - cnt;
+    gbase[tid] = wb_s + off;
+    {  // wave q's run of digit d starts after waves < q's
+        uint32_t run = scan[cur][tid] - cnt;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t c = wcnt[q][tid];  // column tid is this thread's alone here
+            wcnt[q][tid] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kSortIpt; r++) {
+        if (keyr[r] < sp.sentinel) {
+            const uint32_t d = ((keyr[r] & sp.bmask) >> sp.shift) & 0xff;
+            const uint32_t pos = wcnt[wave][d] + slot[r];
+            sk[pos] = keyr[r];
+            sv[pos] = valr[r];
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < tile_items; k += 256) {
+        const uint32_t key = sk[k];
+        const uint32_t d = ((key & sp.bmask) >> sp.shift) & 0xff;
+        const size_t pos = (size_t)gbase[d] + (k - loff[d]);
+        keys_out[pos] = key;
+        vals_out[pos] = sv[k];
+    }
 }
 
 // Bucket accumulation, load-balanced: lane k owns the sorted items
@@ -581,6 +784,7 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     hipError_t e = msm_plan(p, G, n);
     if (e != hipSuccess) return e;
     if (ws_bytes < p.total || !ws) return hipErrorInvalidValue;
+    if (p.items > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit item positions
     char* base = static_cast<char*>(ws);
     uint32_t* keys_in = reinterpret_cast<uint32_t*>(base + p.off_keys_in);
     uint32_t* keys_out = reinterpret_cast<uint32_t*>(base + p.off_keys_out);
@@ -596,10 +800,23 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     hipLaunchKernelGGL(k_msm_digits, dim3(msm_blocks(n, 256)), dim3(256), 0, s, scalars, n, p.c, p.W, p.B, keys_in,
                        vals_in);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    size_t sort_bytes = p.sort_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(base + p.off_sort, sort_bytes, keys_in, keys_out, vals_in, vals_out,
-                                           (int)p.items, 0, (int)p.key_bits, s);
-    if (e != hipSuccess) return e;
+    // the bucketing sort: ping-pong between the _in and _out arrays; the last
+    // destination's tail past the nonzero items is set to sentinel keys first
+    uint32_t* hist = reinterpret_cast<uint32_t*>(base + p.off_hist);
+    uint32_t* wtot = reinterpret_cast<uint32_t*>(base + p.off_wtot);
+    uint32_t *ksrc = keys_in, *vsrc = vals_in, *kdst = keys_out, *vdst = vals_out;
+    const unsigned tiles = p.W * p.tpw;
+    for (uint32_t pass = 0; pass < p.passes; pass++) {
+        const SortPass sp{8 * pass, p.B - 1, p.W * p.B, p.tpw, pass == 0 ? 1u : 0u, n};
+        hipLaunchKernelGGL(k_sort_hist, dim3(tiles), dim3(256), 0, s, ksrc, wtot, sp, hist);
+        hipLaunchKernelGGL(k_sort_scan, dim3(p.W), dim3(1024), 0, s, hist, p.tpw, wtot);
+        if (pass + 1 == p.passes && (e = hipMemsetAsync(kdst, 0xff, 4 * p.items, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_sort_scatter, dim3(tiles), dim3(256), 0, s, ksrc, vsrc, hist, wtot, sp, kdst, vdst);
+        std::swap(ksrc, kdst);
+        std::swap(vsrc, vdst);
+    }
+    keys_out = ksrc;  // the last pass's output
+    vals_out = vsrc;
     if ((e = hipMemsetAsync(start, 0, 4 * nb, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(end, 0, 4 * nb, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_msm_bucket_bounds, dim3(msm_blocks(p.items, 256)), dim3(256), 0, s, keys_out, p.items,

@@ -95,7 +95,7 @@ def test_scalar_mul_bit_exact(gpu, oracle, group):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [0, 1, 2, 3, 17, 300, 4099])
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 17, 300, 4099, 9000])
 def test_g1_multiexp_matches_oracle(gpu, oracle, n):
     g = rng(50 + n)
     p = oracle.g1_mul_generator(random_scalars(g, n), NT)
@@ -137,3 +137,19 @@ def test_g1_multiexp_large_identity(gpu, oracle):
     p = oracle.g1_mul_generator(a, NT)
     got = oracle.g1_into_affine(gpu.g1_multiexp(p, s))
     np.testing.assert_array_equal(got, oracle.g1_mul_generator(combined_scalar(a, s)))
+
+
+@pytest.mark.gpu
+def test_g1_multiexp_deterministic(gpu, oracle):
+    # the bucketing sort is stable (term order inside a bucket), so two runs
+    # give the same Jacobian words, not just the same point; 2^14 terms,
+    # c = 11: two counting-sort passes, the second over 2 bits
+    g = rng(80)
+    n = 1 << 14
+    p = oracle.g1_mul_generator(random_scalars(g, n), NT)
+    s = random_scalars(g, n)
+    s[100:300] = s[7]            # crowded buckets: runs far longer than a tile's share
+    a = gpu.g1_multiexp(p, s)
+    b = gpu.g1_multiexp(p, s)
+    np.testing.assert_array_equal(a, b)
+    assert oracle.g1_eq(a, oracle.g1_multiexp(p, s, NT)).all()

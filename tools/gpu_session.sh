@@ -50,7 +50,7 @@ for step in "$@"; do
         frbench) run bench_fr 300 python bench.py --workload fr_mul --steps 20 --warmup 3 ;;
         msmtests) run pytest_msm 600 python -u -m pytest tests/test_msm.py tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         msmbench) run bench_msm 400 python bench.py --workload msm --steps 5 --warmup 1 ;;
-        profmsm) run prof_msm 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_msm -o run -- python bench.py --workload msm --steps 3 --warmup 1 --no-cpu-baseline ;;
+        profmsm) run prof_msm 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_msm -o run -- python bench.py --workload msm --steps 3 --warmup 1 --no-cpu-baseline ;;
         profwnaf) run prof_wnaf 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_wnaf -o run -- python bench.py --workload wnaf --steps 3 --warmup 1 --no-cpu-baseline ;;
         profdec) run prof_dec 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dec -o run -- python bench.py --workload decode --steps 3 --warmup 1 --no-cpu-baseline ;;
         fqbench) run bench_fq 300 python bench.py --workload fq_mul --steps 20 --warmup 3 --no-cpu-baseline ;;
@@ -65,6 +65,10 @@ for step in "$@"; do
                run pmc_sq2 600 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR -d gpurun_out/pmc_sq2 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
         pmcsq4) run pmc4_sq1 300 env PA_PAIRING_KERNEL=1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES -d gpurun_out/pmc4_sq1 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline &&
                 run pmc4_sq2 300 env PA_PAIRING_KERNEL=1 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR -d gpurun_out/pmc4_sq2 -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+        pmcdec) run pmc_dec 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc_dec -o run -- python bench.py --workload decode --steps 2 --warmup 1 --no-cpu-baseline ;;
+        pmcmsm) run pmc_msm 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc_msm -o run -- python bench.py --workload msm --steps 2 --warmup 1 --no-cpu-baseline &&
+                run pmc_msm_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_msm_fetch -o run -- python bench.py --workload msm --steps 2 --warmup 1 --no-cpu-baseline &&
+                run pmc_msm_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_msm_write -o run -- python bench.py --workload msm --steps 2 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -268,9 +268,29 @@ class Emitter:
             return self.DROP_W[3]
         return max(self.DROP_W["ALM".index(k)] for k in kinds)
 
+    # a value whose only other copy is in the HBM workspace and that is read
+    # again within KEEP_M operations is copied to a free AGPR / LDS slot as it
+    # leaves its V slot, so its next uses reload on chip (PGEN_KEEP_M=0: off)
+    KEEP_M = int(os.environ.get("PGEN_KEEP_M", "0"))
+
+    def free_onchip(self):
+        for kind, tab in (("A", self.aslot), ("L", self.lslot)):
+            for j, o in enumerate(tab):
+                if o is None:
+                    return (kind, j)
+        return None
+
     def evict(self, k, pos):
         vs = self.vslot[k]
         vs.locs.discard(("V", k))
+        if (self.KEEP_M and vs.locs and all(l[0] == "M" for l in vs.locs)
+                and self.next_use(vs, pos) - pos <= self.KEEP_M and vs.val.id in self.local_ids):
+            loc = self.free_onchip()
+            if loc is not None:
+                self.copy(("V", k), loc)
+                self.own(loc, vs)
+                vs.locs.add(loc)
+                self.bump("keep_" + loc[0])
         if not vs.locs:
             loc = self.tier_slot(vs, pos)
             self.copy(("V", k), loc)
