@@ -10,7 +10,7 @@
 static void report(const char* what, float ms) {
     unsigned long long h[8][3];
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(pa::g_coop_prof), sizeof h);
-    const char* names[8] = {"LIN", "P1", "P2", "SQ", "INV", "k5", "k6", "k7"};
+    const char* names[8] = {"LIN", "P1", "P2", "SQ", "INV", "LC", "k6", "k7"};
     unsigned long long tot = 0;
     for (int k = 0; k < 8; k++) tot += h[k][0];
     printf("%s: %.3f ms, %llu profiled cycles\n", what, ms, tot);

@@ -69,6 +69,9 @@ for step in "$@"; do
         pmcmsm) run pmc_msm 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc_msm -o run -- python bench.py --workload msm --steps 2 --warmup 1 --no-cpu-baseline &&
                 run pmc_msm_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_msm_fetch -o run -- python bench.py --workload msm --steps 2 --warmup 1 --no-cpu-baseline &&
                 run pmc_msm_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_msm_write -o run -- python bench.py --workload msm --steps 2 --warmup 1 --no-cpu-baseline ;;
+        cooptests) run pytest_coop 600 python -u -m pytest tests/test_gpu_parity.py tests/test_bench_sizes.py -m gpu -k "coop or multi_pairing" -x -v --timeout 200 --timeout-method thread ;;
+        coopprof) run coop_prof 120 ./tools/coop_prof ;;
+        cooplat) run coop_latency 300 python tools/coop_latency.py ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

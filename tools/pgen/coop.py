@@ -46,15 +46,22 @@ from dsl import Loop, If, Prog  # noqa: E402
 from tower import Tower, X_ABS  # noqa: E402
 
 LANES = 64
-K_LIN, K_P1, K_P2, K_SQ, K_INV = range(5)
-KIND_NAME = ["LIN", "P1", "P2", "SQ", "INV"]
+K_LIN, K_P1, K_P2, K_SQ, K_INV, K_LC = range(6)
+KIND_NAME = ["LIN", "P1", "P2", "SQ", "INV", "LC"]
+# LC (linear combination) tasks replace the LIN chains unless COOP_CHAINS=1:
+# every LIN subgraph between products collapses to sum c_i x_i over
+# materialized values (products, inversions, arguments, constants), one lane
+# task per product operand / returned value, so the steps between two
+# product levels are one LC step instead of a LIN level per chain depth.
+LC = os.environ.get("COOP_CHAINS", "0") != "1"
+LC_TMAX = 15       # terms of one LC task (incl. the zero padding of a split)
 # DSL-level LIN ops
 L_ADD, L_SUB, L_NEG, L_RED = range(4)
 # lane-level chain ops of a LIN task: acc = slot s0, then up to 4 of these
 C_END, C_ADD, C_SUB, C_RSUB, C_NEG, C_RED, C_DBL = range(7)
 MAX_CHAIN, MAX_SIDE = 4, 3
 # latency estimates (instructions) for the list scheduler's priorities
-COST = {K_LIN: 90, K_P1: 560, K_P2: 760, K_SQ: 480, K_INV: 9000}
+COST = {K_LIN: 90, K_P1: 560, K_P2: 760, K_SQ: 480, K_INV: 9000, K_LC: 60}
 GA, GB, GC, GD, GE, GF, GG = 1, 2, 3, 4, 5, 6, 7   # operand areas
 
 
@@ -287,7 +294,8 @@ class Task:
     up to MAX_CHAIN LIN nodes, each consuming the previous one's value (the
     accumulator) and at most MAX_SIDE side operands in total; only the last
     node's value is materialized."""
-    __slots__ = ("id", "kind", "nodes", "out", "deps", "users", "height", "step", "slot")
+    __slots__ = ("id", "kind", "nodes", "out", "deps", "users", "height", "step", "slot", "form", "red", "opnd", "u",
+                 "lay")
 
     def __init__(self, id_, kind, nodes_):
         self.id, self.kind, self.nodes = id_, kind, nodes_
@@ -364,6 +372,188 @@ def build_tasks(nodes):
     return tasks, owner
 
 
+def form_u(f):
+    """limb bound U of sum c x over F<1> leaves: the positive part plus the
+    subtraction constant C_B, B = sum of the negative coefficients (99: none fits)"""
+    pos = sum(c for c in f.values() if c > 0)
+    neg = -sum(c for c in f.values() if c < 0)
+    if neg > 14:
+        return 99
+    return pos + (dsl.SUBCU[neg] if neg else 0)
+
+
+def lc_layout(form, split):
+    """term order of an LC task for a step whose lanes reduce (red) their
+    partial sum after `split` terms (0: no mid-step reduction): the first
+    segment keeps U <= 16; the reduced value (F<1>) plus C_B2 plus the rest
+    too.  Largest coefficients first; the first segment is padded to `split`
+    with (zero slot, 0).  None if the form does not fit."""
+    items = sorted(form.items(), key=lambda kv: (-abs(kv[1]), kv[0]))
+    if not split:
+        return items if len(items) <= LC_TMAX and form_u(dict(items)) <= 16 else None
+    seg1, rest = [], []
+    for kv in items:
+        if len(seg1) < split and form_u(dict(seg1 + [kv])) <= 16:
+            seg1.append(kv)
+        else:
+            rest.append(kv)
+    neg2 = -sum(c for _, c in rest if c < 0)
+    if neg2 > 14 or 1 + form_u(dict(rest)) > 16 or split + len(rest) > LC_TMAX:
+        return None
+    return seg1 + [(("s", (0, 0)), 0)] * (split - len(seg1)) + rest
+
+
+def lc_fits(form):
+    return any(lc_layout(form, sp) is not None for sp in (0, 4, 8))
+
+
+def lc_forms(nodes, mat):
+    """LIN node -> {leaf: coefficient}; leaves are ("n", id) for products,
+    inversions and materialized LIN nodes, ("s", slot) for arguments and
+    constants (the zero constant dropped).  red is the identity on values."""
+    form = {}
+
+    def get(x):
+        if isinstance(x, tuple):
+            return {} if x[1] == (0, 0) else {("s", x[1]): 1}
+        if nodes[x].kind != K_LIN or x in mat:
+            return {("n", x): 1}
+        return form[x]
+    for n in nodes:
+        if n.kind != K_LIN:
+            continue
+        f = dict(get(n.srcs[0]))
+        if n.lop == L_ADD:
+            for k, v in get(n.srcs[1]).items():
+                f[k] = f.get(k, 0) + v
+        elif n.lop == L_SUB:
+            for k, v in get(n.srcs[1]).items():
+                f[k] = f.get(k, 0) - v
+        elif n.lop == L_NEG:
+            f = {k: -v for k, v in f.items()}
+        form[n.id] = {k: v for k, v in f.items() if v}
+    return form, get
+
+
+def build_lc_tasks(nodes):
+    """Tasks for the LC form: products / inversions as before, and one LC
+    task per LIN value that is a product or inversion operand (unless it is a
+    bare leaf), a returned value, or materialized because a form using it
+    would exceed LC_TMAX terms or the bound U <= 16."""
+    prod = (K_P1, K_P2, K_SQ)
+    mat = set()
+    while True:
+        form, get = lc_forms(nodes, mat)
+        need = set(mat)
+        for n in nodes:
+            if n.kind in prod or n.kind == K_INV:
+                need |= {x for x in n.srcs if not isinstance(x, tuple) and nodes[x].kind == K_LIN}
+            if n.ret is not None and n.kind == K_LIN:
+                need.add(n.id)
+        bad = [x for x in sorted(need) if not lc_fits(form[x])]
+        if not bad:
+            break
+        grew = len(mat)
+        for x in bad:
+            # materialize the unmaterialized LIN source with the biggest form
+            # (none left: a source was materialized for an earlier one this round)
+            kids = [y for y in nodes[x].srcs if not isinstance(y, tuple) and nodes[y].kind == K_LIN
+                    and y not in mat]
+            if kids:
+                mat.add(max(kids, key=lambda y: (len(form[y]), form_u(form[y]), y)))
+        assert len(mat) > grew, "LC forms too big with leaf sources only: %s" % bad
+    # tasks, in node order
+    tasks, owner = [], {}
+    # a returned LIN value that is one F<1> leaf (a product, an inversion or a
+    # materialized value, coefficient 1) is returned by that leaf's task
+    # directly instead of through a copy step
+    for x in sorted(need):
+        n = nodes[x]
+        f = form[x]
+        if n.ret is None or x in mat or len(f) != 1 or \
+                any(x in nodes[u].srcs for u in n.users if nodes[u].kind != K_LIN):
+            continue
+        (k, c), = f.items()
+        if c != 1 or k[0] != "n" or nodes[k[1]].ret is not None:
+            continue
+        y = k[1]
+        if nodes[y].kind == K_LIN and y not in mat:
+            continue
+        nodes[y].ret, n.ret = n.ret, None
+        need.discard(x)
+    lc_nodes = sorted(need)
+    lcset = set(lc_nodes)
+    for n in nodes:
+        if n.kind in prod or n.kind == K_INV or n.id in lcset:
+            t = Task(len(tasks), n.kind if n.id not in lcset else K_LC, [n.id])
+            t.form = sorted(form[n.id].items()) if n.id in lcset else None
+            t.red = n.id in lcset and (n.id in mat or n.ret is not None)
+            t.opnd = None
+            tasks.append(t)
+            owner[n.id] = t.id
+    # a bare-leaf LC task (one leaf, coefficient 1, not returned / materialized) is not needed
+    def ref_of(x):
+        """operand x of a product / inversion -> ("t", task) or ("s", slot)"""
+        if isinstance(x, tuple):
+            return ("s", x[1])
+        if nodes[x].kind == K_LIN and not tasks[owner[x]].red:
+            f = form[x]
+            if len(f) == 1:
+                (k, c), = f.items()
+                if c == 1:
+                    return ("s", k[1]) if k[0] == "s" else ("t", owner[k[1]])
+            if not f:
+                return ("s", (0, 0))
+        return ("t", owner[x])
+    used = set()
+    for t in tasks:
+        n = nodes[t.out]
+        if t.kind in prod or t.kind == K_INV:
+            t.opnd = [ref_of(x) for x in n.srcs]
+            used |= {r[1] for r in t.opnd if r[0] == "t"}
+    keep = [t for t in tasks if t.kind != K_LC or t.red or t.id in used]
+    # the limb bound of each LC output; red the largest operand until every
+    # product's column bound holds (P1 / P2: sum U_a U_b <= 17, SQ: U <= 2)
+    for t in keep:
+        if t.kind == K_LC:
+            t.u = 1 if t.red else form_u(dict(t.form))
+    byid = {t.id: t for t in keep}
+
+    def u_of(r):
+        return byid[r[1]].u if r[0] == "t" and byid[r[1]].kind == K_LC else 1
+    for t in keep:
+        if t.kind not in prod and t.kind != K_INV:
+            continue
+        while True:
+            us = [u_of(r) for r in t.opnd]
+            if t.kind == K_INV:
+                ok = us[0] == 1
+            elif t.kind == K_SQ:
+                ok = us[0] <= 2
+            else:
+                ok = sum(us[2 * k] * us[2 * k + 1] for k in range(len(us) // 2)) <= 17
+            if ok:
+                break
+            cands = [r for r in t.opnd if r[0] == "t" and byid[r[1]].kind == K_LC and byid[r[1]].u > 1]
+            r = max(cands, key=lambda r: (byid[r[1]].u, r[1]))
+            byid[r[1]].red, byid[r[1]].u = True, 1
+    # renumber, dependencies
+    remap = {t.id: k for k, t in enumerate(keep)}
+    for k, t in enumerate(keep):
+        t.id = k
+        t.deps, t.users = set(), []
+    for t in keep:
+        if t.kind == K_LC:
+            t.deps = {remap[owner[k[1]]] for k, _ in t.form if k[0] == "n"}
+        else:
+            t.opnd = [("t", remap[r[1]]) if r[0] == "t" else r for r in t.opnd]
+            t.deps = {r[1] for r in t.opnd if r[0] == "t"}
+        for d in t.deps:
+            keep[d].users.append(t.id)
+    owner2 = {t.out: t.id for t in keep}
+    return keep, owner2
+
+
 def schedule(tasks):
     """List scheduling over tasks.  Products of any form share a step (the
     step runs the sop2 leaf, P1 lanes padding with zero, unless every lane is
@@ -372,6 +562,8 @@ def schedule(tasks):
     to a product of (almost) the same height is still ready, so products of
     one level meet in one step."""
     def cost(t):
+        if t.kind == K_LC:
+            return COST[K_LC] + 25 * len(t.form) + (70 if t.red else 0)
         return COST[K_P2 if t.kind in (K_P1, K_P2, K_SQ) else t.kind] if t.kind != K_LIN else \
             COST[K_LIN] + 25 * len(t.nodes)
     for t in reversed(tasks):
@@ -385,9 +577,9 @@ def schedule(tasks):
         top = tasks[ready[0]]
         cls = "P" if top.kind in prod else top.kind
         if cls == "P":
-            best_lin = max((tasks[i].height for i in ready if tasks[i].kind == K_LIN), default=-1)
+            best_lin = max((tasks[i].height for i in ready if tasks[i].kind in (K_LIN, K_LC)), default=-1)
             if best_lin > top.height - COST[K_P2] // 2:
-                cls = K_LIN
+                cls = K_LC if LC else K_LIN
         if cls == "P":
             batch = [i for i in ready if tasks[i].kind in prod][:LANES]
             kinds = {tasks[i].kind for i in batch}
@@ -451,6 +643,8 @@ class Macro:
         self.nodes, self.rets = flatten(prog, consts, cindex)
 
     def build(self, scratch0):
+        if LC:
+            return self.build_lc(scratch0)
         nodes = self.nodes
         self.tasks, owner = build_tasks(nodes)
         self.steps = schedule(self.tasks)
@@ -479,6 +673,64 @@ class Macro:
                     recs.append([0, dst, src_ref(nodes[t.out].srcs[0]), 0, 0, 0, 0, 0])
                 else:
                     recs.append(self._chain(t, src_ref, dst))
+            self.records.append((kind, recs))
+
+    def build_lc(self, scratch0):
+        """records of the LC form.  Products: [0, dst, a, b, c, d, 0, 0];
+        LC: [nterms | red << 5 | B1 << 6 | B2 << 10, dst, (slot, coef) x
+        nterms]; B1 / B2 = the sums of the negative coefficients before / after
+        the step's split point (C_B added at each segment's start, 0: none)"""
+        nodes = self.nodes
+        self.tasks, owner = build_lc_tasks(nodes)
+        self.steps = schedule(self.tasks)
+        self.top = allocate(nodes, self.tasks, self.steps, scratch0)
+        tasks = self.tasks
+
+        def ref(r):
+            return ref16(r[1]) if r[0] == "s" else ref16(tasks[r[1]].slot)
+        self.records = []
+        self.splits = []
+        for kind, batch in self.steps:
+            recs = []
+            split = 0
+            if kind == K_LC:
+                # one mid-step reduction point for the whole step (0, 4 or 8 terms)
+                for split in (0, 4, 8):
+                    lays = [lc_layout(dict(tasks[i].form), split) for i in batch]
+                    if all(l is not None for l in lays):
+                        break
+                else:
+                    raise AssertionError("%s: no common split for an LC step" % self.name)
+                for i, l in zip(batch, lays):
+                    t = tasks[i]
+                    t.lay = l
+                    rest = l[split:] if split else []
+                    if not t.red and split and len(l) > split and 1 + form_u(dict(rest)) > t.u:
+                        t.red = True       # keep the bound the products were checked with
+            self.splits.append(split)
+            for i in batch:
+                t = tasks[i]
+                dst = ref16(t.slot)
+                if kind in (K_P1, K_P2, K_SQ):
+                    srcs = [ref(r) for r in t.opnd]
+                    if nodes[t.out].kind == K_SQ:
+                        srcs = srcs * 2
+                    if len(srcs) == 2:
+                        srcs += [ref16((0, 0))] * 2
+                    recs.append([0, dst] + srcs + [0, 0])
+                elif kind == K_INV:
+                    recs.append([0, dst, ref(t.opnd[0]), 0, 0, 0, 0, 0])
+                else:
+                    lay = t.lay
+                    sp = split
+                    seg1, seg2 = (lay[:sp], lay[sp:]) if sp else (lay, [])
+                    b1 = -sum(c for _, c in seg1 if c < 0)
+                    b2 = -sum(c for _, c in seg2 if c < 0)
+                    rec = [len(lay) | (int(t.red) << 5) | (b1 << 6) | (b2 << 10), dst]
+                    for (k, c) in lay:
+                        leaf = ref16(k[1]) if k[0] == "s" else ref16(tasks[owner[k[1]]].slot)
+                        rec += [leaf, c & 0xffff]
+                    recs.append(rec)
             self.records.append((kind, recs))
 
     def _chain(self, t, src_ref, dst):
@@ -530,7 +782,8 @@ class Macro:
         for kind, recs in self.records:
             c, lanes = by.get(KIND_NAME[kind], (0, 0))
             by[KIND_NAME[kind]] = (c + 1, lanes + len(recs))
-        est = sum(COST[k] + (25 * max(r[0] for r in recs) if k == K_LIN else 0) for k, recs in self.records)
+        est = sum(COST[k] + (25 * max(r[0] & 31 for r in recs) if k in (K_LIN, K_LC) else 0)
+                  for k, recs in self.records)
         return {"nodes": len(self.nodes), "tasks": len(self.tasks), "steps": len(self.records),
                 "scratch_top": self.top, "by_kind": by, "est_instr": est}
 
@@ -561,9 +814,32 @@ def replay(m, consts, args):
 
     def at(r):
         return V[(r >> 13, r & 8191)]
-    for kind, recs in m.records:
+    for si, (kind, recs) in enumerate(m.records):
         res = []
         for rec in recs:
+            if kind == K_LC:
+                # the kernel's u32 limb arithmetic, checked against the F<U> contract
+                nt, red, b1, b2 = rec[0] & 31, (rec[0] >> 5) & 1, (rec[0] >> 6) & 15, rec[0] >> 10
+                split = m.splits[si]
+                terms = [(rec[2 + 2 * j], (rec[3 + 2 * j] ^ 0x8000) - 0x8000) for j in range(nt)]
+                segs = [terms[:split], terms[split:]] if split else [terms]
+                acc, base_u = [0] * 14, 0
+                for k, seg in enumerate(segs):
+                    b = b1 if k == 0 else b2
+                    assert b == -sum(c for _, c in seg if c < 0)
+                    if b:
+                        acc = [p + q for p, q in zip(acc, dsl.SUBC[b])]
+                    for slot, cf in seg:
+                        x = at(slot)
+                        assert max(x) < (1 << 28) and dsl.val_of(x) < 2 * dsl.Q, "LC leaf beyond F<1>"
+                        acc = [p + cf * q for p, q in zip(acc, x)]
+                    u = base_u + form_u({j: c for j, (_, c) in enumerate(seg)})
+                    assert all(0 <= v <= u * dsl.MASK for v in acc), "LC limbs beyond F<%d>" % u
+                    if k + 1 < len(segs):
+                        acc, base_u = list(dsl.red_limbs(acc)), 1
+                r = dsl.red_limbs(acc) if red else tuple(acc)
+                res.append(((rec[1] >> 13, rec[1] & 8191), r))
+                continue
             hdr, dst, a, b, c, d, o01, o23 = rec
             if kind in (K_P1, K_P2):
                 r = dsl.mont_sop([(at(a), at(b)), (at(c), at(d))])
@@ -615,7 +891,15 @@ def check(macros, consts, trials=3):
             args = {r: tuple(dsl.to_mont_limbs(rng.randrange(dsl.Q))) for r in refs}
             want = dsl.evaluate(m.prog, args)
             got = replay(m, consts, args)
-            assert got == want, "%s: schedule replay differs from the DSL macro" % m.name
+            if LC:
+                # the same field values, every output F<1> (limbs < 2^28, value < 2q)
+                assert set(got) == set(want)
+                for k in want:
+                    assert dsl.val_of(got[k]) % dsl.Q == dsl.val_of(want[k]) % dsl.Q, \
+                        "%s: LC schedule replay differs from the DSL macro at %s" % (m.name, k)
+                    assert max(got[k]) < (1 << 28) and dsl.val_of(got[k]) < 2 * dsl.Q, "%s: output not F<1>" % m.name
+            else:
+                assert got == want, "%s: schedule replay differs from the DSL macro" % m.name
     print("all %d macros: schedule replay == DSL (%d trials each)" % (len(macros), trials))
 
 
@@ -624,13 +908,23 @@ def emit(macros, consts, path):
     steps, recs, mtab = [], [], []
     for m in macros:
         mtab.append((len(steps), len(m.records)))
-        for kind, rr in m.records:
-            steps.append((kind, len(rr), len(recs)))
-            recs.extend(rr)
+        for si, (kind, rr) in enumerate(m.records):
+            if kind == K_LC:
+                # R rows of 8 u16 per lane (word 0 = hdr | dst, 1 + j = term j)
+                T = max(r[0] & 31 for r in rr)
+                R = (2 + 2 * T + 7) // 8
+                assert T <= 15 and R <= 4
+                steps.append((kind | (R | T << 4 | (m.splits[si] // 4) << 8) << 16, len(rr), len(recs)))
+                for r in rr:
+                    r = r + [0] * (8 * R - len(r))
+                    recs.extend(r[8 * k:8 * k + 8] for k in range(R))
+            else:
+                steps.append((kind, len(rr), len(recs)))
+                recs.extend(rr)
     nslots = max(m.top for m in macros)
     L = ["// GENERATED by tools/pgen/coop.py -- cooperative (one wave per item) macro-operations", "#pragma once",
          "#include <stdint.h>", "namespace pa {", "namespace coop {",
-         "enum : uint8_t { K_LIN = %d, K_P1, K_P2, K_SQ, K_INV };" % K_LIN,
+         "enum : uint8_t { K_LIN = %d, K_P1, K_P2, K_SQ, K_INV, K_LC };" % K_LIN,
          "enum : uint32_t { C_END = %d, C_ADD, C_SUB, C_RSUB, C_NEG, C_RED, C_DBL };" % C_END,
          "enum Macro : int { %s, kMacros };" % ", ".join("M_%s" % m.name.upper() for m in macros),
          "constexpr int kConsts = %d;      // absolute slots 0 .. kConsts-1: constants (slot 0 = zero)" % len(consts),
@@ -642,7 +936,7 @@ def emit(macros, consts, path):
              len(consts), ", ".join("{" + ", ".join("0x%xu" % x for x in c) + "}" for c in consts)),
          "// macro -> (first step, steps)",
          "__device__ const uint16_t kMacro[%d][2] = {%s};" % (len(mtab), ", ".join("{%d, %d}" % t for t in mtab)),
-         "// step -> kind | lanes << 8, first record",
+         "// step -> kind | lanes << 8 (| LC: record rows R << 16 | max terms T << 20), first record",
          "__device__ const uint32_t kStep[%d][2] = {%s};" % (
              len(steps), ", ".join("{%du, %du}" % (k | (n << 8), b) for k, n, b in steps)),
          "// record: hdr (LIN: chain length), dst, s0..s3, chain ops 0|1, 2|3 (code | bound << 3)",
