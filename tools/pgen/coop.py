@@ -55,6 +55,7 @@ KIND_NAME = ["LIN", "P1", "P2", "SQ", "INV", "LC"]
 # product levels are one LC step instead of a LIN level per chain depth.
 LC = os.environ.get("COOP_CHAINS", "0") != "1"
 LC_TMAX = 15       # terms of one LC task (incl. the zero padding of a split)
+PAIRS = os.environ.get("COOP_PAIRS", "0") == "1"   # measured: +2.5k cycles per product step, a wash
 # DSL-level LIN ops
 L_ADD, L_SUB, L_NEG, L_RED = range(4)
 # lane-level chain ops of a LIN task: acc = slot s0, then up to 4 of these
@@ -491,37 +492,41 @@ def build_lc_tasks(nodes):
             t.opnd = None
             tasks.append(t)
             owner[n.id] = t.id
-    # a bare-leaf LC task (one leaf, coefficient 1, not returned / materialized) is not needed
-    def ref_of(x):
-        """operand x of a product / inversion -> ("t", task) or ("s", slot)"""
+    # product operands: a bare leaf (one term, coefficient 1), a "pair" -- at
+    # most two terms, computed in the product lane's prologue (COOP_PAIRS) --
+    # or an LC task; a bare-leaf LC task not returned / materialized is dropped
+    def leafref(k):
+        return ("s", k[1]) if k[0] == "s" else ("t", owner[k[1]])
+
+    def ref_of(x, pairs_ok):
+        """operand x of a product / inversion -> ("t", task), ("s", slot) or
+        ("p", terms, U, node)"""
         if isinstance(x, tuple):
             return ("s", x[1])
         if nodes[x].kind == K_LIN and not tasks[owner[x]].red:
             f = form[x]
+            if not f:
+                return ("s", (0, 0))
             if len(f) == 1:
                 (k, c), = f.items()
                 if c == 1:
-                    return ("s", k[1]) if k[0] == "s" else ("t", owner[k[1]])
-            if not f:
-                return ("s", (0, 0))
+                    return leafref(k)
+            if pairs_ok and PAIRS and len(f) <= 2 and form_u(f) <= 4:
+                return ("p", tuple((leafref(k), c) for k, c in sorted(f.items())), form_u(f), x)
         return ("t", owner[x])
-    used = set()
     for t in tasks:
-        n = nodes[t.out]
-        if t.kind in prod or t.kind == K_INV:
-            t.opnd = [ref_of(x) for x in n.srcs]
-            used |= {r[1] for r in t.opnd if r[0] == "t"}
-    keep = [t for t in tasks if t.kind != K_LC or t.red or t.id in used]
-    # the limb bound of each LC output; red the largest operand until every
-    # product's column bound holds (P1 / P2: sum U_a U_b <= 17, SQ: U <= 2)
-    for t in keep:
         if t.kind == K_LC:
             t.u = 1 if t.red else form_u(dict(t.form))
-    byid = {t.id: t for t in keep}
+        elif t.kind in prod or t.kind == K_INV:
+            t.opnd = [ref_of(x, t.kind != K_INV) for x in nodes[t.out].srcs]
 
+    # red the largest operand (a pair becomes its LC task first) until every
+    # product's column bound holds (P1 / P2: sum U_a U_b <= 17, SQ: U <= 2)
     def u_of(r):
-        return byid[r[1]].u if r[0] == "t" and byid[r[1]].kind == K_LC else 1
-    for t in keep:
+        if r[0] == "p":
+            return r[2]
+        return tasks[r[1]].u if r[0] == "t" and tasks[r[1]].kind == K_LC else 1
+    for t in tasks:
         if t.kind not in prod and t.kind != K_INV:
             continue
         while True:
@@ -534,9 +539,21 @@ def build_lc_tasks(nodes):
                 ok = sum(us[2 * k] * us[2 * k + 1] for k in range(len(us) // 2)) <= 17
             if ok:
                 break
-            cands = [r for r in t.opnd if r[0] == "t" and byid[r[1]].kind == K_LC and byid[r[1]].u > 1]
-            r = max(cands, key=lambda r: (byid[r[1]].u, r[1]))
-            byid[r[1]].red, byid[r[1]].u = True, 1
+            k = max(range(len(us)), key=lambda j: (us[j], j))
+            r = t.opnd[k]
+            if r[0] == "p":
+                t.opnd[k] = ("t", owner[r[3]])
+            else:
+                assert r[0] == "t" and tasks[r[1]].kind == K_LC and tasks[r[1]].u > 1
+                tasks[r[1]].red, tasks[r[1]].u = True, 1
+    used = set()
+    for t in tasks:
+        for r in t.opnd or ():
+            if r[0] == "t":
+                used.add(r[1])
+            elif r[0] == "p":
+                used |= {lr[1] for lr, _ in r[1] if lr[0] == "t"}
+    keep = [t for t in tasks if t.kind != K_LC or t.red or t.id in used]
     # renumber, dependencies
     remap = {t.id: k for k, t in enumerate(keep)}
     for k, t in enumerate(keep):
@@ -546,8 +563,15 @@ def build_lc_tasks(nodes):
         if t.kind == K_LC:
             t.deps = {remap[owner[k[1]]] for k, _ in t.form if k[0] == "n"}
         else:
-            t.opnd = [("t", remap[r[1]]) if r[0] == "t" else r for r in t.opnd]
-            t.deps = {r[1] for r in t.opnd if r[0] == "t"}
+            def rm(r):
+                if r[0] == "t":
+                    return ("t", remap[r[1]])
+                if r[0] == "p":
+                    return ("p", tuple((rm(lr), c) for lr, c in r[1]), r[2], r[3])
+                return r
+            t.opnd = [rm(r) for r in t.opnd]
+            t.deps = {r[1] for r in t.opnd if r[0] == "t"} | \
+                {lr[1] for r in t.opnd if r[0] == "p" for lr, _ in r[1] if lr[0] == "t"}
         for d in t.deps:
             keep[d].users.append(t.id)
     owner2 = {t.out: t.id for t in keep}
@@ -690,6 +714,7 @@ class Macro:
             return ref16(r[1]) if r[0] == "s" else ref16(tasks[r[1]].slot)
         self.records = []
         self.splits = []
+        self.pro = []
         for kind, batch in self.steps:
             recs = []
             split = 0
@@ -708,10 +733,28 @@ class Macro:
                     if not t.red and split and len(l) > split and 1 + form_u(dict(rest)) > t.u:
                         t.red = True       # keep the bound the products were checked with
             self.splits.append(split)
+            pro = kind in (K_P1, K_P2, K_SQ) and any(r[0] == "p" for i in batch for r in tasks[i].opnd)
+            self.pro.append(pro)
             for i in batch:
                 t = tasks[i]
                 dst = ref16(t.slot)
-                if kind in (K_P1, K_P2, K_SQ):
+                if kind in (K_P1, K_P2, K_SQ) and pro:
+                    # [B_a | B_b << 4 | B_c << 8 | B_d << 12, dst, a1, a2, b1, b2, c1, c2,
+                    #  d1, d2, coefs a, b, c, d (two int8 each), 0, 0]: operand =
+                    # C_B + x1 c1 + x2 c2
+                    ops = list(t.opnd)
+                    if nodes[t.out].kind == K_SQ:
+                        ops = ops * 2
+                    ops += [("s", (0, 0))] * (4 - len(ops))
+                    flags, sl, cw = 0, [], []
+                    for k, r in enumerate(ops):
+                        terms = r[1] if r[0] == "p" else ((r, 1),)
+                        terms = list(terms) + [(("s", (0, 0)), 0)] * (2 - len(terms))
+                        flags |= (-sum(c for _, c in terms if c < 0)) << (4 * k)
+                        sl += [ref(lr) for lr, _ in terms]
+                        cw.append((terms[0][1] & 0xff) | (terms[1][1] & 0xff) << 8)
+                    recs.append([flags, dst] + sl + cw + [0, 0])
+                elif kind in (K_P1, K_P2, K_SQ):
                     srcs = [ref(r) for r in t.opnd]
                     if nodes[t.out].kind == K_SQ:
                         srcs = srcs * 2
@@ -840,6 +883,28 @@ def replay(m, consts, args):
                 r = dsl.red_limbs(acc) if red else tuple(acc)
                 res.append(((rec[1] >> 13, rec[1] & 8191), r))
                 continue
+            if kind in (K_P1, K_P2, K_SQ) and len(rec) == 16:
+                ops = []
+                for k in range(4):
+                    b = (rec[0] >> (4 * k)) & 15
+                    cw = rec[10 + k]
+                    cs = [((cw & 0xff) ^ 0x80) - 0x80, ((cw >> 8) ^ 0x80) - 0x80]
+                    acc = list(dsl.SUBC[b]) if b else [0] * 14
+                    plain = cs == [1, 0]      # a bare operand (any bound; the product checks its columns)
+                    for slot, cf in zip(rec[2 + 2 * k:4 + 2 * k], cs):
+                        x = at(slot)
+                        if cf and not plain:
+                            assert max(x) < (1 << 28) and dsl.val_of(x) < 2 * dsl.Q, "pair term beyond F<1>"
+                        acc = [p + cf * q for p, q in zip(acc, x)]
+                    u = form_u({j: c for j, c in enumerate(cs) if c})
+                    assert plain or all(0 <= v <= u * dsl.MASK for v in acc), "prologue limbs beyond F<%d>" % u
+                    ops.append(tuple(acc))
+                if kind == K_SQ:
+                    r = dsl.mont_sop([(ops[0], ops[0])])
+                else:
+                    r = dsl.mont_sop([(ops[0], ops[1]), (ops[2], ops[3])])
+                res.append(((rec[1] >> 13, rec[1] & 8191), r))
+                continue
             hdr, dst, a, b, c, d, o01, o23 = rec
             if kind in (K_P1, K_P2):
                 r = dsl.mont_sop([(at(a), at(b)), (at(c), at(d))])
@@ -918,8 +983,12 @@ def emit(macros, consts, path):
                 for r in rr:
                     r = r + [0] * (8 * R - len(r))
                     recs.extend(r[8 * k:8 * k + 8] for k in range(R))
+            elif kind in (K_P1, K_P2, K_SQ) and m.pro[si]:
+                steps.append((kind | 2 << 16, len(rr), len(recs)))   # 2 record rows: prologue operands
+                for r in rr:
+                    recs.extend([r[0:8], r[8:16]])
             else:
-                steps.append((kind, len(rr), len(recs)))
+                steps.append((kind | 1 << 16, len(rr), len(recs)))
                 recs.extend(rr)
     nslots = max(m.top for m in macros)
     L = ["// GENERATED by tools/pgen/coop.py -- cooperative (one wave per item) macro-operations", "#pragma once",
