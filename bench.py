@@ -59,7 +59,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 16, help="pairings per GPU per step")
     ap.add_argument("--global-batch", type=int, default=0,
-                    help="pairing workload: a fixed global batch split over the ranks (contiguous shards, "
+                    help="a fixed global batch split over the ranks (contiguous shards, every workload but "
+                         "verify; "
                          "pairing_amd/shard.py) instead of --batch per GPU; BASELINE config 5 is "
                          "--gpus 8 --global-batch 1048576")
     ap.add_argument("--stub-echo", action="store_true",
@@ -360,12 +361,23 @@ def main():
     k_ms = {"a": [], "b": [], "c": []}
 
     n_global = n * ws
+    from pairing_amd.shard import gather_rows_to_root, shard_range
+
+    def shard(per_rank):
+        """(n, n_global, rows of the global sequence this rank owns): weak
+        scaling (per_rank rows per rank) or, with --global-batch, the rank's
+        contiguous shard of the fixed global batch -- each rank builds and
+        stages only its own rows"""
+        if args.global_batch:
+            a, b = shard_range(args.global_batch, ws, rank)
+            return b - a, args.global_batch, np.arange(a, b, dtype=np.int64)
+        return per_rank, per_rank * ws, np.arange(rank * per_rank, (rank + 1) * per_rank, dtype=np.int64)
+
     if args.workload == "pairing":
         span = None
         if args.global_batch:
             # config 5 shape: a fixed global batch in contiguous shards, each
             # rank building and staging only its own rows
-            from pairing_amd.shard import shard_range
             span = shard_range(args.global_batch, ws, rank)
             n, n_global = span[1] - span[0], args.global_batch
         p_np, q_np = make_pairs(n, rank, span=span)
@@ -373,7 +385,6 @@ def main():
         q = torch.from_numpy(q_np.view(np.int64)).to(dev)
         out = pdev.empty_records(n, 72, dev)
         scratch = pdev.empty_records(n, 72, dev)
-        from pairing_amd.shard import gather_rows_to_root
 
         def step(timed):
             if timed:
@@ -389,14 +400,15 @@ def main():
                 gather_rows_to_root(out, n_global)
     elif args.workload == "wnaf":
         # config 3: Wnaf::new().base(g, 2^18).scalar(s_i) + G1::batch_normalization
-        n = args.batch if args.batch != (1 << 16) else (1 << 18)
+        n, n_global, idx = shard(args.batch if args.batch != (1 << 16) else (1 << 18))
         d = np.load(os.path.join(ROOT, "tests", "golden", "bench_points.npz"))
         base_np = np.zeros((1, 18), np.uint64)
         base_np[0, :12] = d["g1"][0, :12]
         base_np[0, 12:18] = np.array([0x760900000002fffd, 0xebf4000bc40c0002, 0x5f48985753c758ba,
                                       0x77ce585370525745, 0x5c071a97a256ec6d, 0x15f65ec3fa80e493], np.uint64)
-        s_np = np.ascontiguousarray(d["s1"][np.arange(n) % 256])
-        s_np[:, 0] ^= np.arange(n, dtype=np.uint64) << np.uint64(8)
+        # scalars split over the ranks, every rank its own table (Wnaf::shared(), wnaf.rs:131-154)
+        s_np = np.ascontiguousarray(d["s1"][idx % 256])
+        s_np[:, 0] ^= idx.astype(np.uint64) << np.uint64(8)
         base = torch.from_numpy(base_np.view(np.int64)).to(dev)
         scal = torch.from_numpy(s_np.view(np.int64)).to(dev)
         out = pdev.empty_records(n, 18, dev)
@@ -413,6 +425,8 @@ def main():
             pdev.g1_batch_normalization(out, stream)
             if timed:
                 ev[2].record(stream)
+            if dist_on:
+                gather_rows_to_root(out, n_global)
 
         def comb_parts_ms(reps=3):
             """the GLV table build and the GLV comb multiply as separate
@@ -434,7 +448,8 @@ def main():
     elif args.workload == "decode":
         # SURVEY.md §8 f rank 1: the verifier's front end -- compressed G1 and G2
         # records decoded with the on-curve (square root) and subgroup (r*P) checks
-        p_np, q_np = make_pairs(n, rank)
+        n, n_global, idx = shard(n)
+        p_np, q_np = make_pairs(n, rank, span=(int(idx[0]), int(idx[-1]) + 1) if n else (0, 0))
         enc1_np = pairing_amd.g1_encode(p_np, True)
         enc2_np = pairing_amd.g2_encode(q_np, True)
         enc1 = torch.from_numpy(enc1_np).to(dev)
@@ -453,20 +468,25 @@ def main():
             pdev.decode(1, enc1, True, True, out1, st1, stream)
             if timed:
                 ev[2].record(stream)
+            if dist_on:
+                gather_rows_to_root(out2, n_global)
+                gather_rows_to_root(out1, n_global)
     elif args.workload == "msm":
         # SURVEY.md §8 f rank 3: one G1 multi-scalar multiplication of 2^20 terms
         # (the prover's multiexp).  Distinct bases k_i*G made on the device
         # (fixed-base comb + batch_normalization), random 255-bit scalars.
-        n = args.batch if args.batch != (1 << 16) else (1 << 20)
+        # one MSM over n_global terms: each rank sums its shard's terms, the
+        # root adds one partial sum per rank (shard.sharded_reduce's shape)
+        n, n_global, idx = shard(args.batch if args.batch != (1 << 16) else (1 << 20))
         d = np.load(os.path.join(ROOT, "tests", "golden", "bench_points.npz"))
         base_np = np.zeros((1, 18), np.uint64)
         base_np[0, :12] = d["g1"][0, :12]
         base_np[0, 12:18] = np.array([0x760900000002fffd, 0xebf4000bc40c0002, 0x5f48985753c758ba,
                                       0x77ce585370525745, 0x5c071a97a256ec6d, 0x15f65ec3fa80e493], np.uint64)
-        g = np.random.default_rng(1234 + rank)
+        g = np.random.default_rng(1234 + (0 if args.global_batch else rank))
         k_np = g.integers(0, 1 << 63, size=(n, 4), dtype=np.uint64)
         s_np = g.integers(0, 1 << 63, size=(n, 4), dtype=np.uint64)
-        k_np[:, 0] ^= np.arange(n, dtype=np.uint64)            # distinct k_i
+        k_np[:, 0] ^= idx.astype(np.uint64)                    # distinct k_i
         k_np[:, 3] &= np.uint64(0x0fffffffffffffff)            # < r
         s_np[:, 3] &= np.uint64(0x0fffffffffffffff)
         base = torch.from_numpy(base_np.view(np.int64)).to(dev)
@@ -481,6 +501,9 @@ def main():
         scal = torch.from_numpy(s_np.view(np.int64)).to(dev)
         msm_out = pdev.empty_records(1, 18, dev)
         msm_ws = pdev.multiexp_workspace(1, n, dev)
+        if dist_on:
+            parts = pdev.empty_records(ws, 18, dev) if rank == 0 else None
+            total = pdev.empty_records(1, 18, dev)
         torch.cuda.synchronize()
 
         def step(timed):
@@ -489,6 +512,13 @@ def main():
             pdev.multiexp(1, bases, scal, msm_out, msm_ws, stream)
             if timed:
                 ev[1].record(stream)
+            if dist_on:
+                # the exchange: one Jacobian partial sum (144 B) per rank to the root
+                dist.gather(msm_out, list(parts.split(1)) if rank == 0 else None, dst=0)
+                if rank == 0:
+                    total.copy_(parts[0:1])
+                    for r in range(1, ws):
+                        pdev.group_add(1, total, parts[r:r + 1], total, stream)
     elif args.workload == "verify":
         # SURVEY.md §8 f rank 2, the verifier shape: one multi_pairing over a few
         # pairs (Engine::miller_loop product + final_exponentiation, mod.rs:40-160)
@@ -508,10 +538,10 @@ def main():
             if timed:
                 ev[1].record(stream)
     elif args.workload == "fr_mul":
-        g = np.random.default_rng(rank)
-        n = args.batch if args.batch != (1 << 16) else (1 << 20)
-        a_np = g.integers(0, 1 << 63, size=(4096, 4), dtype=np.uint64)[np.arange(n) % 4096]
-        b_np = g.integers(0, 1 << 63, size=(4096, 4), dtype=np.uint64)[(np.arange(n) * 7 + 3) % 4096]
+        g = np.random.default_rng(0 if args.global_batch else rank)
+        n, n_global, idx = shard(args.batch if args.batch != (1 << 16) else (1 << 20))
+        a_np = g.integers(0, 1 << 63, size=(4096, 4), dtype=np.uint64)[idx % 4096]
+        b_np = g.integers(0, 1 << 63, size=(4096, 4), dtype=np.uint64)[(idx * 7 + 3) % 4096]
         a_np[:, 3] &= np.uint64(0x0fffffffffffffff)
         b_np[:, 3] &= np.uint64(0x0fffffffffffffff)
         a = torch.from_numpy(np.ascontiguousarray(a_np).view(np.int64)).to(dev)
@@ -524,13 +554,15 @@ def main():
             pdev.fr_mul(a, b, out, stream)
             if timed:
                 ev[1].record(stream)
+            if dist_on:
+                gather_rows_to_root(out, n_global)
     else:
-        g = np.random.default_rng(rank)
+        g = np.random.default_rng(0 if args.global_batch else rank)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from helpers import random_fq
-        n = args.batch if args.batch != (1 << 16) else (1 << 20)
-        a_np = random_fq(g, 4096)[np.arange(n) % 4096]
-        b_np = random_fq(g, 4096)[(np.arange(n) * 7 + 3) % 4096]
+        n, n_global, idx = shard(args.batch if args.batch != (1 << 16) else (1 << 20))
+        a_np = random_fq(g, 4096)[idx % 4096]
+        b_np = random_fq(g, 4096)[(idx * 7 + 3) % 4096]
         if args.layout == "soa":
             a = torch.from_numpy(np.ascontiguousarray(a_np.T).view(np.int64)).to(dev)
             b = torch.from_numpy(np.ascontiguousarray(b_np.T).view(np.int64)).to(dev)
@@ -548,6 +580,8 @@ def main():
             mul(a, b, out, stream)
             if timed:
                 ev[1].record(stream)
+            if dist_on and args.layout != "soa":
+                gather_rows_to_root(out, n_global)
 
     for _ in range(args.warmup):
         step(False)
@@ -594,10 +628,10 @@ def main():
             table_ms, mul_ms = comb_parts_ms()
             dom_name, dom_ms, dom_bytes = ("g1_glv_comb_mul", mul_ms, 32 + 144) if mul_ms >= norm_ms else \
                 ("g1_batch_normalize", norm_ms, 144 + 144)
-            value = ws * n * args.steps / elapsed
+            value = n_global * args.steps / elapsed
             metric, unit = "G1 fixed-base scalar mults + batch_normalization per second at batch 2^18", "points/s"
             config = {"workload": "Wnaf::base(g, 2^18).scalar(s_i) then G1::batch_normalization",
-                      "batch_per_gpu": n, "global_batch": n * ws,
+                      "batch_per_gpu": n, "global_batch": n_global,
                       "kernel_ms": {"table+fixed_base_mul (overlapped)": round(tot_ms, 3),
                                     "batch_normalize": round(norm_ms, 3),
                                     "separately: glv table": round(table_ms, 3), "separately: glv mul": round(mul_ms, 3)}}
@@ -605,20 +639,20 @@ def main():
             g2_ms, g1_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
             dom_name, dom_ms, dom_bytes = ("g2_decode_compressed", g2_ms, 96 + 200 + 1) if g2_ms >= g1_ms else \
                 ("g1_decode_compressed", g1_ms, 48 + 104 + 1)
-            value = ws * n * args.steps / elapsed
+            value = n_global * args.steps / elapsed
             metric, unit = "compressed G1+G2 point pairs decoded (checked) per second at batch 2^16", "point pairs/s"
             config = {"workload": "G2Compressed + G1Compressed ::into_affine (sqrt + on-curve + r*P subgroup check)",
-                      "batch_per_gpu": n, "global_batch": n * ws,
+                      "batch_per_gpu": n, "global_batch": n_global,
                       "kernel_ms": {"g2_decode": round(g2_ms, 3), "g1_decode": round(g1_ms, 3)}}
         elif args.workload == "msm":
             dom_name, dom_ms = "g1_multiexp", float(np.mean(k_ms["a"]))
             # per term: W = ceil(257/16) = 17 windows x (104 B base gather + 8 B sort key/value)
             # + 32 B scalar read; the buckets' own traffic is per bucket, not per term
             dom_bytes = 17 * (104 + 8) + 32
-            value = ws * n * args.steps / elapsed
+            value = n_global * args.steps / elapsed
             metric, unit = "G1 multi-scalar multiplication terms per second at n = 2^20", "terms/s"
             config = {"workload": "one G1 MSM sum_i s_i P_i over 2^20 distinct affine bases (Pippenger, c = 16)",
-                      "batch_per_gpu": n, "global_batch": n * ws, "kernel_ms": {"multiexp": round(dom_ms, 3)}}
+                      "batch_per_gpu": n, "global_batch": n_global, "kernel_ms": {"multiexp": round(dom_ms, 3)}}
         elif args.workload == "verify":
             dom_name, dom_ms, dom_bytes = "multi_pairing", float(np.mean(k_ms["a"])), 304 * n + 577
             value = dom_ms
@@ -628,16 +662,19 @@ def main():
                       "batch_per_gpu": n, "global_batch": n * ws, "kernel_ms": {"multi_pairing": round(dom_ms, 3)}}
         elif args.workload == "fr_mul":
             dom_name, dom_ms, dom_bytes = "fr_mul_batch", float(np.mean(k_ms["a"])), 96
-            value = ws * n * args.steps / elapsed
+            value = n_global * args.steps / elapsed
             metric, unit = "Fr::mul_assign per second at batch 2^20", "muls/s"
             config = {"workload": "2^20 Fr Montgomery multiplications (AoS 4x u64)", "batch_per_gpu": n,
-                      "global_batch": n * ws}
+                      "global_batch": n_global}
         else:
             dom_name, dom_ms, dom_bytes = "fq_mul_batch", float(np.mean(k_ms["a"])), 144
-            value = ws * n * args.steps / elapsed
+            value = n_global * args.steps / elapsed
             metric, unit = "Fq::mul_assign per second at batch 2^20", "muls/s"
             config = {"workload": "2^20 Fq Montgomery multiplications (%s 6x u64)" % args.layout.upper(), "batch_per_gpu": n,
-                      "global_batch": n * ws}
+                      "global_batch": n_global}
+        if dist_on and args.workload != "pairing":
+            config["parallelism"] = ("shard%d+partial_sums_to_root" if args.workload == "msm" else
+                                     "replicas%d" if args.workload == "verify" else "shard%d+rccl_gather") % ws
         achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9
         traffic = None
         tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -766,7 +803,7 @@ def main():
                 cpu = cpu_baseline_fq_mul(a_np, b_np, args.cpu_seconds)
         line = {"metric": metric, "value": value, "unit": unit, "n_gpus": ws, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": args.workload != "verify",
-                "scaling": "weak", "vs_baseline": None,
+                "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None,
                 "dtype": "u32 (14 x 28-bit lazy Montgomery limbs)" if args.workload in ("pairing", "verify", "fq_mul")
                 else "u32 (256-bit Montgomery, 8 x u32 limbs)" if args.workload == "fr_mul"
                 else "u32 (14 x 28-bit lazy Montgomery limbs; 12 x u32 normalize)" if args.workload == "wnaf"

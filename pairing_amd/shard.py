@@ -1,4 +1,4 @@
-"""Multi-GPU sharding of a pairing batch.
+"""Multi-GPU sharding of the path's batches.
 
 One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm).
 Pairings are independent, so a global batch is split into contiguous shards,
@@ -7,6 +7,13 @@ single gather of the Fq12 results to the root.  For the trait's multi-pair
 semantics (Engine::miller_loop over all pairs = the product of per-pair
 Miller values, mod.rs:40-102) each rank reduces its shard to one Fq12 and
 the root gathers 576 B per rank.
+
+The other batch shapes shard the same way: an Fq / Fr multiply batch, a
+point-decoding batch and a fixed-base scalar batch (`Wnaf::base(g, n)
+.scalar(s_i)` with the scalars split and every rank holding its own table --
+what `Wnaf::shared()`, wnaf.rs:131-154, exists for) are `sharded_batch_from`
+with a gather of their rows; a multi-scalar multiplication is
+`sharded_reduce`: each rank sums its terms, the root adds one point per rank.
 
 The functions are backend-agnostic (they take the local compute as a
 callable and use torch.distributed collectives), so the same code path runs
@@ -68,16 +75,28 @@ def sharded_batch(p, q, compute, root=0, group=None):
     return sharded_batch_from(lambda a, b: (p[a:b], q[a:b]), p.shape[0], compute, root=root, group=group)
 
 
-def sharded_product(p, q, local_product, combine, root=0, group=None):
-    """The multi-pair Miller loop across ranks: each rank reduces its shard to
-    one Fq12 with `local_product(p_shard, q_shard) -> (1, 72)`, the root
-    gathers one row per rank and folds them with `combine((world, 72)) -> (1, 72)`."""
+def sharded_reduce(load, n, local_reduce, combine, root=0, group=None):
+    """A reduction over a global batch of n items sharded across ranks: each
+    rank stages only its rows, load(start, stop) -> operands, and reduces them
+    to one row, local_reduce(*operands) -> (1, w) tensor; the root gathers one
+    row per rank and folds them, combine((world, w)) -> result.  Returns the
+    result on root, None elsewhere.  Used for the multi-pair Miller loop
+    (sharded_product) and the multi-scalar multiplication (sum of per-rank
+    partial sums)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    a, b = shard_range(p.shape[0], world, rank)
-    local = local_product(p[a:b], q[a:b])
+    a, b = shard_range(n, world, rank)
+    local = local_reduce(*load(a, b))
     rows = [torch.empty_like(local) for _ in range(world)] if rank == root else None
     dist.gather(local.contiguous(), rows, dst=root, group=group)
     if rank != root:
         return None
     return combine(torch.cat(rows, dim=0))
+
+
+def sharded_product(p, q, local_product, combine, root=0, group=None):
+    """The multi-pair Miller loop across ranks: each rank reduces its shard to
+    one Fq12 with `local_product(p_shard, q_shard) -> (1, 72)`, the root
+    gathers one row per rank and folds them with `combine((world, 72)) -> (1, 72)`."""
+    return sharded_reduce(lambda a, b: (p[a:b], q[a:b]), p.shape[0], local_product, combine, root=root,
+                          group=group)

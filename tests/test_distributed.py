@@ -184,3 +184,56 @@ def test_sharded_batch_from_stages_only_the_shard(tmp_path):
     got = np.load(out_path)
     want = (2 * np.arange(n) + 1)[:, None] * np.ones((1, 3), np.int64)
     np.testing.assert_array_equal(got, want)
+
+
+def _worker_other(rank, world, port, n, result_path):
+    """Fq multiply batch, fixed-base scalar batch (scalars split, every rank
+    its own table) and one multi-scalar multiplication (per-rank partial sums
+    folded on the root) over a gloo group, oracle compute per rank."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from oracle import binding as oracle
+    from helpers import random_fq, random_scalars
+    from pairing_amd.shard import sharded_batch_from, sharded_reduce
+
+    g = np.random.default_rng(5)            # the same global batch on every rank
+    a, b = random_fq(g, n), random_fq(g, n)
+    s = random_scalars(g, n)
+    bases = oracle.g1_mul_generator(random_scalars(g, n))
+    base = oracle.g1_mul_generator_jacobian(random_scalars(g, 1))
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64))      # noqa: E731
+    u = lambda x: np.ascontiguousarray(x.numpy()).view(np.uint64)               # noqa: E731
+
+    fq = sharded_batch_from(lambda i, j: (a[i:j], b[i:j]), n, lambda x, y: t(oracle.fq_mul(x, y)))
+    wnaf = sharded_batch_from(lambda i, j: (s[i:j],), n, lambda x: t(oracle.g1_wnaf_fixed_base(base, x)))
+
+    def fold(rows):
+        acc = u(rows[0:1])
+        for r in range(1, rows.shape[0]):
+            acc = oracle.g1_add(acc, u(rows[r:r + 1]))
+        return t(acc)
+    msm = sharded_reduce(lambda i, j: (bases[i:j], s[i:j]), n, lambda p, x: t(oracle.g1_multiexp(p, x)), fold)
+    if rank == 0:
+        np.savez(result_path, fq=fq.numpy(), wnaf=wnaf.numpy(), msm=msm.numpy(), a=a, b=b, s=s, bases=bases,
+                 base=base)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [6, 9])  # even and ragged shards
+def test_sharded_other_batches_world2_gloo(tmp_path, oracle, n):
+    world = 2
+    path = str(tmp_path / "other.npz")
+    mp.spawn(_worker_other, args=(world, _free_port(), n, path), nprocs=world, join=True)
+    r = np.load(path)
+    u = lambda x: np.ascontiguousarray(x).view(np.uint64)                       # noqa: E731
+    np.testing.assert_array_equal(u(r["fq"]), oracle.fq_mul(r["a"], r["b"]))
+    # Wnaf::base(g, count) picks its window from the count (ec.rs:895-921), so a
+    # shard's Jacobian words may differ from the whole batch's: equal as points
+    assert oracle.g1_eq(u(r["wnaf"]), oracle.g1_wnaf_fixed_base(r["base"], r["s"])).all()
+    assert oracle.g1_eq(u(r["msm"]), oracle.g1_multiexp(r["bases"], r["s"])).all()

@@ -72,6 +72,10 @@ for step in "$@"; do
         cooptests) run pytest_coop 600 python -u -m pytest tests/test_gpu_parity.py tests/test_bench_sizes.py -m gpu -k "coop or multi_pairing" -x -v --timeout 200 --timeout-method thread ;;
         coopprof) run coop_prof 120 ./tools/coop_prof ;;
         cooplat) run coop_latency 300 python tools/coop_latency.py ;;
+        distwl) for w in fq_mul fr_mul wnaf decode msm; do
+                    run dist1_$w 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29513 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline || exit 1
+                done
+                run dist1_msm_global 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29514 bench.py --workload msm --global-batch 1000003 --steps 3 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
