@@ -238,7 +238,9 @@ int pa_fq2_sqrt_batch(const pa_fq2 *a, pa_fq2 *out, uint8_t *ok, size_t n);
 int pa_multi_miller_loop_affine(const pa_g1_affine *p, const pa_g2_affine *q, size_t n, pa_fq12 *out);
 int pa_multi_pairing(const pa_g1_affine *p, const pa_g2_affine *q, size_t n, pa_fq12 *out, uint8_t *ok);
 /* pa_pairing_batch split over devices 0..ndev-1 of this process (contiguous
- * shards, one host thread per device); ndev <= pa_device_count. */
+ * shards, one host thread per device); ndev <= pa_device_count.  The
+ * environment variable PA_DEVICE_MAP (a comma list of device ordinals) maps
+ * shard d to its d-th entry instead, e.g. "4,5,6,7"; then ndev <= its length. */
 int pa_pairing_batch_multi_gpu(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n, int ndev);
 
 /* ---- variable-base scalar multiplication and MSM (SURVEY.md §8 f, rank 3) ----

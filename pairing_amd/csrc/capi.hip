@@ -607,7 +607,23 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
 int pa_pairing_batch_multi_gpu(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n, int ndev) {
     int count = 0;
     PA_TRY(hipGetDeviceCount(&count), "hipGetDeviceCount");
-    if (ndev < 1 || ndev > count) return fail(PA_ERR_INVALID_ARGUMENT, "ndev out of range");
+    // shard d runs on device d, or on the d-th entry of PA_DEVICE_MAP (a comma
+    // list of device ordinals, e.g. "2,3,6,7" to use a subset of the node, or
+    // "0,0" to run two shards' workers on one device)
+    std::vector<int> dev_of;
+    if (const char* m = getenv("PA_DEVICE_MAP")) {
+        for (const char* c = m; *c;) {
+            char* end = nullptr;
+            const long v = strtol(c, &end, 10);
+            if (end == c || v < 0 || v >= count) return fail(PA_ERR_INVALID_ARGUMENT, "bad PA_DEVICE_MAP");
+            dev_of.push_back((int)v);
+            c = *end == ',' ? end + 1 : end;
+            if (*end && *end != ',') return fail(PA_ERR_INVALID_ARGUMENT, "bad PA_DEVICE_MAP");
+        }
+    } else {
+        for (int d = 0; d < count; d++) dev_of.push_back(d);
+    }
+    if (ndev < 1 || ndev > (int)dev_of.size()) return fail(PA_ERR_INVALID_ARGUMENT, "ndev out of range");
     if (n == 0) return PA_OK;
     if (!p || !q || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     // contiguous shards (SURVEY.md §8 e); each worker thread owns one device
@@ -618,8 +634,9 @@ int pa_pairing_batch_multi_gpu(const pa_g1_affine* p, const pa_g2_affine* q, pa_
     size_t lo = 0;
     for (int d = 0; d < ndev; d++) {
         const size_t cnt = base + ((size_t)d < extra ? 1 : 0);
+        const int dv = dev_of[d];
         workers.emplace_back([=, &rcs, &errs] {
-            hipError_t e = hipSetDevice(d);
+            hipError_t e = hipSetDevice(dv);
             if (e != hipSuccess) {
                 rcs[d] = fail(hip_code(e), "hipSetDevice", e);
             } else {

@@ -202,6 +202,24 @@ def test_pairing_multi_gpu_entry(gpu, oracle, pairs):
         gpu.pairing_multi_gpu(p, q, gpu.device_count() + 1)
 
 
+@pytest.mark.gpu
+def test_pairing_multi_gpu_workers_over_a_device_map(gpu, oracle, pairs, monkeypatch):
+    """ndev = 2 and 3 worker threads (ragged contiguous shards) mapped onto
+    device 0 by PA_DEVICE_MAP: the multi-device sharding and join logic on a
+    one-GPU box, bit-exact vs the single call"""
+    p, q = pairs
+    want = gpu.pairing(p, q)
+    for m, ndev in (("0,0", 2), ("0,0,0", 3)):
+        monkeypatch.setenv("PA_DEVICE_MAP", m)
+        np.testing.assert_array_equal(gpu.pairing_multi_gpu(p[:-1], q[:-1], ndev), want[:-1])
+    monkeypatch.setenv("PA_DEVICE_MAP", "0,0")
+    with pytest.raises(gpu.PairingError):
+        gpu.pairing_multi_gpu(p, q, 3)
+    monkeypatch.setenv("PA_DEVICE_MAP", "0,x")
+    with pytest.raises(gpu.PairingError):
+        gpu.pairing_multi_gpu(p, q, 1)
+
+
 def test_final_exponentiation_matches_oracle(gpu, oracle, pairs, lanes):
     p, q = pairs
     f = oracle.miller_loop_batch(p[:32], oracle.g2_prepare(q[:32], NT), NT)
