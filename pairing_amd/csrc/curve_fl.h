@@ -125,4 +125,73 @@ PA_DEV void fl_jac_double_3lane(FlJac& p, int lane) {
     p.y = red(sub(mul(e, sub(d, p.x)), dbl(dbl(dbl(c)))));
 }
 
+// ---- four lanes per point (a quad: lanes 4k..4k+3, q = lane & 3) ----
+// One coordinate of quad lane `src` in every lane of the quad (DPP
+// quad_perm broadcast, no LDS).
+template <int SRC>
+PA_DEV F<1> fl_from_quad(const F<1>& x) {
+    F<1> r;
+    constexpr int ctrl = SRC * 0x55;   // quad_perm [SRC, SRC, SRC, SRC]
+#pragma unroll
+    for (int i = 0; i < 14; i++) r.w[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.w[i], ctrl, 0xf, 0xf, false);
+    return r;
+}
+template <int U>
+PA_DEV F<U> pick4(int q, const F<U>& a, const F<U>& b, const F<U>& c, const F<U>& d) {
+    F<U> r;
+#pragma unroll
+    for (int i = 0; i < 14; i++) r.w[i] = q == 0 ? a.w[i] : (q == 1 ? b.w[i] : (q == 2 ? c.w[i] : d.w[i]));
+    return r;
+}
+
+// fl_jac_add (add-2007-bl, ec.rs:421-481) with its sixteen products in five
+// dependent levels over the four lanes of a quad -- the same products of the
+// same operands, so the same field values; every lane of the quad holds both
+// points on entry and the sum on exit.
+PA_DEV void fl_jac_add_q(FlJac& s, const FlJac& o, int q) {
+    if (fl_is_zero(s.z)) {
+        s = o;
+        return;
+    }
+    if (fl_is_zero(o.z)) return;
+    F<1> m = mul(pick4(q, s.z, o.z, s.y, o.y), pick4(q, s.z, o.z, o.z, s.z));
+    const F<1> z1z1 = fl_from_quad<0>(m), z2z2 = fl_from_quad<1>(m), y1z2 = fl_from_quad<2>(m),
+               y2z1 = fl_from_quad<3>(m);
+    m = mul(pick4(q, s.x, o.x, y1z2, y2z1), pick4(q, z2z2, z1z1, z2z2, z1z1));
+    const F<1> u1 = fl_from_quad<0>(m), u2 = fl_from_quad<1>(m), s1 = fl_from_quad<2>(m), s2 = fl_from_quad<3>(m);
+    if (fl_eq(u1, u2) && fl_eq(s1, s2)) {
+        fl_jac_double(s);
+        return;
+    }
+    const F<3> h = sub(u2, u1);
+    const F<1> hh = red(dbl(h));
+    const F<1> r = red(dbl(sub(s2, s1)));
+    const F<2> zs = add(s.z, o.z);
+    m = sqr(pick4(q, relax<2>(hh), relax<2>(r), zs, relax<2>(hh)));
+    const F<1> i = fl_from_quad<0>(m), rr = fl_from_quad<1>(m), zz = fl_from_quad<2>(m);
+    const F<1> zr = red(sub(sub(zz, z1z1), z2z2));
+    m = mul(pick4(q, h, relax<3>(u1), relax<3>(zr), h), pick4(q, relax<3>(i), relax<3>(i), h, relax<3>(i)));
+    const F<1> j = fl_from_quad<0>(m), v = fl_from_quad<1>(m), z3 = fl_from_quad<2>(m);
+    const F<1> x3 = red(sub(sub(sub(rr, j), v), v));
+    m = mul(pick4(q, r, s1, r, s1), pick4(q, relax<3>(sub(v, x3)), relax<3>(j), relax<3>(sub(v, x3)), relax<3>(j)));
+    const F<1> t1 = fl_from_quad<0>(m), t2 = fl_from_quad<1>(m);
+    s.x = x3;
+    s.y = red(sub(t1, dbl(t2)));
+    s.z = z3;
+}
+
+// fl_jac_double_3lane within a quad (lane 3 repeats lane 0's products)
+PA_DEV void fl_jac_double_q(FlJac& p, int q) {
+    F<1> m = mul(q == 1 ? p.y : (q == 2 ? p.y : p.x), q == 1 ? p.y : (q == 2 ? p.z : p.x));
+    const F<1> a = fl_from_quad<0>(m), b = fl_from_quad<1>(m), t = fl_from_quad<2>(m);
+    const F<3> e = add(dbl(a), a);
+    const F<3> s = q == 1 ? relax<3>(add(p.x, b)) : (q == 2 ? e : relax<3>(b));
+    m = sqr(s);
+    const F<1> c = fl_from_quad<0>(m), dd = fl_from_quad<1>(m), f = fl_from_quad<2>(m);
+    const F<1> d = red(dbl(sub(dd, add(a, c))));
+    p.z = red(dbl(t));
+    p.x = red(sub(f, dbl(d)));
+    p.y = red(sub(mul(e, sub(d, p.x)), dbl(dbl(dbl(c)))));
+}
+
 }  // namespace pa

@@ -678,6 +678,29 @@ __global__ void __launch_bounds__(64) k_msm_group_sum(const uint64_t* __restrict
     store_jac(out + (size_t)JW * t, acc);
 }
 
+// k_msm_group_sum<1> on the lazy core, one quad per output (fl_jac_add_q)
+__global__ void __launch_bounds__(64) k_msm_group_sum_fl(const uint64_t* __restrict__ in, uint32_t count,
+                                                         uint32_t group, uint32_t gpw, uint32_t W,
+                                                         uint64_t* __restrict__ out) {
+    constexpr int JW = Grp<1>::JW;
+    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    const int q = threadIdx.x & 3;
+    if (t >= (size_t)W * gpw) return;
+    const size_t w = t / gpw;
+    const uint32_t g = (uint32_t)(t % gpw);
+    FlJac acc;
+    acc.x = fl_zero();
+    acc.y = fl_one();
+    acc.z = fl_zero();
+#pragma unroll 1
+    for (uint32_t k = 0; k < group; k++) {
+        const uint32_t idx = g * group + k;
+        if (idx >= count) break;
+        fl_jac_add_q(acc, fl_load_jac(in + (size_t)JW * (w * count + idx)), q);
+    }
+    if (q == 0) fl_store_jac(out + (size_t)JW * t, acc);
+}
+
 template <int G>
 __global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ wsum, uint32_t W, uint32_t c,
                                                    uint64_t* __restrict__ out) {
@@ -723,6 +746,8 @@ __global__ void __launch_bounds__(64) k_msm_horner_fl(const uint64_t* __restrict
 // k_msm_segments<1> on the lazy core (same sums, same formulas)
 __global__ void __launch_bounds__(64) k_msm_segments_fl(const uint64_t* __restrict__ buckets, uint32_t B, uint32_t L,
                                                         size_t nseg, uint64_t* __restrict__ segs) {
+    // one lane per segment: the kernel is throughput bound (4 k waves); a quad
+    // per segment (fl_jac_add_q) measured 0.57 -> 1.29 ms (profiles/r03_msm_quad_ab.txt)
     constexpr int JW = Grp<1>::JW;
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nseg) return;
@@ -854,8 +879,12 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
             return (uint32_t)(g < 2 ? 2 : (g > 16 ? 16 : g));
         }();
         const uint32_t gpw = (count + group - 1) / group;
-        hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks((size_t)p.W * gpw, 64)), dim3(64), 0, s, src, count,
-                           group, gpw, p.W, dst);
+        if constexpr (G == 1)
+            hipLaunchKernelGGL(k_msm_group_sum_fl, dim3(msm_blocks(4 * (size_t)p.W * gpw, 64)), dim3(64), 0, s, src,
+                               count, group, gpw, p.W, dst);
+        else
+            hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks((size_t)p.W * gpw, 64)), dim3(64), 0, s, src, count,
+                               group, gpw, p.W, dst);
         count = gpw;
         uint64_t* t = src;
         src = dst;

@@ -76,6 +76,14 @@ for step in "$@"; do
                     run dist1_$w 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29513 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline || exit 1
                 done
                 run dist1_msm_global 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29514 bench.py --workload msm --global-batch 1000003 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        verifycpu) run bench_verify_cpu 300 python bench.py --workload verify --steps 10 --warmup 2 ;;
+        allbench) run bench 600 python bench.py &&
+                  run bench_verify_cpu 300 python bench.py --workload verify --steps 10 --warmup 2 &&
+                  run bench_decode 300 python bench.py --workload decode --steps 5 --warmup 1 &&
+                  run bench_msm 400 python bench.py --workload msm --steps 5 --warmup 1 &&
+                  run bench_wnaf 300 python bench.py --workload wnaf --steps 5 --warmup 1 &&
+                  run bench_fq 300 python bench.py --workload fq_mul --steps 20 --warmup 3 &&
+                  run bench_fr 300 python bench.py --workload fr_mul --steps 20 --warmup 3 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
