@@ -54,7 +54,7 @@ for step in "$@"; do
         profwnaf) run prof_wnaf 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_wnaf -o run -- python bench.py --workload wnaf --steps 3 --warmup 1 --no-cpu-baseline ;;
         profdec) run prof_dec 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dec -o run -- python bench.py --workload decode --steps 3 --warmup 1 --no-cpu-baseline ;;
         fqbench) run bench_fq 300 python bench.py --workload fq_mul --steps 20 --warmup 3 --no-cpu-baseline ;;
-        prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
         frbench_nc) run bench_fr 300 python bench.py --workload fr_mul --steps 20 --warmup 3 --no-cpu-baseline ;;
         proffq) run prof_fq 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fq -o run -- python bench.py --workload fq_mul --steps 10 --warmup 2 --no-cpu-baseline ;;
         pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline &&
