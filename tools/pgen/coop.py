@@ -55,7 +55,8 @@ KIND_NAME = ["LIN", "P1", "P2", "SQ", "INV", "LC"]
 # product levels are one LC step instead of a LIN level per chain depth.
 LC = os.environ.get("COOP_CHAINS", "0") != "1"
 LC_TMAX = 15       # terms of one LC task (incl. the zero padding of a split)
-PAIRS = os.environ.get("COOP_PAIRS", "0") == "1"   # measured: +2.5k cycles per product step, a wash
+PAIRS = os.environ.get("COOP_PAIRS", "0") == "1"
+SPLIT_SOP = os.environ.get("COOP_SPLIT_SOP", "1") == "1"   # measured: +2.5k cycles per product step, a wash
 # DSL-level LIN ops
 L_ADD, L_SUB, L_NEG, L_RED = range(4)
 # lane-level chain ops of a LIN task: acc = slot s0, then up to 4 of these
@@ -590,7 +591,20 @@ def schedule(tasks):
             return COST[K_LC] + 25 * len(t.form) + (70 if t.red else 0)
         return COST[K_P2 if t.kind in (K_P1, K_P2, K_SQ) else t.kind] if t.kind != K_LIN else \
             COST[K_LIN] + 25 * len(t.nodes)
-    for t in reversed(tasks):
+    # heights in reverse topological order (task ids need not be topological:
+    # split products are appended after their users)
+    order, indeg = [], {t.id: len(t.deps) for t in tasks}
+    stack = [t.id for t in tasks if not t.deps]
+    while stack:
+        i = stack.pop()
+        order.append(i)
+        for u in tasks[i].users:
+            indeg[u] -= 1
+            if indeg[u] == 0:
+                stack.append(u)
+    assert len(order) == len(tasks), "cycle in the task graph"
+    for i in reversed(order):
+        t = tasks[i]
         t.height = cost(t) + max((tasks[u].height for u in t.users), default=0)
     pending = {t.id: len(t.deps) for t in tasks}
     ready = [t.id for t in tasks if not t.deps]
@@ -707,6 +721,23 @@ class Macro:
         nodes = self.nodes
         self.tasks, owner = build_lc_tasks(nodes)
         self.steps = schedule(self.tasks)
+        if SPLIT_SOP:
+            # a product step whose lanes are mostly plain products runs the
+            # sum-of-products leaf for all of them: split its few a*b + c*d
+            # into two plain products (the sum moves into the consumers' LC
+            # forms) when the lanes allow, then rebuild
+            split = []
+            for kind, batch in self.steps:
+                if kind != K_P2:
+                    continue
+                two = [self.tasks[i].out for i in batch if nodes[self.tasks[i].out].kind == K_P2]
+                if 4 * len(two) <= len(batch) and len(batch) + len(two) <= LANES:
+                    split += two
+            if split:
+                for x in split:
+                    self._split_sop(x)
+                self.tasks, owner = build_lc_tasks(nodes)
+                self.steps = schedule(self.tasks)
         self.top = allocate(nodes, self.tasks, self.steps, scratch0)
         tasks = self.tasks
 
@@ -775,6 +806,25 @@ class Macro:
                         rec += [leaf, c & 0xffff]
                     recs.append(rec)
             self.records.append((kind, recs))
+
+    def _split_sop(self, x):
+        """node x = a*b + c*d -> x = n1 + n2 (LIN) with n1 = a*b, n2 = c*d"""
+        nodes = self.nodes
+        n = nodes[x]
+        a, b, c, d = n.srcs
+        halves = []
+        for srcs in ((a, b), (c, d)):
+            h = Node(len(nodes), K_P1, 0, None, list(srcs))
+            nodes.append(h)
+            for s_ in srcs:
+                if not isinstance(s_, tuple):
+                    us = nodes[s_].users
+                    if x in us:
+                        us.remove(x)
+                    us.append(h.id)
+            h.users = [x]
+            halves.append(h.id)
+        n.kind, n.lop, n.imm, n.srcs = K_LIN, L_ADD, None, halves
 
     def _chain(self, t, src_ref, dst):
         """LIN task -> [nops, dst, s0, s1, s2, s3, ops01, ops23]: acc = s0,
