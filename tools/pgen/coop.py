@@ -55,7 +55,9 @@ KIND_NAME = ["LIN", "P1", "P2", "SQ", "INV", "LC"]
 # product levels are one LC step instead of a LIN level per chain depth.
 LC = os.environ.get("COOP_CHAINS", "0") != "1"
 LC_TMAX = 15       # terms of one LC task (incl. the zero padding of a split)
-PAIRS = os.environ.get("COOP_PAIRS", "0") == "1"
+# macros whose product lanes compute their <= 2-term operands in a prologue
+# (measured: a wash on the Miller-loop macros, -5 % on the cyclotomic square)
+PAIRS = set(os.environ.get("COOP_PAIRS", "cyc").split(","))
 SPLIT_SOP = os.environ.get("COOP_SPLIT_SOP", "1") == "1"   # measured: +2.5k cycles per product step, a wash
 # DSL-level LIN ops
 L_ADD, L_SUB, L_NEG, L_RED = range(4)
@@ -437,7 +439,7 @@ def lc_forms(nodes, mat):
     return form, get
 
 
-def build_lc_tasks(nodes):
+def build_lc_tasks(nodes, pairs=False):
     """Tasks for the LC form: products / inversions as before, and one LC
     task per LIN value that is a product or inversion operand (unless it is a
     bare leaf), a returned value, or materialized because a form using it
@@ -512,7 +514,7 @@ def build_lc_tasks(nodes):
                 (k, c), = f.items()
                 if c == 1:
                     return leafref(k)
-            if pairs_ok and PAIRS and len(f) <= 2 and form_u(f) <= 4:
+            if pairs_ok and pairs and len(f) <= 2 and form_u(f) <= 4:
                 return ("p", tuple((leafref(k), c) for k, c in sorted(f.items())), form_u(f), x)
         return ("t", owner[x])
     for t in tasks:
@@ -719,7 +721,7 @@ class Macro:
         nterms]; B1 / B2 = the sums of the negative coefficients before / after
         the step's split point (C_B added at each segment's start, 0: none)"""
         nodes = self.nodes
-        self.tasks, owner = build_lc_tasks(nodes)
+        self.tasks, owner = build_lc_tasks(nodes, self.name in PAIRS)
         self.steps = schedule(self.tasks)
         if SPLIT_SOP:
             # a product step whose lanes are mostly plain products runs the
@@ -736,7 +738,7 @@ class Macro:
             if split:
                 for x in split:
                     self._split_sop(x)
-                self.tasks, owner = build_lc_tasks(nodes)
+                self.tasks, owner = build_lc_tasks(nodes, self.name in PAIRS)
                 self.steps = schedule(self.tasks)
         self.top = allocate(nodes, self.tasks, self.steps, scratch0)
         tasks = self.tasks
