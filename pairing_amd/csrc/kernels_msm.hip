@@ -467,7 +467,8 @@ __global__ void __launch_bounds__(64) k_msm_chunk_acc(const uint64_t* __restrict
 }
 
 // G1 on the lazy 28-bit core: the affine bases converted once per MSM
-// (x, y -> 28 u32; infinity stays in the ABI record) ...
+// (x, y -> 28 u32; the infinity flag in bit 31 of x's top limb, which is
+// below 2^18, so a bucket item gathers ONE 112-byte record) ...
 __global__ void __launch_bounds__(256) k_msm_bases_fl(const uint64_t* __restrict__ bases, size_t n,
                                                       uint32_t* __restrict__ fl) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -478,7 +479,7 @@ __global__ void __launch_bounds__(256) k_msm_bases_fl(const uint64_t* __restrict
     uint32_t* d = fl + 28 * i;
 #pragma unroll
     for (int k = 0; k < 14; k++) {
-        d[k] = x.w[k];
+        d[k] = x.w[k] | (k == 13 && a.inf ? 0x80000000u : 0u);
         d[14 + k] = y.w[k];
     }
 }
@@ -534,7 +535,6 @@ __global__ void __launch_bounds__(64) k_msm_chunk_acc_fl(const uint64_t* __restr
         inf = true;
         if (kk < sentinel) {
             const uint32_t idx = vv & 0x7fffffffu;
-            inf = (bases[(size_t)Grp<1>::AW * idx + 12] & 0xff) != 0;
             const uint2* src = reinterpret_cast<const uint2*>(basefl + 28 * (size_t)idx);
 #pragma unroll
             for (int q = 0; q < 7; q++) {
@@ -544,6 +544,8 @@ __global__ void __launch_bounds__(64) k_msm_chunk_acc_fl(const uint64_t* __restr
                 y.w[2 * q] = b.x;
                 y.w[2 * q + 1] = b.y;
             }
+            inf = (x.w[13] >> 31) != 0;
+            x.w[13] &= 0x7fffffffu;
         }
     };
     uint32_t key0, v0, key1, v1;
