@@ -128,6 +128,43 @@ def test_coop_schedules_replay_equal_dsl():
     assert sum(len(m.records) for m in macros) < 200
 
 
+def test_coop_lc_schedules_on_edge_values():
+    """the LC (linear-combination) schedules replayed on extreme canonical
+    inputs -- arguments 0, 1, q - 1 ... in Montgomery form and the
+    non-canonical q and 2q - 1, mixed -- with the kernel's u32 limb arithmetic: no limb leaves
+    its F<U> bound, no product column overflows (mont_sop asserts), and the
+    field values equal the DSL macro's"""
+    import random
+    import coop
+    import dsl
+    from dsl import Loop, If
+    assert coop.LC
+    macros, consts = coop.build_all()
+    rng = random.Random(7)
+    # canonical Montgomery forms of edge values, plus non-canonical F<1>
+    # inputs a product can hand on: q itself and 2q - 1 (value bound 2q)
+    edge = [tuple(dsl.to_mont_limbs(v)) for v in (0, 1, dsl.Q - 1, dsl.Q - 2, (dsl.Q - 1) // 2)]
+    edge += [tuple(dsl.gen_fl.limbs(dsl.Q)), tuple(dsl.gen_fl.limbs(2 * dsl.Q - 1))]
+    for m in macros:
+        refs = set()
+
+        def collect(block):
+            for it in block.items:
+                if isinstance(it, (Loop, If)):
+                    collect(it.body)
+                elif it.kind == "arg":
+                    refs.add(it.imm)
+        collect(m.prog.root)
+        for trial in range(3):
+            args = {r: edge[(trial + k) % len(edge)] if trial < 2 else rng.choice(edge)
+                    for k, r in enumerate(sorted(refs))}
+            want = dsl.evaluate(m.prog, args)
+            got = coop.replay(m, consts, args)
+            for k in want:
+                assert dsl.val_of(got[k]) % dsl.Q == dsl.val_of(want[k]) % dsl.Q, (m.name, k)
+                assert max(got[k]) < (1 << 28) and dsl.val_of(got[k]) < 2 * dsl.Q, (m.name, k)
+
+
 # ---- round 2: value bounds, carry normalization, add fusion, subtraction tables ----
 def test_subtraction_tables_dominate_subtrahends():
     """SUBC[(u, v)]: a multiple of q whose limbs 0..12 are >= u (2^28 - 1) and whose
