@@ -77,6 +77,8 @@ std::string lib_dir() {
     return ".";
 }
 
+size_t wave_bytes();
+
 // Loads every code object or none: on a failure the modules already loaded
 // are unloaded and the next launch tries again.
 hipError_t load(GenDevice& d) {
@@ -95,6 +97,29 @@ hipError_t load(GenDevice& d) {
             g_detail = "kernel " + std::string(kName[k]) + " in " + path;
             k++;  // this module did load
             break;
+        }
+        // the code object states its spill slots per wave: one that needs more
+        // workspace than this library allocates (a stale or swapped file,
+        // PA_GEN_DIR) would write past its wave's slice -- refuse it
+        {
+            hipDeviceptr_t gp = nullptr;
+            size_t gb = 0;
+            uint32_t need = 0;
+            const std::string sym = std::string(kName[k]) + "_mem_slots";
+            if ((e = hipModuleGetGlobal(&gp, &gb, d.mod[k], sym.c_str())) != hipSuccess || gb != 4 ||
+                (e = hipMemcpyDtoH(&need, gp, 4)) != hipSuccess) {
+                if (e == hipSuccess) e = hipErrorInvalidImage;
+                g_detail = "workspace size symbol " + sym + " in " + path;
+                k++;
+                break;
+            }
+            if ((size_t)need * kSlotBytes > wave_bytes()) {
+                e = hipErrorInvalidImage;
+                g_detail = path + " needs " + std::to_string(need) + " workspace slots per wave, the library allocates " +
+                           std::to_string(wave_bytes() / kSlotBytes) + " (rebuild, or PA_GEN_WS_SLOTS)";
+                k++;
+                break;
+            }
         }
     }
     if (e != hipSuccess) {

@@ -115,7 +115,8 @@ def build(which, outdir):
     prog, cfg, kname, nmem, code, em = f.cache["r"]
     import emit
     asm = render.kernel_asm(kname, code, em.lds_bytes, lanes=prog.lanes,
-                            nvgpr=256 if prog.lanes == 1 else min(256, -(-(emit.VSLOT0 + 14 * em.NV) // 4) * 4))
+                            nvgpr=256 if prog.lanes == 1 else min(256, -(-(emit.VSLOT0 + 14 * em.NV) // 4) * 4),
+                            mem_slots=nmem)
     out = os.path.join(outdir, FILES[which])
     os.makedirs(os.path.dirname(out), exist_ok=True)
     render.assemble(asm, out, os.path.join(ROOT, "build", "pgen"))

@@ -134,7 +134,10 @@ class Renderer:
         return out
 
 
-def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256):
+def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256, mem_slots=None):
+    """mem_slots: the HBM spill slots per wave the code uses, exported as the
+    global `<name>_mem_slots` so the loader (gen_launch.hip) can refuse a code
+    object that needs a larger workspace than the library allocates"""
     body = Renderer(code).text()
     args = "\n".join(
         "      - .offset: %d\n        .size: 8\n        .value_kind: %s%s" % (
@@ -150,7 +153,7 @@ def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256):
 {body}
 .Lfunc_end_{name}:
 \t.size {name}, .Lfunc_end_{name}-{name}
-
+{memsym}
 \t.rodata
 \t.p2align 6
 \t.amdhsa_kernel {name}
@@ -189,6 +192,9 @@ amdhsa.kernels:
 ...
 \t.end_amdgpu_metadata
 """.format(name=name, body="\n".join(body), lds=lds_bytes, kb=8 * nargs, args=args,
+           memsym="" if mem_slots is None else
+           "\n\t.rodata\n\t.globl {n}_mem_slots\n\t.p2align 2\n\t.type {n}_mem_slots,@object\n"
+           "{n}_mem_slots:\n\t.long {m}\n\t.size {n}_mem_slots, 4\n".format(n=name, m=int(mem_slots)),
            nfree=512 if lanes == 1 else 256, aoff=nvgpr, nagpr=(512 if lanes == 1 else 256) - nvgpr)
 
 
