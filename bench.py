@@ -50,6 +50,8 @@ G1A_BYTES, G2A_BYTES = 104, 200  # ABI records (coordinates + infinity flag + pa
 # algorithmic HBM bytes per pairing, per kernel (DESIGN.md "Roofline")
 ML_BYTES = 96 + 192 + 2 + FQ12_BYTES   # P, Q coordinates + flags in, f out
 FE_BYTES = FQ12_BYTES + FQ12_BYTES     # f in, e(P,Q) out
+G2P_BYTES = 68 * 3 * 96 + 8            # G2Prepared record: 68 (Fq2, Fq2, Fq2) lines + infinity word
+ML_PREP_BYTES = G1A_BYTES + G2P_BYTES + FQ12_BYTES
 
 
 def parse():
@@ -66,7 +68,7 @@ def parse():
     ap.add_argument("--stub-echo", action="store_true",
                     help="with --cpu-stub: each rank echoes its shard instead of computing pairings "
                          "(plumbing test of large shapes)")
-    ap.add_argument("--workload", choices=["pairing", "fq_mul", "fr_mul", "wnaf", "decode", "msm", "verify"],
+    ap.add_argument("--workload", choices=["pairing", "prepared", "fq_mul", "fr_mul", "wnaf", "decode", "msm", "verify"],
                     default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -177,6 +179,32 @@ def cpu_baseline_pairing(p, q, seconds):
                       "host affinity %d cores%s" % (n1, w1, nt, threads, wt, host,
                                                     ", OMP_NUM_THREADS=%s" % os.environ["OMP_NUM_THREADS"]
                                                     if os.environ.get("OMP_NUM_THREADS") else "")}
+
+
+def cpu_baseline_prepared(p, q, seconds):
+    """The oracle's miller_loop over materialized G2Prepared + final
+    exponentiation (the prepare itself outside the timing, as on the GPU),
+    one core then every thread, over a prefix of the same batch"""
+    from oracle import binding as oracle
+    host, threads = host_threads()
+    res = []
+    for th in sorted({1, threads}):
+        k = 2 * th
+        t0 = time.perf_counter()
+        oracle.final_exponentiation(oracle.miller_loop_batch(p[:k], oracle.g2_prepare(q[:k], th), th), th)
+        per = max(time.perf_counter() - t0, 1e-4) / k
+        m = int(max(k, min(len(p), max(5.0, seconds / 2) / per)))
+        prep = oracle.g2_prepare(q[:m], th)
+        t0 = time.perf_counter()
+        oracle.final_exponentiation(oracle.miller_loop_batch(p[:m], prep, th), th)
+        wall = time.perf_counter() - t0
+        res.append((th, m / wall, m, wall))
+    v1 = res[0][1]
+    th, vt, mt, wt = res[-1]
+    return {"value": vt, "unit": "pairings/s", "cores": th, "kind": "port", "host_cores": host, "value_1core": v1,
+            "sample": "C restatement of the reference (oracle/): miller_loop_batch over prepared records + "
+                      "final_exponentiation, %d pairs on 1 core in %.1f s; %d pairs on %d threads in %.1f s"
+                      % (res[0][2], res[0][3], mt, th, wt)}
 
 
 def cpu_baseline_decode(enc1, enc2, seconds):
@@ -398,6 +426,41 @@ def main():
             if dist_on:
                 # the path's one exchange: every shard's Fq12 results to rank 0 (RCCL over xGMI)
                 gather_rows_to_root(out, n_global)
+    elif args.workload == "prepared":
+        # the north-star's own call shape: Bls12::miller_loop over (G1Affine,
+        # G2Prepared) pairs + final_exponentiation, the G2Prepared records (68
+        # line coefficients each, 19 592 B) materialized in HBM once before the
+        # timed region (G2Affine::prepare, timed separately below)
+        from pairing_amd._native import W_G2P
+        span = shard_range(args.global_batch, ws, rank) if args.global_batch else None
+        if span:
+            n, n_global = span[1] - span[0], args.global_batch
+        p_np, q_np = make_pairs(n, rank, span=span)
+        p = torch.from_numpy(p_np.view(np.int64)).to(dev)
+        q = torch.from_numpy(q_np.view(np.int64)).to(dev)
+        qp = pdev.empty_records(n, W_G2P, dev)
+        out = pdev.empty_records(n, 72, dev)
+        scratch = pdev.empty_records(n, 72, dev)
+        prep_ms = []
+        for _ in range(3):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            e[0].record(stream)
+            pdev.g2_prepare(q, qp, stream)
+            e[1].record(stream)
+            torch.cuda.synchronize()
+            prep_ms.append(e[0].elapsed_time(e[1]))
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            pdev.miller_loop_prepared(p, qp, scratch, stream)
+            if timed:
+                ev[1].record(stream)
+            pdev.final_exponentiation(scratch, out, None, stream)
+            if timed:
+                ev[2].record(stream)
+            if dist_on:
+                gather_rows_to_root(out, n_global)
     elif args.workload == "wnaf":
         # config 3: Wnaf::new().base(g, 2^18).scalar(s_i) + G1::batch_normalization
         n, n_global, idx = shard(args.batch if args.batch != (1 << 16) else (1 << 18))
@@ -597,7 +660,7 @@ def main():
     elapsed = time.perf_counter() - t0
     for e in step_ev:
         k_ms["a"].append(e[0].elapsed_time(e[1]))
-        if args.workload in ("pairing", "wnaf", "decode"):
+        if args.workload in ("pairing", "prepared", "wnaf", "decode"):
             k_ms["b"].append(e[1].elapsed_time(e[2]))
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -623,6 +686,20 @@ def main():
                       "batch_per_gpu": n, "global_batch": n_global, "parallelism": "shard%d+rccl_gather" % ws
                       if dist_on else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}
+        elif args.workload == "prepared":
+            ml = float(np.mean(k_ms["a"]))
+            fe = float(np.mean(k_ms["b"]))
+            dom_name, dom_ms, dom_bytes = ("final_exponentiation", fe, FE_BYTES) if fe >= ml else \
+                ("miller_loop_prepared", ml, ML_PREP_BYTES)
+            value = n_global * args.steps / elapsed
+            metric, unit = "BLS12-381 miller_loop(G1Affine, G2Prepared) + final_exponentiation per second " \
+                           "at batch 2^16", "pairings/s"
+            config = {"workload": "bls12_381 final_exponentiation(miller_loop([(P_i, Q_i.prepare())])) batch, "
+                                  "G2Prepared materialized in HBM (19 592 B per pair)",
+                      "batch_per_gpu": n, "global_batch": n_global,
+                      "parallelism": "shard%d+rccl_gather" % ws if dist_on else "single",
+                      "kernel_ms": {"miller_loop_prepared": round(ml, 3), "final_exponentiation": round(fe, 3),
+                                    "untimed: g2_prepare": round(float(np.median(prep_ms)), 3)}}
         elif args.workload == "wnaf":
             tot_ms, norm_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
             table_ms, mul_ms = comb_parts_ms()
@@ -672,7 +749,7 @@ def main():
             metric, unit = "Fq::mul_assign per second at batch 2^20", "muls/s"
             config = {"workload": "2^20 Fq Montgomery multiplications (%s 6x u64)" % args.layout.upper(), "batch_per_gpu": n,
                       "global_batch": n_global}
-        if dist_on and args.workload != "pairing":
+        if dist_on and args.workload not in ("pairing", "prepared"):
             config["parallelism"] = ("shard%d+partial_sums_to_root" if args.workload == "msm" else
                                      "replicas%d" if args.workload == "verify" else "shard%d+rccl_gather") % ws
         achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9
@@ -682,7 +759,7 @@ def main():
             with open(tr_path) as f:
                 # the split final exponentiation has its own entry (the three
                 # kernels' bytes per step); null until measured
-                fe_split = args.workload == "pairing" and dom_name == "final_exponentiation" and \
+                fe_split = args.workload in ("pairing", "prepared") and dom_name == "final_exponentiation" and \
                     os.environ.get("PA_FE_SPLIT", "0") == "1"
                 traffic = json.load(f).get(dom_name + ("_split" if fe_split else ""))
         roof = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
@@ -696,7 +773,8 @@ def main():
             roof["copy_GBs"] = round(copy_gbs, 1)
             roof["frac_of_copy"] = achieved / copy_gbs
         work_path = os.path.join(ROOT, "pairing_amd", "lib", "pa_gen_work.json")
-        if args.workload == "pairing" and os.path.exists(work_path):
+        if (args.workload == "pairing" or (args.workload == "prepared" and dom_name == "final_exponentiation")) \
+                and os.path.exists(work_path):
             # the pairing kernels are VALU-issue bound (multiply-accumulate
             # chains), not HBM bound: report that roofline, with the HBM view
             # kept alongside
@@ -781,6 +859,8 @@ def main():
         if not args.no_cpu_baseline and ws == 1:
             if args.workload == "pairing":
                 cpu = cpu_baseline_pairing(p_np, q_np, args.cpu_seconds)
+            elif args.workload == "prepared":
+                cpu = cpu_baseline_prepared(p_np, q_np, args.cpu_seconds)
             elif args.workload == "wnaf":
                 cpu = cpu_baseline_wnaf(base_np, s_np, args.cpu_seconds)
             elif args.workload == "decode":
@@ -804,7 +884,8 @@ def main():
         line = {"metric": metric, "value": value, "unit": unit, "n_gpus": ws, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": args.workload != "verify",
                 "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None,
-                "dtype": "u32 (14 x 28-bit lazy Montgomery limbs)" if args.workload in ("pairing", "verify", "fq_mul")
+                "dtype": "u32 (14 x 28-bit lazy Montgomery limbs)"
+                if args.workload in ("pairing", "prepared", "verify", "fq_mul")
                 else "u32 (256-bit Montgomery, 8 x u32 limbs)" if args.workload == "fr_mul"
                 else "u32 (14 x 28-bit lazy Montgomery limbs; 12 x u32 normalize)" if args.workload == "wnaf"
                 else "u32 (384-bit Montgomery, 12 x u32 limbs)",

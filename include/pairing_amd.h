@@ -350,6 +350,13 @@ int pa_final_exponentiation_batch_device(const pa_fq12 *in, pa_fq12 *out, uint8_
  * pa_fq12 (the per-pair Miller values, reduced in place to their product) */
 int pa_multi_pairing_device(const pa_g1_affine *p, const pa_g2_affine *q, size_t n, pa_fq12 *out, uint8_t *ok,
                             pa_fq12 *work, void *stream);
+/* G2Prepared::from_affine (mod.rs:168-358) and miller_loop over (G1Affine,
+ * G2Prepared) pairs (mod.rs:40-102) on device records: the north-star form
+ * whose line coefficients are materialized in HBM (19 592 B per point).
+ * Same records and bits as pa_g2_prepare_batch / pa_miller_loop_batch. */
+int pa_g2_prepare_batch_device(const pa_g2_affine *q, pa_g2_prepared *out, size_t n, void *stream);
+int pa_miller_loop_batch_device(const pa_g1_affine *p, const pa_g2_prepared *q, pa_fq12 *out, size_t n,
+                                void *stream);
 /* e(p[i], q[i]); `scratch` must hold n pa_fq12 (the Miller-loop values) */
 int pa_pairing_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, pa_fq12 *scratch,
                             size_t n, void *stream);

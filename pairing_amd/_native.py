@@ -104,6 +104,8 @@ _SIGS = {
     "pa_fq_mul_batch_device": [_P, _P, _P, _N, _P],
     "pa_fq_mul_batch_soa_device": [_P, _P, _P, _N, _P],
     "pa_miller_loop_fused_batch_device": [_P, _P, _P, _N, _P],
+    "pa_g2_prepare_batch_device": [_P, _P, _N, _P],
+    "pa_miller_loop_batch_device": [_P, _P, _P, _N, _P],
     "pa_final_exponentiation_batch_device": [_P, _P, _P, _N, _P],
     "pa_pairing_batch_device": [_P, _P, _P, _P, _N, _P],
     "pa_g1_decode_batch": [_P, _N, ctypes.c_int, ctypes.c_int, _P, _P],

@@ -872,6 +872,19 @@ int pa_final_exponentiation_batch_device(const pa_fq12* in, pa_fq12* out, uint8_
     PA_TRY(fe_launch((const uint64_t*)in, (uint64_t*)out, ok, n, (hipStream_t)stream), "kernel launch");
     return PA_OK;
 }
+int pa_g2_prepare_batch_device(const pa_g2_affine* q, pa_g2_prepared* out, size_t n, void* stream) {
+    if (n && (!q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_g2_prepare((const uint64_t*)q, (uint64_t*)out, n, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
+int pa_miller_loop_batch_device(const pa_g1_affine* p, const pa_g2_prepared* q, pa_fq12* out, size_t n,
+                                void* stream) {
+    if (n && (!p || !q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_miller_loop_prepared((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n,
+                                           (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
 int pa_pairing_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, pa_fq12* scratch,
                             size_t n, void* stream) {
     if (n && (!p || !q || !out || !scratch)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");

@@ -1,6 +1,6 @@
-// Materialized-G2Prepared pairing kernels, one pairing per lane (the
-// fused Miller loop and final exponentiation of the hot path are the
-// generated code objects of tools/pgen, gen_launch.hip).
+// Materialized-G2Prepared pairing kernels, one pairing per lane on the lazy
+// 28-bit core (pairing_fl.h; the fused Miller loop and final exponentiation
+// of the hot path are the generated code objects of tools/pgen, gen_launch.hip).
 //
 //   k_g2_prepare             G2Prepared::from_affine  (mod.rs:168-358)
 //   k_miller_loop_prepared   miller_loop([(p, q_prepared)])  (mod.rs:40-102)
@@ -8,7 +8,7 @@
 //
 // HBM records use the reference's in-memory order (include/pairing_amd.h).
 #include "launch.h"
-#include "pairing.h"
+#include "pairing_fl.h"
 
 namespace pa {
 
@@ -16,80 +16,62 @@ constexpr int kAffG1Words = 13;  // {x, y, infinity+pad}
 constexpr int kAffG2Words = 25;
 constexpr int kPreparedWords = kNumCoeffs * 36 + 1;
 
+// G2Prepared::from_affine on the lazy core: 63 doubling + 5 addition steps,
+// each line stored canonical as it is produced.
 __global__ void __launch_bounds__(64) k_g2_prepare(const uint64_t* __restrict__ q_aff,
                                                    uint64_t* __restrict__ prepared, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Aff<Fq2> q;
-    load_aff(q, q_aff + kAffG2Words * i);
+    const uint64_t* src = q_aff + kAffG2Words * i;
+    const bool qinf = (src[24] & 0xff) != 0;
+    const F2<1> qx = load2(src), qy = load2(src + 12);
     uint64_t* dst = prepared + kPreparedWords * i;
-    Jac<Fq2> r;
-    r.x = q.x;
-    r.y = q.y;
-    one(r.z);
-    EllCoeff c;
+    G2JacFl r{qx, qy, f2_one()};
     int k = 0;
 #pragma unroll 1
     for (int bit = 61; bit >= 0; bit--) {
-        doubling_step(c, r);
-        store8(dst + 36 * k, c.c0); store8(dst + 36 * k + 12, c.c1); store8(dst + 36 * k + 24, c.c2);
-        k++;
-        if (((kBlsX >> 1) >> bit) & 1) {
-            addition_step(c, r, q.x, q.y);
-            store8(dst + 36 * k, c.c0); store8(dst + 36 * k + 12, c.c1); store8(dst + 36 * k + 24, c.c2);
-            k++;
-        }
+        store_line(dst + 36 * k++, dbl_step_fl(r));
+        if (((kBlsX >> 1) >> bit) & 1) store_line(dst + 36 * k++, add_step_fl(r, qx, qy));
     }
-    doubling_step(c, r);
-    store8(dst + 36 * k, c.c0); store8(dst + 36 * k + 12, c.c1); store8(dst + 36 * k + 24, c.c2);
-    if (q.inf) {
+    store_line(dst + 36 * k, dbl_step_fl(r));
+    if (qinf) {
         // reference: coeffs = vec![], infinity = true (mod.rs:169-174)
         for (int w = 0; w < kNumCoeffs * 36; w++) dst[w] = 0;
     }
-    dst[kNumCoeffs * 36] = q.inf ? 1ull : 0ull;
+    dst[kNumCoeffs * 36] = qinf ? 1ull : 0ull;
 }
 
+// miller_loop over one (G1Affine, G2Prepared) pair per lane on the lazy core
 __global__ void __launch_bounds__(64) k_miller_loop_prepared(const uint64_t* __restrict__ p_aff,
                                                              const uint64_t* __restrict__ prepared,
                                                              uint64_t* __restrict__ out, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Aff<Fq> p;
-    load_aff(p, p_aff + kAffG1Words * i);
+    const uint64_t* pp = p_aff + kAffG1Words * i;
+    const bool pinf = (pp[12] & 0xff) != 0;
+    const F<1> kx = mul(fl_load(pp), fl_c(FL_TO));
+    const F<1> ky = mul(fl_load(pp + 6), fl_c(FL_TO));
     const uint64_t* src = prepared + kPreparedWords * i;
     const bool qinf = (src[kNumCoeffs * 36] & 0xff) != 0;
-    Fq12 f;
-    one(f);
-    EllCoeff c;
+    F12<1> f = f12_one();
     int k = 0;
 #pragma unroll 1
     for (int bit = 61; bit >= 0; bit--) {
-        load8(c.c0, src + 36 * k); load8(c.c1, src + 36 * k + 12); load8(c.c2, src + 36 * k + 24);
-        k++;
-        ell(f, c, p.x, p.y);
-        if (((kBlsX >> 1) >> bit) & 1) {
-            load8(c.c0, src + 36 * k); load8(c.c1, src + 36 * k + 12); load8(c.c2, src + 36 * k + 24);
-            k++;
-            ell(f, c, p.x, p.y);
-        }
-        sqr(f, f);
+        f = ell_fl(f, src + 36 * k++, kx, ky);
+        if (((kBlsX >> 1) >> bit) & 1) f = ell_fl(f, src + 36 * k++, kx, ky);
+        f = sqr(f);
     }
-    load8(c.c0, src + 36 * k); load8(c.c1, src + 36 * k + 12); load8(c.c2, src + 36 * k + 24);
-    ell(f, c, p.x, p.y);
-    conjugate(f, f);
-    if (p.inf || qinf) one(f);
-    store(out + 72 * i, f);
+    f = ell_fl(f, src + 36 * k, kx, ky);
+    f = red(conj(f));
+    if (pinf || qinf) f = f12_one();
+    store12(out + 72 * i, f);
 }
 
 // one tree level: work[i] *= work[i + half] for i < cnt - half
 __global__ void __launch_bounds__(64) k_fq12_product_level(uint64_t* __restrict__ work, size_t cnt, size_t half) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= half || i + half >= cnt) return;
-    Fq12 x, y;
-    load(x, work + 72 * i);
-    load(y, work + 72 * (i + half));
-    mul(x, x, y);
-    store(work + 72 * i, x);
+    store12(work + 72 * i, mul(load12(work + 72 * i), load12(work + 72 * (i + half))));
 }
 
 static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }

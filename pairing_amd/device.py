@@ -9,7 +9,7 @@ import ctypes
 
 import torch
 
-from ._native import W_FQ, W_FQ12, W_G1, W_G1A, W_G2, W_G2A, _lib, call
+from ._native import W_FQ, W_FQ12, W_G1, W_G1A, W_G2, W_G2A, W_G2P, _lib, call
 
 
 def _stream_ptr(stream):
@@ -85,6 +85,23 @@ def miller_loop(p, q, out, stream=None):
     _rows(q, n, "q")
     _rows(out, n, "out")
     call("pa_miller_loop_fused_batch_device", *args, n, _stream_ptr(stream))
+
+
+def g2_prepare(q, out, stream=None):
+    """G2Prepared::from_affine over a batch (mod.rs:168-358): out (n, W_G2P) int64 records."""
+    n = q.shape[0]
+    args = (_dptr(q, W_G2A, "q"), _dptr(out, W_G2P, "out"))
+    _rows(out, n, "out")
+    call("pa_g2_prepare_batch_device", *args, n, _stream_ptr(stream))
+
+
+def miller_loop_prepared(p, qp, out, stream=None):
+    """out[i] = miller_loop([(p[i], qp[i])]) over materialized G2Prepared records (mod.rs:40-102)."""
+    n = p.shape[0]
+    args = (_dptr(p, W_G1A, "p"), _dptr(qp, W_G2P, "qp"), _dptr(out, W_FQ12, "out"))
+    _rows(qp, n, "qp")
+    _rows(out, n, "out")
+    call("pa_miller_loop_batch_device", *args, n, _stream_ptr(stream))
 
 
 def final_exponentiation(f, out, ok=None, stream=None):

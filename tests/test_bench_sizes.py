@@ -183,6 +183,36 @@ def test_pairing_host_pipeline_pieces_with_empty_last_piece(oracle):
     np.testing.assert_array_equal(got, oracle.pairing(p, q, _threads()))
 
 
+@pytest.mark.parametrize("n", [1 << 16, 333])
+def test_prepared_path_device_bit_exact_at_bench_size(gpu, oracle, n):
+    """bench.py --workload prepared: pa_g2_prepare_batch_device writes the
+    reference's G2Prepared records (68 line coefficients, mod.rs:168-358) and
+    pa_miller_loop_batch_device + the final exponentiation over them give
+    e(P, Q) (mod.rs:40-160), bit for bit; some Q at infinity (empty coeffs +
+    flag, mod.rs:169-174) besides bench.make_pairs' infinite P"""
+    import torch
+    import bench
+    import pairing_amd.device as pdev
+    from pairing_amd._native import W_G2P
+    p_np, q_np = bench.make_pairs(n, 0, seed=11)
+    qinf = np.arange(n)[np.arange(n) % 97 == 3]
+    q_np[qinf, :24] = 0
+    q_np[qinf, 12:18] = limbs(pow(2, 384, Q))
+    q_np[qinf, 24] = 1
+    dq = _dev(q_np)
+    prep = pdev.empty_records(n, W_G2P, "cuda:0")
+    pdev.g2_prepare(dq, prep)
+    f = pdev.empty_records(n, 72, "cuda:0")
+    out = pdev.empty_records(n, 72, "cuda:0")
+    pdev.miller_loop_prepared(_dev(p_np), prep, f)
+    pdev.final_exponentiation(f, out)
+    torch.cuda.synchronize()
+    exp_prep = oracle.g2_prepare(q_np, _threads())
+    np.testing.assert_array_equal(_host(prep), exp_prep)
+    np.testing.assert_array_equal(_host(f), oracle.miller_loop_batch(p_np, exp_prep, _threads()))
+    np.testing.assert_array_equal(_host(out), oracle.pairing(p_np, q_np, _threads()))
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 5])
 def test_multi_pairing_device_matches_oracle(gpu, oracle, n):
     """bench.py --workload verify: pa_multi_pairing_device (cooperative Miller
