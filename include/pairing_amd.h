@@ -87,12 +87,16 @@ int pa_synchronize(void);
  *   1 = generated kernels with a lane pair per pairing, every size (A/B)
  *   2 = cooperative kernels for every size (A/B, tests)
  *   3 = generated one-pairing-per-lane kernels for every size (A/B, tests)
+ *   4 = cooperative kernels for every size on the round-2 one-wave VM
+ *       (A/B, tests; added in round 3 -- 0 and 2 now run batches of up to
+ *       PA_COOP_QUAD_MAX items on the four-wave quad VM, same results)
  * Process-wide; not part of the reference interface.
  * Behavior change in round 2: the numbering was 0 = hipcc lazy core,
  * 1 / 2 = hipcc 32-bit word kernels (one lane / two lanes), 3 = generated,
  * 4 / 5 = generated lane pairs / lazy reduction.  Those kernels are gone; the
- * values above now mean what is listed and 4, 5 (and anything else outside
- * 0..3) return PA_ERR_INVALID_ARGUMENT. */
+ * values above now mean what is listed and anything outside 0..4 returns
+ * PA_ERR_INVALID_ARGUMENT (4 was "lazy reduction" before round 2 and is the
+ * one-wave cooperative VM since round 3). */
 int pa_set_pairing_kernel(int variant);
 
 /* ---- Fq (src/bls12_381/fq.rs, Field trait src/lib.rs:267-325) ---- */

@@ -25,7 +25,8 @@ thread_local std::string g_last_error;
 // pairing (the generated kernels), with batches of at most coop_max() pairs
 // on the cooperative one-wave-per-pairing kernels (kernels_coop.hip, ~1/10
 // of the latency); 1 -> lane pairs; 2 -> cooperative for every batch size;
-// 3 -> one lane per pairing for every batch size.
+// 3 -> one lane per pairing for every batch size; 4 -> cooperative for every
+// batch size on the round-2 one-wave VM (A/B against the quad VM).
 int g_pairing_variant = 0;
 
 size_t coop_max() {
@@ -35,14 +36,17 @@ size_t coop_max() {
     }();
     return v;
 }
-bool use_coop(size_t n) { return g_pairing_variant == 2 || (g_pairing_variant == 0 && n <= coop_max()); }
+bool use_coop(size_t n) {
+    return g_pairing_variant == 2 || g_pairing_variant == 4 || (g_pairing_variant == 0 && n <= coop_max());
+}
+int coop_vm() { return g_pairing_variant == 4 ? 1 : 0; }
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
-    if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s);
+    if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s, coop_vm());
     return pa::launch_miller_loop_gen(g_pairing_variant == 1 ? 2 : 1, p, q, out, n, s);
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
-    if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s);
+    if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s, coop_vm());
     return pa::launch_final_exp_gen(g_pairing_variant == 1 ? 2 : 1, in, out, ok, n, s);
 }
 
@@ -273,7 +277,7 @@ int pa_set_device(int device) {
     return PA_OK;
 }
 int pa_set_pairing_kernel(int variant) {
-    if (variant < 0 || variant > 3) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..3");
+    if (variant < 0 || variant > 4) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..4");
     g_pairing_variant = variant;
     return PA_OK;
 }

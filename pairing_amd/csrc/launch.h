@@ -81,12 +81,15 @@ hipError_t launch_miller_loop_gen(int lanes, const uint64_t* p_aff, const uint64
 hipError_t launch_fq_inv_strided(uint64_t* v, size_t stride, size_t n, hipStream_t stream);
 hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
                                 hipStream_t stream);
-// Cooperative kernels (kernels_coop.hip): one WAVE per pairing, for small
+// Cooperative kernels (kernels_coop.hip): a workgroup per pairing, for small
 // batches -- miller_loop with fused prepare / final_exponentiation, same
-// results as the one-lane kernels at ~1/10 of their latency
+// results as the one-lane kernels at a fraction of their latency.  vm: 0 =
+// by batch size (the four-wave quad VM up to PA_COOP_QUAD_MAX items, else the
+// one-wave VM; PA_COOP_VM=1 / 4 overrides), 1 = one-wave VM, 4 = quad VM
 hipError_t launch_coop_miller_loop(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                   hipStream_t stream);
-hipError_t launch_coop_final_exp(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream);
+                                   hipStream_t stream, int vm = 0);
+hipError_t launch_coop_final_exp(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream,
+                                 int vm = 0);
 // out[0] = prod_i in[i] (Fq12), in-place tree reduction over `work` (n entries, clobbered)
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
 

@@ -52,3 +52,30 @@ def launch(name, a0, a1, a2, n, ws_slots=1):
         torch.cuda.synchronize()
     finally:
         hip.hipModuleUnload(mod)
+
+
+def launch_kernel(path, name, args, grid, block):
+    """run extern "C" kernel `name` of the code object at `path` with args =
+    [(ctypes type, value), ...] packed as its kernel-argument struct"""
+    import torch
+    hip = _hip()
+    mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+    if not os.path.exists(path):
+        raise FileNotFoundError(path)
+    assert hip.hipModuleLoad(ctypes.byref(mod), path.encode()) == 0, "hipModuleLoad " + path
+    try:
+        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, name.encode()) == 0, name
+
+        class Args(ctypes.Structure):
+            _fields_ = [("a%d" % i, t) for i, (t, _) in enumerate(args)]
+        packed = Args(*[v for _, v in args])
+        size = ctypes.c_size_t(ctypes.sizeof(packed))
+        extra = (ctypes.c_void_p * 5)(ctypes.c_void_p(1), ctypes.cast(ctypes.pointer(packed), ctypes.c_void_p),
+                                      ctypes.c_void_p(2), ctypes.cast(ctypes.pointer(size), ctypes.c_void_p),
+                                      ctypes.c_void_p(3))
+        torch.cuda.synchronize()
+        rc = hip.hipModuleLaunchKernel(fn, grid, 1, 1, block, 1, 1, 0, None, None, extra)
+        assert rc == 0, "hipModuleLaunchKernel %d" % rc
+        torch.cuda.synchronize()
+    finally:
+        hip.hipModuleUnload(mod)

@@ -114,7 +114,7 @@ def _points(seed, n, inf_every=0):
     return s1, s2
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["default", "gen2", "coop", "gen"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["default", "gen2", "coop", "gen", "coop1"])
 def lanes(request, gpu):
     gpu.set_pairing_kernel(request.param)
     yield request.param

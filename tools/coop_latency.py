@@ -33,7 +33,7 @@ def timed(fn, reps=5):
 
 
 sizes = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 16, 64, 256, 1024, 2048, 4096]
-for variant, name in ((2, "coop"), (3, "one-lane")):
+for variant, name in ((2, "coop4"), (4, "coop1"), (3, "one-lane")):
     pairing_amd.set_pairing_kernel(variant)
     for n in sizes:
         p_np, q_np = bench.make_pairs(n, 0, seed=5)

@@ -210,6 +210,8 @@ def main():
     H.append("__constant__ const uint32_t FL_ONE[%d] = %s;" % (NL, arr(1)))
     H.append("// red(): quotient estimate k = (T * FL_KQ) >> 64, T = top two limbs (x13 2^28 + x12)")
     H.append("constexpr uint32_t FL_KQ = 0x%xu;" % KQ)
+    H.append("// Montgomery digit factor -q^-1 mod 2^28 (the leaves' s%d; coop_quad.h)" % QI)
+    H.append("constexpr uint32_t FL_QINV = 0x%xu;" % QINV)
     H.append("__constant__ const uint32_t FL_FROB_FQ2_C1[2][%d] = {%s};" % (NL, ", ".join(arr(v) for v in FROB_FQ2_C1)))
     for nm, tab in (("FROB_FQ6_C1", FROB_FQ6_C1), ("FROB_FQ6_C2", FROB_FQ6_C2), ("FROB_FQ12_C1", FROB_FQ12_C1)):
         H.append("__constant__ const uint32_t FL_%s[%d][2][%d] = {\n    %s};" % (

@@ -71,6 +71,8 @@ for step in "$@"; do
                 run pmc_msm_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_msm_write -o run -- python bench.py --workload msm --steps 2 --warmup 1 --no-cpu-baseline ;;
         cooptests) run pytest_coop 600 python -u -m pytest tests/test_gpu_parity.py tests/test_bench_sizes.py -m gpu -k "coop or multi_pairing" -x -v --timeout 200 --timeout-method thread ;;
         coopprof) run coop_prof 120 ./tools/coop_prof ;;
+        quadtests) run pytest_quad 300 python -u -m pytest tests/test_coop_quad.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+        cooplat_small) run coop_latency 300 python tools/coop_latency.py 1 2 16 64 256 1024 2048 ;;
         cooplat) run coop_latency 300 python tools/coop_latency.py ;;
         distwl) for w in fq_mul fr_mul wnaf decode msm; do
                     run dist1_$w 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29513 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline || exit 1
