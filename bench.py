@@ -585,7 +585,7 @@ def main():
     elif args.workload == "verify":
         # SURVEY.md §8 f rank 2, the verifier shape: one multi_pairing over a few
         # pairs (Engine::miller_loop product + final_exponentiation, mod.rs:40-160)
-        # -- a latency, on the cooperative one-wave-per-pairing kernels
+        # -- a latency, on the cooperative kernels (quad VM: four waves per pairing)
         n = args.batch if args.batch != (1 << 16) else 2
         p_np, q_np = make_pairs(n, rank, seed=3)
         p = torch.from_numpy(p_np.view(np.int64)).to(dev)
@@ -735,7 +735,7 @@ def main():
             value = dom_ms
             metric, unit = "multi_pairing latency, %d pairs (verifier shape)" % n, "ms"
             config = {"workload": "final_exponentiation(miller_loop([(P_i, Q_i)])) over %d pairs, inputs in HBM, "
-                                  "cooperative one-wave-per-pairing kernels" % n,
+                                  "cooperative kernels (quad VM: four waves per pairing, four lanes per Fq value)" % n,
                       "batch_per_gpu": n, "global_batch": n * ws, "kernel_ms": {"multi_pairing": round(dom_ms, 3)}}
         elif args.workload == "fr_mul":
             dom_name, dom_ms, dom_bytes = "fr_mul_batch", float(np.mean(k_ms["a"])), 96
@@ -854,7 +854,7 @@ def main():
         if args.workload == "verify":
             roof = {"kernel": "multi_pairing", "bound": "latency", "achieved": round(dom_ms, 4), "peak": None,
                     "unit": "ms", "frac": None, "traffic": None,
-                    "note": "dependent product levels of one wave (DESIGN.md section 4, cooperative kernels)"}
+                    "note": "dependent product / linear-combination steps of the quad VM (DESIGN.md section 4, cooperative kernels)"}
         cpu = None
         if not args.no_cpu_baseline and ws == 1:
             if args.workload == "pairing":

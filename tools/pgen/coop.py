@@ -56,8 +56,10 @@ KIND_NAME = ["LIN", "P1", "P2", "SQ", "INV", "LC"]
 LC = os.environ.get("COOP_CHAINS", "0") != "1"
 LC_TMAX = 15       # terms of one LC task (incl. the zero padding of a split)
 # macros whose product lanes compute their <= 2-term operands in a prologue
-# (measured: a wash on the Miller-loop macros, -5 % on the cyclotomic square)
-PAIRS = set(os.environ.get("COOP_PAIRS", "cyc").split(","))
+# (one-wave VM: a wash on the Miller-loop macros, -5 % on the cyclotomic
+# square; quad VM (profiles/r03_s3_coop_pairs_ab.txt): ML +13 % with
+# prologues, FE -3 % with them on every FE macro)
+PAIRS = set(os.environ.get("COOP_PAIRS", "cyc,conj12,mul12,frob1,frob2,frob3,inv12").split(","))
 SPLIT_SOP = os.environ.get("COOP_SPLIT_SOP", "1") == "1"   # measured: +2.5k cycles per product step, a wash
 # DSL-level LIN ops
 L_ADD, L_SUB, L_NEG, L_RED = range(4)
@@ -1075,7 +1077,7 @@ def main():
         print("%-7s %s" % (m.name, m.stats()))
     if "--check" in sys.argv:
         check(macros, consts)
-    out = os.path.join(ROOT, "pairing_amd", "csrc", "coop_prog.h")
+    out = os.environ.get("COOP_OUT") or os.path.join(ROOT, "pairing_amd", "csrc", "coop_prog.h")
     ns, nr, nslots = emit(macros, consts, out)
     print("wrote %s: %d steps, %d lane records (%d B), %d absolute slots, %d constants"
           % (out, ns, nr, nr * 16, nslots, len(consts)))
