@@ -40,6 +40,10 @@ bool use_coop(size_t n) {
     return g_pairing_variant == 2 || g_pairing_variant == 4 || (g_pairing_variant == 0 && n <= coop_max());
 }
 int coop_vm() { return g_pairing_variant == 4 ? 1 : 0; }
+// multi-pairings of at most this many pairs multiply their Miller values inside
+// the cooperative final exponentiation (sequential mul12 macros); larger ones
+// use the log-depth product tree first
+constexpr size_t kCoopProductMax = 16;
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s, coop_vm());
@@ -693,6 +697,14 @@ int pa_multi_pairing_device(const pa_g1_affine* p, const pa_g2_affine* q, size_t
         return PA_OK;
     }
     PA_TRY(ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)work, n, s), "kernel launch");
+    if (n <= kCoopProductMax && use_coop(1)) {
+        // the product of a few Miller values inside the cooperative final
+        // exponentiation (mul12 macros, ~6 us each) instead of the one-lane
+        // product-tree kernel (~117 us per level)
+        PA_TRY(pa::launch_coop_final_exp((const uint64_t*)work, (uint64_t*)out, ok, 1, s, coop_vm(), n),
+               "kernel launch");
+        return PA_OK;
+    }
     PA_TRY(pa::launch_fq12_product((uint64_t*)work, n, (uint64_t*)work, s), "kernel launch");
     PA_TRY(fe_launch((const uint64_t*)work, (uint64_t*)out, ok, 1, s), "kernel launch");
     return PA_OK;

@@ -88,8 +88,10 @@ hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, ui
 // one-wave VM; PA_COOP_VM=1 / 4 overrides), 1 = one-wave VM, 4 = quad VM
 hipError_t launch_coop_miller_loop(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                    hipStream_t stream, int vm = 0);
+// nin > 1 (with n = 1): the final exponentiation of in[0] * ... * in[nin - 1]
+// (a multi-pairing's per-pair Miller values), the product on the same VM
 hipError_t launch_coop_final_exp(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream,
-                                 int vm = 0);
+                                 int vm = 0, size_t nin = 1);
 // out[0] = prod_i in[i] (Fq12), in-place tree reduction over `work` (n entries, clobbered)
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
 

@@ -78,6 +78,7 @@ for step in "$@"; do
                     run dist1_$w 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29513 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline || exit 1
                 done
                 run dist1_msm_global 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29514 bench.py --workload msm --global-batch 1000003 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        profverify) run prof_verify 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_verify -o run -- python bench.py --workload verify --steps 10 --warmup 2 --no-cpu-baseline ;;
         profprep) run prof_prep 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_prep -o run -- python bench.py --workload prepared --steps 3 --warmup 1 --no-cpu-baseline ;;
         prepbench) run bench_prepared 400 python bench.py --workload prepared --steps 5 --warmup 1 ;;
         preptests) run pytest_prep 600 python -u -m pytest tests/test_bench_sizes.py tests/test_gpu_parity.py -m gpu -k "prepare or miller_loop" -x -v --timeout 300 --timeout-method thread ;;
