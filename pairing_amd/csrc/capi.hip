@@ -712,10 +712,27 @@ int pa_multi_pairing_device(const pa_g1_affine* p, const pa_g2_affine* q, size_t
 
 int pa_multi_pairing(const pa_g1_affine* p, const pa_g2_affine* q, size_t n, pa_fq12* out, uint8_t* ok) {
     if (!out || !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
-    pa_fq12 ml;
-    int rc = pa_multi_miller_loop_affine(p, q, n, &ml);
-    if (rc) return rc;
-    return pa_final_exponentiation_batch(&ml, out, ok, 1);
+    if (n && (!p || !q)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (n == 0) {   // the empty product: final_exponentiation(one) = one
+        pa_fq12 ml;
+        int rc = pa_multi_miller_loop_affine(p, q, 0, &ml);
+        if (rc) return rc;
+        return pa_final_exponentiation_batch(&ml, out, ok, 1);
+    }
+    // one stream round trip: the pairs up, the device entry (Miller loops,
+    // product, final exponentiation), the result down
+    DevBuf dp, dq, dwork, dout, dok;
+    int rc;
+    if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_affine) * n)))
+        return rc;
+    PA_TRY(dwork.alloc(576 * n), "device scratch");
+    PA_TRY(dout.alloc(576), "device scratch");
+    PA_TRY(dok.alloc(1), "device scratch");
+    if ((rc = pa_multi_pairing_device(dp.as<pa_g1_affine>(), dq.as<pa_g2_affine>(), n, dout.as<pa_fq12>(),
+                                      dok.as<uint8_t>(), dwork.as<pa_fq12>(), call_stream())))
+        return rc;
+    if ((rc = download(out, dout, 576))) return rc;
+    return download(ok, dok, 1);
 }
 
 // ---- point encodings ----
