@@ -90,9 +90,11 @@ hipError_t launch_miller_loop_prepared(const uint64_t* p_aff, const uint64_t* pr
 }
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream) {
     if (n == 0) return hipErrorInvalidValue;
-    // a few values: sequential mul12 macros on the cooperative VM (~6 us each)
-    // beat the one-lane tree (~117 us per level)
-    if (n >= 2 && n <= 16) return launch_coop_fq12_product(work, n, out, stream);
+    // up to 2^16 values: levels of 16-value products as mul12 macros on the
+    // cooperative VM (~6 us per product, one workgroup per 16 values) beat the
+    // one-lane tree (~117 us per level of 2); larger ones use the tree, whose
+    // levels are wide enough to fill the GPU
+    if (n >= 2 && n <= 65536) return launch_coop_fq12_product(work, n, out, stream);
     size_t cnt = n;
     while (cnt > 1) {
         const size_t half = (cnt + 1) / 2;

@@ -92,9 +92,9 @@ hipError_t launch_coop_miller_loop(const uint64_t* p_aff, const uint64_t* q_aff,
 // (a multi-pairing's per-pair Miller values), the product on the same VM
 hipError_t launch_coop_final_exp(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t stream,
                                  int vm = 0, size_t nin = 1);
-// out = in[0] * ... * in[n - 1] on one cooperative workgroup (mul12 macros;
-// launch_fq12_product uses it for 2 <= n <= 16)
-hipError_t launch_coop_fq12_product(const uint64_t* in, size_t n, uint64_t* out, hipStream_t stream);
+// out = work[0] * ... * work[n - 1] by levels of 16-value products on the
+// cooperative VM (mul12 macros, one workgroup per 16 values; `work` clobbered)
+hipError_t launch_coop_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
 // out[0] = prod_i in[i] (Fq12), in-place tree reduction over `work` (n entries, clobbered)
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream);
 

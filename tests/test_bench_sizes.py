@@ -213,11 +213,12 @@ def test_prepared_path_device_bit_exact_at_bench_size(gpu, oracle, n):
     np.testing.assert_array_equal(_host(out), oracle.pairing(p_np, q_np, _threads()))
 
 
-@pytest.mark.parametrize("n", [0, 1, 2, 5, 16, 17])
+@pytest.mark.parametrize("n", [0, 1, 2, 5, 16, 17, 300])
 def test_multi_pairing_device_matches_oracle(gpu, oracle, n):
     """bench.py --workload verify: pa_multi_pairing_device (cooperative Miller
     loops; up to 16 pairs the Miller values' product inside the cooperative
-    final exponentiation, 17 and more the product tree first) == the oracle's
+    final exponentiation, more first in levels of 16-value cooperative
+    products) == the oracle's
     final_exponentiation(miller_loop(pairs)); the empty product is one"""
     import torch
     import bench

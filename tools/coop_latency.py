@@ -47,7 +47,7 @@ for variant, name in ((2, "coop4"), (4, "coop1"), (3, "one-lane")):
         print("%-8s n=%5d  pairing batch %8.3f ms (ML %7.3f, FE %7.3f)  -> %9.0f pairings/s"
               % (name, n, ms, ml, fe, n / ms * 1e3), flush=True)
 pairing_amd.set_pairing_kernel(0)
-for n in (1, 2, 4, 16):
+for n in (1, 2, 4, 16, 64, 256):
     p_np, q_np = bench.make_pairs(n, 0, seed=9)
     import time
     pairing_amd.multi_pairing(p_np, q_np)
