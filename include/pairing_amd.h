@@ -79,7 +79,7 @@ int pa_set_device(int device);
 int pa_synchronize(void);
 /* Tuning knob: which kernels run the Miller loop / final exponentiation
  * (identical results):
- *   0 = default: batches of more than PA_COOP_MAX (2048) pairings on the
+ *   0 = default: batches of more than PA_COOP_MAX (4096) pairings on the
  *       generated one-pairing-per-lane kernels (tools/pgen: own register
  *       allocation, code objects lib/pa_gen_*.hsaco loaded at first use),
  *       smaller batches on the cooperative kernels (one wave per pairing,

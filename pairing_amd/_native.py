@@ -200,7 +200,7 @@ def device_count():
 
 
 def set_pairing_kernel(variant):
-    """Pairing kernels: 0 default (one lane per pairing; batches <= 2048 on the
+    """Pairing kernels: 0 default (one lane per pairing; batches <= 4096 on the
     cooperative kernels: a four-wave quad VM per pairing), 1 lane pairs, 2
     cooperative for every size, 3 one lane per pairing for every size, 4
     cooperative for every size on the round-2 one-wave VM.  Identical results."""

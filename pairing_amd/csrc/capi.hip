@@ -22,7 +22,7 @@ namespace {
 
 thread_local std::string g_last_error;
 // Pairing kernel selection (pa_set_pairing_kernel): 0 -> one lane per
-// pairing (the generated kernels), with batches of at most coop_max() pairs
+// pairing (the generated kernels), with batches of at most coop_max() (4096) pairs
 // on the cooperative one-wave-per-pairing kernels (kernels_coop.hip, ~1/10
 // of the latency); 1 -> lane pairs; 2 -> cooperative for every batch size;
 // 3 -> one lane per pairing for every batch size; 4 -> cooperative for every
@@ -31,8 +31,10 @@ int g_pairing_variant = 0;
 
 size_t coop_max() {
     static const size_t v = [] {
+        // the quad VM's ~270 k pairings/s meets the one-lane kernels' flat
+        // ~15.7 ms per batch at ~4 k pairs (profiles/r03_s3_coop_crossover.txt)
         const char* e = getenv("PA_COOP_MAX");   // A/B measurements
-        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)2048;
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
     }();
     return v;
 }

@@ -286,7 +286,7 @@ def test_final_exp_split_and_in_place_agree(gpu, oracle):
     equal the oracle, including f == 0 (reference None: zero, ok = 0)."""
     import torch
     import pairing_amd.device as pdev
-    n = 2300        # above the cooperative kernels' batch limit (PA_COOP_MAX 2048)
+    n = 4200        # above the cooperative kernels' batch limit (PA_COOP_MAX 4096)
     f = _field_rows(41, n * 12, 6, FQ_TOP, [1]).reshape(n, 72)
     f[7] = 0
     exp, ok_exp = oracle.final_exponentiation(f, _threads())
