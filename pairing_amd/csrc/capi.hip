@@ -21,27 +21,41 @@
 namespace {
 
 thread_local std::string g_last_error;
-// Pairing kernel selection (pa_set_pairing_kernel): 0 -> one lane per
-// pairing (the generated kernels), with batches of at most coop_max() (4096) pairs
-// on the cooperative one-wave-per-pairing kernels (kernels_coop.hip, ~1/10
-// of the latency); 1 -> lane pairs; 2 -> cooperative for every batch size;
-// 3 -> one lane per pairing for every batch size; 4 -> cooperative for every
-// batch size on the round-2 one-wave VM (A/B against the quad VM).
+// Pairing kernel selection (pa_set_pairing_kernel).  0 (default) by batch
+// size, each where it is fastest (profiles/r03_s3_batch_regimes.txt):
+//   n <= coop_max() (2560): the cooperative kernels (kernels_coop.hip, a
+//      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
+//   n <= pair_max() (32768): the generated kernels with a lane pair per
+//      pairing (<= 1 wave per SIMD either way, so half the instructions per
+//      lane is half the time: ~10 ms where one lane takes ~15.7 ms);
+//   larger: one lane per pairing (2^16: 17.3 vs 20.3 ms for lane pairs).
+// 1 -> lane pairs for every batch size; 2 -> cooperative for every batch
+// size; 3 -> one lane per pairing for every batch size; 4 -> cooperative for
+// every batch size on the round-2 one-wave VM (A/B against the quad VM).
 int g_pairing_variant = 0;
 
+size_t env_size(const char* name, size_t dflt) {
+    const char* e = getenv(name);   // A/B measurements
+    return e ? (size_t)strtoull(e, nullptr, 10) : dflt;
+}
 size_t coop_max() {
-    static const size_t v = [] {
-        // the quad VM's ~270 k pairings/s meets the one-lane kernels' flat
-        // ~15.7 ms per batch at ~4 k pairs (profiles/r03_s3_coop_crossover.txt)
-        const char* e = getenv("PA_COOP_MAX");   // A/B measurements
-        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
-    }();
+    static const size_t v = env_size("PA_COOP_MAX", 2560);
+    return v;
+}
+size_t pair_max() {
+    static const size_t v = env_size("PA_PAIR_MAX", 32768);
     return v;
 }
 bool use_coop(size_t n) {
     return g_pairing_variant == 2 || g_pairing_variant == 4 || (g_pairing_variant == 0 && n <= coop_max());
 }
 int coop_vm() { return g_pairing_variant == 4 ? 1 : 0; }
+// lanes per pairing of the generated kernels
+int gen_lanes(size_t n) {
+    if (g_pairing_variant == 1) return 2;
+    if (g_pairing_variant == 3) return 1;
+    return n <= pair_max() ? 2 : 1;
+}
 // multi-pairings of at most this many pairs multiply their Miller values inside
 // the cooperative final exponentiation (sequential mul12 macros); larger ones
 // use the log-depth product tree first
@@ -49,11 +63,11 @@ constexpr size_t kCoopProductMax = 16;
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s, coop_vm());
-    return pa::launch_miller_loop_gen(g_pairing_variant == 1 ? 2 : 1, p, q, out, n, s);
+    return pa::launch_miller_loop_gen(gen_lanes(n), p, q, out, n, s);
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s, coop_vm());
-    return pa::launch_final_exp_gen(g_pairing_variant == 1 ? 2 : 1, in, out, ok, n, s);
+    return pa::launch_final_exp_gen(gen_lanes(n), in, out, ok, n, s);
 }
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {

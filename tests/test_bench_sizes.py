@@ -105,6 +105,22 @@ def test_pairing_device_bit_exact_at_bench_size(gpu, oracle):
     assert (got[inf] == one).all()
 
 
+@pytest.mark.parametrize("n", [2561, 32768])
+def test_pairing_default_mid_size_batches(gpu, oracle, n):
+    """The default selection's middle regime (PA_COOP_MAX < n <= PA_PAIR_MAX:
+    the generated kernels with a lane pair per pairing) at both ends, every
+    pairing against the oracle"""
+    import torch
+    import bench
+    import pairing_amd.device as pdev
+    p_np, q_np = bench.make_pairs(n, 0, seed=29)
+    out = pdev.empty_records(n, 72, "cuda:0")
+    scratch = pdev.empty_records(n, 72, "cuda:0")
+    pdev.pairing(_dev(p_np), _dev(q_np), out, scratch)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(out), oracle.pairing(p_np, q_np, _threads()))
+
+
 def test_pairing_two_streams_concurrently(gpu, oracle):
     """Two pairing batches enqueued on two streams before either finishes:
     both bit-exact (each launch draws its own spill workspace)"""
@@ -286,18 +302,22 @@ def test_final_exp_split_and_in_place_agree(gpu, oracle):
     equal the oracle, including f == 0 (reference None: zero, ok = 0)."""
     import torch
     import pairing_amd.device as pdev
-    n = 4200        # above the cooperative kernels' batch limit (PA_COOP_MAX 4096)
-    f = _field_rows(41, n * 12, 6, FQ_TOP, [1]).reshape(n, 72)
-    f[7] = 0
-    exp, ok_exp = oracle.final_exponentiation(f, _threads())
-    d_in = _dev(f)
-    out = pdev.empty_records(n, 72, "cuda:0")
-    ok = torch.empty(n, dtype=torch.uint8, device="cuda:0")
-    pdev.final_exponentiation(d_in, out, ok)
-    d_same = _dev(f)
-    ok2 = torch.empty(n, dtype=torch.uint8, device="cuda:0")
-    pdev.final_exponentiation(d_same, d_same, ok2)
-    torch.cuda.synchronize()
+    n = 2300
+    gpu.set_pairing_kernel(3)   # the one-lane generated kernels, whose FE has the split form
+    try:
+        f = _field_rows(41, n * 12, 6, FQ_TOP, [1]).reshape(n, 72)
+        f[7] = 0
+        exp, ok_exp = oracle.final_exponentiation(f, _threads())
+        d_in = _dev(f)
+        out = pdev.empty_records(n, 72, "cuda:0")
+        ok = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        pdev.final_exponentiation(d_in, out, ok)
+        d_same = _dev(f)
+        ok2 = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        pdev.final_exponentiation(d_same, d_same, ok2)
+        torch.cuda.synchronize()
+    finally:
+        gpu.set_pairing_kernel(0)
     np.testing.assert_array_equal(_host(out), exp)
     np.testing.assert_array_equal(_host(d_same), exp)
     np.testing.assert_array_equal(ok.cpu().numpy(), np.asarray(ok_exp, np.uint8))
