@@ -138,6 +138,18 @@ def make_pairs(n, rank, seed=0, span=None):
     return p, q
 
 
+def kernel_variant_label(n):
+    """the pairing kernels a batch of n per GPU runs on (capi.hip: PA_PAIRING_KERNEL 0 = by
+    batch size, <= PA_COOP_MAX cooperative quad VM, <= PA_PAIR_MAX generated lane pairs, else
+    generated one lane; 1 lane pairs, 2 quad VM, 3 one lane, 4 one-wave VM)"""
+    v = int(os.environ.get("PA_PAIRING_KERNEL", "0"))
+    if v == 0:
+        if n <= int(os.environ.get("PA_COOP_MAX", "2560")):
+            return "coop"
+        return "gen2" if n <= int(os.environ.get("PA_PAIR_MAX", "32768")) else "gen"
+    return {1: "gen2", 2: "coop", 3: "gen", 4: "coop1"}.get(v, "variant%d" % v)
+
+
 def host_threads():
     """(host cores this process may run on, threads the CPU baseline uses):
     the affinity mask, capped by OMP_NUM_THREADS when the environment sets it
@@ -682,7 +694,7 @@ def main():
                 wl += "; fixed global batch %d in %d contiguous shards (BASELINE config 5 at 2^20 over 8)" % (
                     n_global, ws)
             config = {"workload": wl,
-                      "kernel_variant": ["gen", "gen2", "coop", "gen"][int(os.environ.get("PA_PAIRING_KERNEL", "0"))],
+                      "kernel_variant": kernel_variant_label(n),
                       "batch_per_gpu": n, "global_batch": n_global, "parallelism": "shard%d+rccl_gather" % ws
                       if dist_on else "single", "kernel_ms": {"miller_loop_fused": round(ml, 3),
                                                              "final_exponentiation": round(fe, 3)}}
@@ -757,11 +769,7 @@ def main():
         tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tr_path):
             with open(tr_path) as f:
-                # the split final exponentiation has its own entry (the three
-                # kernels' bytes per step); null until measured
-                fe_split = args.workload in ("pairing", "prepared") and dom_name == "final_exponentiation" and \
-                    os.environ.get("PA_FE_SPLIT", "0") == "1"
-                traffic = json.load(f).get(dom_name + ("_split" if fe_split else ""))
+                traffic = json.load(f).get(dom_name)
         roof = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "bytes_per_unit": dom_bytes, "avg_launch_ms": round(dom_ms, 4)}
@@ -781,16 +789,10 @@ def main():
             with open(work_path) as f:
                 work = json.load(f)
             # the final exponentiation step is one generated kernel (round 3:
-            # in-kernel binary-GCD inversions, compressed squarings); with
-            # PA_FE_SPLIT=1 round 2's split form: norm kernel + binary-GCD
-            # inversion kernel + the rest, whose MACs / instructions are the two
-            # generated kernels' (the inversion kernel's integer work is not
-            # limb MACs).  The in-kernel binary GCD's instructions are counted,
-            # its 64-bit approximation steps are not limb MACs either.
-            split = os.environ.get("PA_FE_SPLIT", "0") == "1" and "fe_inv" in work
-            wk = (work["miller_loop"] if dom_name != "final_exponentiation" else
-                  {k: work["fe_norm"][k] + work["fe_inv"][k] for k in ("limb_macs", "instructions")}
-                  if split else work["final_exp"])
+            # in-kernel binary-GCD inversions, compressed squarings).  The
+            # binary GCD's instructions are counted, its 64-bit approximation
+            # steps are not limb MACs.
+            wk = work["miller_loop"] if dom_name != "final_exponentiation" else work["final_exp"]
             macs = wk["limb_macs"]
             mac_rate = macs * n / (dom_ms * 1e-3) / 1e12
             roof = {"kernel": dom_name, "bound": "valu", "achieved": round(mac_rate, 3),

@@ -150,12 +150,19 @@ int pa_pairing_batch(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out,
  * already-normalized points are left untouched; others get z = 1. */
 int pa_g1_batch_normalization(pa_g1 *v, size_t n);
 /* Wnaf::new().base(*base, n).scalar(scalars[i]) for every i (wnaf.rs:93-107,
- * 169-178): out[i] = scalars[i] * base as a Jacobian point (equal as a point to
- * the reference's; representation-independent PartialEq, ec.rs:45-85).  Any
- * 256-bit FrRepr is multiplied exactly; the reference's wnaf_form wraps
- * (add_nocarry, wnaf.rs:30-35) for raw reprs within 2^w of 2^256, values no
- * Fr::into_repr produces, so those two differ only there. */
+ * 169-178): out[i] = the reference's wNAF product of scalars[i] and base as a
+ * Jacobian point (equal as a point to the reference's; representation-
+ * independent PartialEq, ec.rs:45-85).  That is scalars[i] * base for every
+ * 256-bit FrRepr except where the reference's wnaf_form wraps in add_nocarry
+ * (wnaf.rs:30-35: s odd with bits w..255 all ones, w the window
+ * recommended_wnaf_for_num_scalars(n)); there it is (s - 2^256) * base, which
+ * these entries reproduce. */
 int pa_g1_wnaf_fixed_base(const pa_g1 *base, const pa_fr_repr *scalars, size_t n, pa_g1 *out);
+/* the same with the window given: Wnaf::new().base(*base, num_scalars) picks
+ * window = recommended_wnaf_for_num_scalars(num_scalars) and .shared() copies
+ * may then multiply any number n of scalars (wnaf.rs:93-107, 131-154);
+ * window in 1..62 */
+int pa_g1_wnaf_fixed_base_window(const pa_g1 *base, const pa_fr_repr *scalars, size_t n, int window, pa_g1 *out);
 
 /* ---- CurveProjective / CurveAffine per-op batches, G1 and G2 ----
  * The `curve_impl!` group law (ec.rs:1-621) for both groups, one item per
@@ -191,11 +198,11 @@ int pa_g2_eq_batch(const pa_g2 *a, const pa_g2 *b, uint8_t *eq, size_t n);
 /* G2 CurveProjective::batch_normalization, ec.rs:246-294, in place */
 int pa_g2_batch_normalization(pa_g2 *v, size_t n);
 /* G2 Wnaf::new().base(*base, n).scalar(scalars[i]) (wnaf.rs:93-107, 169-178):
- * out[i] = scalars[i] * base, equal as a point to the reference's (PartialEq,
- * ec.rs:45-85).  Any 256-bit FrRepr is multiplied exactly; the reference's
- * wnaf_form instead wraps (add_nocarry, wnaf.rs:30-35) for raw reprs within
- * 2^w of 2^256, values no Fr::into_repr produces. */
+ * out[i] = the reference's wNAF product, equal as a point to the reference's
+ * (PartialEq, ec.rs:45-85), including its add_nocarry wrap (wnaf.rs:30-35; see
+ * pa_g1_wnaf_fixed_base); _window: the window given, 1..62 */
 int pa_g2_wnaf_fixed_base(const pa_g2 *base, const pa_fr_repr *scalars, size_t n, pa_g2 *out);
+int pa_g2_wnaf_fixed_base_window(const pa_g2 *base, const pa_fr_repr *scalars, size_t n, int window, pa_g2 *out);
 /* CurveProjective::recommended_wnaf_for_scalar / _for_num_scalars
  * (lib.rs:166-174; G1 ec.rs:895-921, G2 ec.rs:1586-1612): the window the
  * reference's Wnaf would pick (returned as a positive int).  The GPU
@@ -297,7 +304,10 @@ int pa_g1_decode_batch_device(const uint8_t *enc, size_t n, int compressed, int 
 int pa_g2_decode_batch_device(const uint8_t *enc, size_t n, int compressed, int checked, pa_g2_affine *out,
                               uint8_t *status, void *stream);
 int pa_g1_batch_normalization_device(pa_g1 *v, size_t n, void *stream);
-/* u64 words of the fixed-base table and of the scratch used to build it */
+/* u64 words of the fixed-base table and of the scratch used to build it.  The
+ * multiply stages below give the reference's wNAF point for the window
+ * recommended_wnaf_for_num_scalars(n) (its add_nocarry wrap included, see
+ * pa_g1_wnaf_fixed_base). */
 size_t pa_g1_fixed_base_table_words(void);
 size_t pa_g1_fixed_base_workspace_words(void);
 int pa_g1_fixed_base_table_device(const pa_g1 *base, uint64_t *table, uint64_t *workspace, void *stream);
@@ -314,6 +324,8 @@ int pa_g1_fixed_base_glv_mul_device(const pa_g1 *base, const uint64_t *table, co
  * events); equal as points to pa_g1_fixed_base_table_device + pa_g1_fixed_base_mul_device. */
 int pa_g1_wnaf_fixed_base_device(const pa_g1 *base, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
                                  uint64_t *table, uint64_t *workspace, void *stream);
+int pa_g1_wnaf_fixed_base_window_device(const pa_g1 *base, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
+                                        int window, uint64_t *table, uint64_t *workspace, void *stream);
 int pa_fq_mul_batch_device(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n, void *stream);
 /* Fq::mul_assign (fq.rs:909-960) on the SoA device layout of SURVEY.md 8(d) config 2: u64 word j
  * (0..5, little-endian, Montgomery, < q) of element i at a[j * n + i]; same bits as the AoS form */
@@ -331,6 +343,8 @@ size_t pa_g2_fixed_base_table_words(void);
 size_t pa_g2_fixed_base_workspace_words(void);
 int pa_g2_wnaf_fixed_base_device(const pa_g2 *base, const pa_fr_repr *scalars, pa_g2 *out, size_t n,
                                  uint64_t *table, uint64_t *workspace, void *stream);
+int pa_g2_wnaf_fixed_base_window_device(const pa_g2 *base, const pa_fr_repr *scalars, pa_g2 *out, size_t n,
+                                        int window, uint64_t *table, uint64_t *workspace, void *stream);
 /* group law on device memory (see the host batches above) */
 int pa_g1_double_batch_device(const pa_g1 *a, pa_g1 *out, size_t n, void *stream);
 int pa_g2_double_batch_device(const pa_g2 *a, pa_g2 *out, size_t n, void *stream);
@@ -344,13 +358,10 @@ int pa_g1_eq_batch_device(const pa_g1 *a, const pa_g1 *b, uint8_t *eq, size_t n,
 int pa_g2_eq_batch_device(const pa_g2 *a, const pa_g2 *b, uint8_t *eq, size_t n, void *stream);
 int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
                                       void *stream);
-/* final_exponentiation (mod.rs:104-160) on device records.  With `out` apart
- * from `in`, batches above PA_COOP_MAX run in three launches on `stream`: the
- * Fq value f^-1 needs inverted is written to Fq 0 of each `out` record,
- * inverted there by binary GCD, and read back by the rest of the
- * exponentiation, which then overwrites `out`; `in` is left unchanged.
- * in == out (or overlapping) runs the one-kernel form in place.  Same bits
- * either way; PA_FE_SPLIT=0 in the environment forces the one-kernel form. */
+/* final_exponentiation (mod.rs:104-160) on device records: one kernel launch
+ * on `stream` (the cooperative kernel up to PA_COOP_MAX records, the generated
+ * one above); `out` may equal `in` (in place) or lie apart from it, in which
+ * case `in` is left unchanged.  ok[i] = 0 iff in[i] == 0 (None). */
 int pa_final_exponentiation_batch_device(const pa_fq12 *in, pa_fq12 *out, uint8_t *ok, size_t n, void *stream);
 /* pa_multi_pairing on device memory (the verifier's check without host copies); `work` holds n
  * pa_fq12 (the per-pair Miller values, reduced in place to their product) */

@@ -420,7 +420,7 @@ template <> struct GroupAbi<1> {
     static constexpr auto normalize = &pa_g1_batch_normalization;
     static constexpr auto mul_assign = &pa_g1_mul_assign_batch;
     static constexpr auto affine_mul = &pa_g1_affine_mul_batch;
-    static constexpr auto fixed_base = &pa_g1_wnaf_fixed_base;
+    static constexpr auto fixed_base = &pa_g1_wnaf_fixed_base_window;
     static constexpr auto window_for_scalar = &pa_g1_recommended_wnaf_for_scalar;
     static constexpr auto window_for_count = &pa_g1_recommended_wnaf_for_num_scalars;
     static constexpr auto multiexp = &pa_g1_multiexp;
@@ -441,7 +441,7 @@ template <> struct GroupAbi<2> {
     static constexpr auto normalize = &pa_g2_batch_normalization;
     static constexpr auto mul_assign = &pa_g2_mul_assign_batch;
     static constexpr auto affine_mul = &pa_g2_affine_mul_batch;
-    static constexpr auto fixed_base = &pa_g2_wnaf_fixed_base;
+    static constexpr auto fixed_base = &pa_g2_wnaf_fixed_base_window;
     static constexpr auto window_for_scalar = &pa_g2_recommended_wnaf_for_scalar;
     static constexpr auto window_for_count = &pa_g2_recommended_wnaf_for_num_scalars;
     static constexpr auto multiexp = &pa_g2_multiexp;
@@ -681,10 +681,23 @@ inline Fq12 G2Affine::pairing_with(const G1Affine& other) const { return Bls12::
 // window is the reference's recommended_wnaf_* choice (window()), but the GPU
 // multiplies with a signed base-256 comb (fixed base) or the reference's
 // mul_assign (fixed scalar), so the resulting POINTS equal the reference's
-// (PartialEq, ec.rs:45-85) while Jacobian words may differ.  Any 256-bit
-// FrRepr is multiplied exactly; the reference's wnaf_form wraps (add_nocarry,
-// wnaf.rs:30-35) for raw reprs within 2^window of 2^256, values no
-// Fr::into_repr produces.
+// (PartialEq, ec.rs:45-85) while Jacobian words may differ.  That includes
+// the reference's wnaf_form wrap (add_nocarry, wnaf.rs:30-35): for an odd repr
+// whose bits window..255 are all ones its digits spell s - 2^256, and so does
+// the product here (wnaf_wraps below; the fixed-base entries do it on device).
+//
+// wnaf_wraps(s, w): whether wnaf_form(s, w) wraps; t = 2^256 - s then.
+inline bool wnaf_wraps(const FrRepr& s, size_t window, FrRepr* t) {
+    if (window < 1 || window > 62 || !(s.v.l[0] & 1)) return false;
+    if ((s.v.l[0] | ((1ull << window) - 1)) != ~0ull || (s.v.l[1] & s.v.l[2] & s.v.l[3]) != ~0ull) return false;
+    uint64_t c = 1;
+    for (int k = 0; k < 4; k++) {
+        const uint64_t v = ~s.v.l[k] + c;
+        c = (c && v == 0) ? 1 : 0;
+        t->v.l[k] = v;
+    }
+    return true;
+}
 template <class P>
 class WnafBase {
 public:
@@ -693,7 +706,7 @@ public:
     WnafBase shared() const { return *this; }
     std::vector<P> scalars(const std::vector<FrRepr>& s) const {
         std::vector<P> out(s.size());
-        if (!s.empty()) check(P::Abi::fixed_base(&base_.v, &s[0].v, s.size(), &out[0].v), "Wnaf::scalar");
+        if (!s.empty()) check(P::Abi::fixed_base(&base_.v, &s[0].v, s.size(), (int)window_, &out[0].v), "Wnaf::scalar");
         return out;
     }
     P scalar(const FrRepr& s) const { return scalars({s})[0]; }
@@ -708,13 +721,16 @@ public:
     explicit WnafScalar(const FrRepr& s) : s_(s) {}
     template <class P>
     P base(const P& g) const {
-        P r = g;
-        r.mul_assign(s_);
-        return r;
+        return bases(std::vector<P>{g})[0];
     }
     template <class P>
     std::vector<P> bases(const std::vector<P>& g) const {
-        return P::mul_assign_batch(g, std::vector<FrRepr>(g.size(), s_));
+        FrRepr t;
+        const bool wraps = wnaf_wraps(s_, window_for<P>(s_), &t);
+        auto out = P::mul_assign_batch(g, std::vector<FrRepr>(g.size(), wraps ? t : s_));
+        if (wraps)
+            for (auto& r : out) r.negate();   // the digits spell s - 2^256 = -t
+        return out;
     }
     template <class P>
     static size_t window_for(const FrRepr& s) { return P::recommended_wnaf_for_scalar(s); }

@@ -83,6 +83,10 @@ def _declare(L):
         "o_g2_batch_normalization": [_P, _N],
         "o_g1_wnaf_fixed_base": [_P, _P, _N, _P, _I],
         "o_g2_wnaf_fixed_base": [_P, _P, _N, _P, _I],
+        "o_g1_wnaf_fixed_base_w": [_P, _P, _N, _I, _P, _I],
+        "o_g2_wnaf_fixed_base_w": [_P, _P, _N, _I, _P, _I],
+        "o_g1_wnaf_fixed_scalar": [_P, _P, _N, _P, _I],
+        "o_g2_wnaf_fixed_scalar": [_P, _P, _N, _P, _I],
         "o_g1_kg_vectors": [_P, _N, _I],
         "o_g2_kg_vectors": [_P, _N, _I],
         "o_g2_prepare_batch": [_P, _N, _P, _I],
@@ -370,16 +374,41 @@ def g2_batch_normalization(v):
     v = np.ascontiguousarray(v.copy()); lib().o_g2_batch_normalization(_p(v), _n(v)); return v
 
 
-def g1_wnaf_fixed_base(base, scalars, nthreads=1):
+def g1_wnaf_fixed_base(base, scalars, nthreads=1, window=None):
+    """Wnaf::new().base(base, n).scalar(s_i) (wnaf.rs:93-107, 169-178); window
+    default recommended_wnaf_for_num_scalars(n)"""
     b = np.ascontiguousarray(base.reshape(1, W_G1))
     o = _out(_n(scalars), W_G1)
-    lib().o_g1_wnaf_fixed_base(_p(b), _p(scalars), _n(scalars), _p(o), nthreads); return o
+    if window is None:
+        lib().o_g1_wnaf_fixed_base(_p(b), _p(scalars), _n(scalars), _p(o), nthreads)
+    else:
+        lib().o_g1_wnaf_fixed_base_w(_p(b), _p(scalars), _n(scalars), int(window), _p(o), nthreads)
+    return o
 
 
-def g2_wnaf_fixed_base(base, scalars, nthreads=1):
+def g2_wnaf_fixed_base(base, scalars, nthreads=1, window=None):
     b = np.ascontiguousarray(base.reshape(1, W_G2))
     o = _out(_n(scalars), W_G2)
-    lib().o_g2_wnaf_fixed_base(_p(b), _p(scalars), _n(scalars), _p(o), nthreads); return o
+    if window is None:
+        lib().o_g2_wnaf_fixed_base(_p(b), _p(scalars), _n(scalars), _p(o), nthreads)
+    else:
+        lib().o_g2_wnaf_fixed_base_w(_p(b), _p(scalars), _n(scalars), int(window), _p(o), nthreads)
+    return o
+
+
+def g1_wnaf_fixed_scalar(bases, scalar, nthreads=1):
+    """Wnaf::new().scalar(s).base(g_i) (wnaf.rs:111-128, 156-165)"""
+    b = np.ascontiguousarray(bases.reshape(-1, W_G1))
+    s = np.ascontiguousarray(np.asarray(scalar, np.uint64).reshape(4))
+    o = _out(b.shape[0], W_G1)
+    lib().o_g1_wnaf_fixed_scalar(_p(b), _p(s), b.shape[0], _p(o), nthreads); return o
+
+
+def g2_wnaf_fixed_scalar(bases, scalar, nthreads=1):
+    b = np.ascontiguousarray(bases.reshape(-1, W_G2))
+    s = np.ascontiguousarray(np.asarray(scalar, np.uint64).reshape(4))
+    o = _out(b.shape[0], W_G2)
+    lib().o_g2_wnaf_fixed_scalar(_p(b), _p(s), b.shape[0], _p(o), nthreads); return o
 
 
 def wnaf_form(scalar, window):

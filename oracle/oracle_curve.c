@@ -128,11 +128,21 @@ int o_g2_recommended_wnaf_for_num_scalars(size_t n) {                    /* ec.r
     return recommend_num(n, rec, 11);
 }
 
+void o_g1_wnaf_fixed_base_w(const o_g1 *base, const uint64_t *scalars, size_t n, int w, o_g1 *out, int nthreads);
+void o_g2_wnaf_fixed_base_w(const o_g2 *base, const uint64_t *scalars, size_t n, int w, o_g2 *out, int nthreads);
+
 /* Wnaf::new().base(g, num_scalars) then .scalar(s) per scalar (wnaf.rs:93-107,
  * 169-178): one shared table, one wNAF per scalar.  OpenMP over scalars is
  * what `Wnaf::shared()` (wnaf.rs:131-141) exists for. */
 void o_g1_wnaf_fixed_base(const o_g1 *base, const uint64_t *scalars, size_t n, o_g1 *out, int nthreads) {
-    int w = o_g1_recommended_wnaf_for_num_scalars(n);
+    o_g1_wnaf_fixed_base_w(base, scalars, n, o_g1_recommended_wnaf_for_num_scalars(n), out, nthreads);
+}
+void o_g2_wnaf_fixed_base(const o_g2 *base, const uint64_t *scalars, size_t n, o_g2 *out, int nthreads) {
+    o_g2_wnaf_fixed_base_w(base, scalars, n, o_g2_recommended_wnaf_for_num_scalars(n), out, nthreads);
+}
+/* the same with the window given: Wnaf::new().base(g, num_scalars) fixes the
+ * window from num_scalars, and its shared() copies multiply any count */
+void o_g1_wnaf_fixed_base_w(const o_g1 *base, const uint64_t *scalars, size_t n, int w, o_g1 *out, int nthreads) {
     o_g1 *table = (o_g1 *)malloc(sizeof(o_g1) * ((size_t)1 << (w - 1)));
     o_g1_wnaf_table(table, base, w);
 #pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads > 0 ? nthreads : 1)
@@ -143,8 +153,7 @@ void o_g1_wnaf_fixed_base(const o_g1 *base, const uint64_t *scalars, size_t n, o
     }
     free(table);
 }
-void o_g2_wnaf_fixed_base(const o_g2 *base, const uint64_t *scalars, size_t n, o_g2 *out, int nthreads) {
-    int w = o_g2_recommended_wnaf_for_num_scalars(n);
+void o_g2_wnaf_fixed_base_w(const o_g2 *base, const uint64_t *scalars, size_t n, int w, o_g2 *out, int nthreads) {
     o_g2 *table = (o_g2 *)malloc(sizeof(o_g2) * ((size_t)1 << (w - 1)));
     o_g2_wnaf_table(table, base, w);
 #pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads > 0 ? nthreads : 1)
@@ -154,6 +163,31 @@ void o_g2_wnaf_fixed_base(const o_g2 *base, const uint64_t *scalars, size_t n, o
         out[k] = o_g2_wnaf_exp(table, digits, len);
     }
     free(table);
+}
+
+/* Wnaf::new().scalar(s) then .base(g) per base (wnaf.rs:111-128, 156-165):
+ * the window is recommended_wnaf_for_scalar(s), one wNAF form, a table per base */
+void o_g1_wnaf_fixed_scalar(const o_g1 *bases, const uint64_t scalar[4], size_t n, o_g1 *out, int nthreads) {
+    int w = o_g1_recommended_wnaf_for_scalar(scalar);
+    int64_t digits[300];
+    size_t len = o_wnaf_form(digits, scalar, w);
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads > 0 ? nthreads : 1)
+    for (size_t k = 0; k < n; k++) {
+        o_g1 table[8];
+        o_g1_wnaf_table(table, &bases[k], w);
+        out[k] = o_g1_wnaf_exp(table, digits, len);
+    }
+}
+void o_g2_wnaf_fixed_scalar(const o_g2 *bases, const uint64_t scalar[4], size_t n, o_g2 *out, int nthreads) {
+    int w = o_g2_recommended_wnaf_for_scalar(scalar);
+    int64_t digits[300];
+    size_t len = o_wnaf_form(digits, scalar, w);
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads > 0 ? nthreads : 1)
+    for (size_t k = 0; k < n; k++) {
+        o_g2 table[8];
+        o_g2_wnaf_table(table, &bases[k], w);
+        out[k] = o_g2_wnaf_exp(table, digits, len);
+    }
 }
 
 /* ---- encodings (README.md "Serialization") ---- */

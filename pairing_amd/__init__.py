@@ -251,13 +251,18 @@ def g1_batch_normalization(v):
     return v
 
 
-def g1_wnaf_fixed_base(base, scalars):
+def g1_wnaf_fixed_base(base, scalars, window=None):
     """Wnaf::new().base(base, n).scalar(s) for each FrRepr scalar (wnaf.rs:93-107,
-    169-178): Jacobian points equal to scalars[i] * base."""
+    169-178): Jacobian points equal to the reference's wNAF products -- s_i *
+    base, or (s_i - 2^256) * base where its wnaf_form wraps (wnaf.rs:30-35).
+    `window`: the table's window (default recommended_wnaf_for_num_scalars(n))."""
     b = as_rows(base, W_G1, "base")
     s = as_rows(scalars, 4, "scalars")
     out = np.empty((s.shape[0], W_G1), np.uint64)
-    call("pa_g1_wnaf_fixed_base", ptr(b), ptr(s), s.shape[0], ptr(out))
+    if window is None:
+        call("pa_g1_wnaf_fixed_base", ptr(b), ptr(s), s.shape[0], ptr(out))
+    else:
+        call("pa_g1_wnaf_fixed_base_window", ptr(b), ptr(s), s.shape[0], int(window), ptr(out))
     return out
 
 
@@ -595,12 +600,16 @@ def g2_batch_normalization(v):
     return v
 
 
-def g2_wnaf_fixed_base(base, scalars):
-    """G2 Wnaf::new().base(base, n).scalar(s) (wnaf.rs:93-107, 169-178): points equal to s_i * base."""
+def g2_wnaf_fixed_base(base, scalars, window=None):
+    """G2 Wnaf::new().base(base, n).scalar(s) (wnaf.rs:93-107, 169-178): points
+    equal to the reference's wNAF products (see g1_wnaf_fixed_base)."""
     b = as_rows(base, W_G2, "base")
     s = as_rows(scalars, 4, "scalars")
     out = np.empty((s.shape[0], W_G2), np.uint64)
-    call("pa_g2_wnaf_fixed_base", ptr(b), ptr(s), s.shape[0], ptr(out))
+    if window is None:
+        call("pa_g2_wnaf_fixed_base", ptr(b), ptr(s), s.shape[0], ptr(out))
+    else:
+        call("pa_g2_wnaf_fixed_base_window", ptr(b), ptr(s), s.shape[0], int(window), ptr(out))
     return out
 
 

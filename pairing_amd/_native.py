@@ -95,10 +95,12 @@ _SIGS = {
     "pa_pairing_batch": [_P, _P, _P, _N],
     "pa_g1_batch_normalization": [_P, _N],
     "pa_g1_wnaf_fixed_base": [_P, _P, _N, _P],
+    "pa_g1_wnaf_fixed_base_window": [_P, _P, _N, ctypes.c_int, _P],
     "pa_g1_batch_normalization_device": [_P, _N, _P],
     "pa_g1_fixed_base_table_device": [_P, _P, _P, _P],
     "pa_g1_fixed_base_mul_device": [_P, _P, _P, _N, _P],
     "pa_g1_wnaf_fixed_base_device": [_P, _P, _P, _N, _P, _P, _P],
+    "pa_g1_wnaf_fixed_base_window_device": [_P, _P, _P, _N, ctypes.c_int, _P, _P, _P],
     "pa_g1_fixed_base_glv_table_device": [_P, _P, _P, _P],
     "pa_g1_fixed_base_glv_mul_device": [_P, _P, _P, _P, _P, _N, _P],
     "pa_fq_mul_batch_device": [_P, _P, _P, _N, _P],
@@ -164,7 +166,9 @@ _SIGS.update({
     "pa_g2_batch_normalization": [_P, _N],
     "pa_g2_batch_normalization_device": [_P, _N, _P],
     "pa_g2_wnaf_fixed_base": [_P, _P, _N, _P],
+    "pa_g2_wnaf_fixed_base_window": [_P, _P, _N, ctypes.c_int, _P],
     "pa_g2_wnaf_fixed_base_device": [_P, _P, _P, _N, _P, _P, _P],
+    "pa_g2_wnaf_fixed_base_window_device": [_P, _P, _P, _N, ctypes.c_int, _P, _P, _P],
 })
 for _name, _args in _SIGS.items():
     _fn = getattr(_lib, _name)

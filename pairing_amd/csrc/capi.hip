@@ -60,6 +60,10 @@ int gen_lanes(size_t n) {
 // the cooperative final exponentiation (sequential mul12 macros); larger ones
 // use the log-depth product tree first
 constexpr size_t kCoopProductMax = 16;
+// largest wNAF window the explicit-window fixed-base entries accept (the
+// reference's heuristics pick 2..16 for G1, 2..15 for G2; its wnaf_form keeps
+// a digit mod 2^(w+1) in a u64)
+constexpr int kMaxWnafWindow = 62;
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s, coop_vm());
@@ -828,8 +832,12 @@ int pa_g1_batch_normalization(pa_g1* v, size_t n) {
 }
 
 int pa_g1_wnaf_fixed_base(const pa_g1* base, const pa_fr_repr* scalars, size_t n, pa_g1* out) {
+    return pa_g1_wnaf_fixed_base_window(base, scalars, n, pa_g1_recommended_wnaf_for_num_scalars(n), out);
+}
+int pa_g1_wnaf_fixed_base_window(const pa_g1* base, const pa_fr_repr* scalars, size_t n, int window, pa_g1* out) {
     if (n == 0) return PA_OK;
     if (!base || !scalars || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (window < 1 || window > kMaxWnafWindow) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range");
     DevBuf db, ds, dt, dw, dout;
     int rc;
     if ((rc = upload(db, base, sizeof(pa_g1))) || (rc = upload(ds, scalars, sizeof(pa_fr_repr) * n))) return rc;
@@ -837,7 +845,7 @@ int pa_g1_wnaf_fixed_base(const pa_g1* base, const pa_fr_repr* scalars, size_t n
     PA_TRY(dw.alloc(8 * pa::g1_comb_workspace_words()), "device scratch");
     PA_TRY(dout.alloc(sizeof(pa_g1) * n), "device scratch");
     PA_TRY(pa::launch_g1_fixed_base(db.as<uint64_t>(), ds.as<uint64_t>(), dout.as<uint64_t>(), n, dt.as<uint64_t>(),
-                                    dw.as<uint64_t>(), call_stream()),
+                                    dw.as<uint64_t>(), window, call_stream()),
            "kernel launch");
     PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, sizeof(pa_g1) * n);
@@ -873,7 +881,8 @@ int pa_g1_fixed_base_table_device(const pa_g1* base, uint64_t* table, uint64_t* 
 int pa_g1_fixed_base_mul_device(const uint64_t* table, const pa_fr_repr* scalars, pa_g1* out, size_t n,
                                 void* stream) {
     if (n && (!table || !scalars || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
-    PA_TRY(pa::launch_g1_comb_mul(table, (const uint64_t*)scalars, (uint64_t*)out, n, (hipStream_t)stream),
+    PA_TRY(pa::launch_g1_comb_mul(table, (const uint64_t*)scalars, (uint64_t*)out, n,
+                                  pa_g1_recommended_wnaf_for_num_scalars(n), (hipStream_t)stream),
            "kernel launch");
     return PA_OK;
 }
@@ -886,15 +895,22 @@ int pa_g1_fixed_base_glv_mul_device(const pa_g1* base, const uint64_t* table, co
                                     const pa_fr_repr* scalars, pa_g1* out, size_t n, void* stream) {
     if (n && (!base || !table || !workspace || !scalars || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     PA_TRY(pa::launch_g1_glv_mul((const uint64_t*)base, table, workspace,
-                                 (const uint64_t*)scalars, (uint64_t*)out, n, (hipStream_t)stream),
+                                 (const uint64_t*)scalars, (uint64_t*)out, n, pa_g1_recommended_wnaf_for_num_scalars(n),
+                                 (hipStream_t)stream),
            "kernel launch");
     return PA_OK;
 }
 int pa_g1_wnaf_fixed_base_device(const pa_g1* base, const pa_fr_repr* scalars, pa_g1* out, size_t n,
                                  uint64_t* table, uint64_t* workspace, void* stream) {
+    return pa_g1_wnaf_fixed_base_window_device(base, scalars, out, n, pa_g1_recommended_wnaf_for_num_scalars(n), table,
+                                               workspace, stream);
+}
+int pa_g1_wnaf_fixed_base_window_device(const pa_g1* base, const pa_fr_repr* scalars, pa_g1* out, size_t n,
+                                        int window, uint64_t* table, uint64_t* workspace, void* stream) {
     if (n && (!base || !scalars || !out || !table || !workspace)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (window < 1 || window > kMaxWnafWindow) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range");
     PA_TRY(pa::launch_g1_fixed_base((const uint64_t*)base, (const uint64_t*)scalars, (uint64_t*)out, n, table,
-                                    workspace, (hipStream_t)stream),
+                                    workspace, window, (hipStream_t)stream),
            "kernel launch");
     return PA_OK;
 }
@@ -1207,24 +1223,34 @@ size_t pa_g2_fixed_base_table_words(void) { return pa::g2_comb_table_words(); }
 size_t pa_g2_fixed_base_workspace_words(void) { return pa::g2_comb_workspace_words(); }
 int pa_g2_wnaf_fixed_base_device(const pa_g2* base, const pa_fr_repr* scalars, pa_g2* out, size_t n,
                                  uint64_t* table, uint64_t* workspace, void* stream) {
+    return pa_g2_wnaf_fixed_base_window_device(base, scalars, out, n, pa_g2_recommended_wnaf_for_num_scalars(n), table,
+                                               workspace, stream);
+}
+int pa_g2_wnaf_fixed_base_window_device(const pa_g2* base, const pa_fr_repr* scalars, pa_g2* out, size_t n,
+                                        int window, uint64_t* table, uint64_t* workspace, void* stream) {
     if (n == 0) return PA_OK;
     if (!base || !scalars || !out || !table || !workspace) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (window < 1 || window > kMaxWnafWindow) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range");
     PA_TRY(pa::launch_g2_comb_table((const uint64_t*)base, table, workspace, (hipStream_t)stream), "kernel launch");
-    PA_TRY(pa::launch_g2_comb_mul(table, (const uint64_t*)scalars, (uint64_t*)out, n, (hipStream_t)stream),
+    PA_TRY(pa::launch_g2_comb_mul(table, (const uint64_t*)scalars, (uint64_t*)out, n, window, (hipStream_t)stream),
            "kernel launch");
     return PA_OK;
 }
 int pa_g2_wnaf_fixed_base(const pa_g2* base, const pa_fr_repr* scalars, size_t n, pa_g2* out) {
+    return pa_g2_wnaf_fixed_base_window(base, scalars, n, pa_g2_recommended_wnaf_for_num_scalars(n), out);
+}
+int pa_g2_wnaf_fixed_base_window(const pa_g2* base, const pa_fr_repr* scalars, size_t n, int window, pa_g2* out) {
     if (n == 0) return PA_OK;
     if (!base || !scalars || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    if (window < 1 || window > kMaxWnafWindow) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range");
     DevBuf db, ds, dt, dw, dout;
     int rc;
     if ((rc = upload(db, base, sizeof(pa_g2))) || (rc = upload(ds, scalars, sizeof(pa_fr_repr) * n))) return rc;
     PA_TRY(dt.alloc(8 * pa::g2_comb_table_words()), "device scratch");
     PA_TRY(dw.alloc(8 * pa::g2_comb_workspace_words()), "device scratch");
     PA_TRY(dout.alloc(sizeof(pa_g2) * n), "device scratch");
-    if ((rc = pa_g2_wnaf_fixed_base_device(db.as<pa_g2>(), ds.as<pa_fr_repr>(), dout.as<pa_g2>(), n,
-                                           dt.as<uint64_t>(), dw.as<uint64_t>(), call_stream())))
+    if ((rc = pa_g2_wnaf_fixed_base_window_device(db.as<pa_g2>(), ds.as<pa_fr_repr>(), dout.as<pa_g2>(), n, window,
+                                                  dt.as<uint64_t>(), dw.as<uint64_t>(), call_stream())))
         return rc;
     PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, sizeof(pa_g2) * n);

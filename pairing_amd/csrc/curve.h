@@ -250,6 +250,27 @@ PA_DEV void jac_double_3lane(Jac<F>& p, int lane) {
     sub(p.y, p.y, c8);
 }
 
+// wnaf_form's add_nocarry wrap (wnaf.rs:24-35).  Only the first digit can
+// wrap: for an odd repr s with s mod 2^(w+1) > 2^w the recoding adds
+// 2^(w+1) - (s mod 2^(w+1)), which overflows 2^256 exactly when bits w..255
+// of s are all ones; the digits then spell s - 2^256 = -(2^256 - s).  On such
+// an s this replaces s by t = 2^256 - s (< 2^w) and returns true, so the caller
+// multiplies by t and negates; window <= 0 keeps s (the exact product).
+PA_DEV bool wnaf_wrap(uint64_t s[4], int window) {
+    if (window <= 0 || window >= 64 || !(s[0] & 1)) return false;
+    const bool wraps = (s[0] | ((1ull << window) - 1)) == ~0ull && (s[1] & s[2] & s[3]) == ~0ull;
+    if (wraps) {
+        uint64_t c = 1;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t v = ~s[k] + c;
+            c = (c && v == 0) ? 1 : 0;
+            s[k] = v;
+        }
+    }
+    return wraps;
+}
+
 template <class F>
 PA_DEV void jac_negate(Jac<F>& p) {  // ec.rs:528-532
     if (!jac_is_zero(p)) neg(p.y, p.y);

@@ -28,7 +28,7 @@
 namespace pa {
 namespace {
 
-constexpr int kKernels = 6;
+constexpr int kKernels = 4;
 constexpr size_t kSlotBytes = 3584;  // one 14-limb spill slot for a 64-lane wave
 
 struct Workspace {
@@ -49,19 +49,15 @@ std::mutex g_mu;
 GenDevice g_dev[64];
 thread_local std::string g_detail;   // the code object that failed to load, for pa_last_error
 
-// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing; 4, 5: the
-// one-lane final exponentiation split around a binary-GCD inversion (norm,
-// then the rest with the inverse as input slot 12; tools/pgen/kernels.py)
+// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing
 const char* const kFile[kKernels] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco",
-                                     "pa_gen_miller_loop2.hsaco", "pa_gen_final_exp2.hsaco",
-                                     "pa_gen_fe_norm.hsaco", "pa_gen_fe_inv.hsaco"};
+                                     "pa_gen_miller_loop2.hsaco", "pa_gen_final_exp2.hsaco"};
 const char* const kName[kKernels] = {"pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2",
-                                     "pa_gen_final_exp2", "pa_gen_fe_norm", "pa_gen_fe_inv"};
+                                     "pa_gen_final_exp2"};
 const size_t kWaveBytes[kKernels] = {PA_GEN_MILLER_LOOP_MEM_SLOTS * kSlotBytes, PA_GEN_FINAL_EXP_MEM_SLOTS * kSlotBytes,
                                      PA_GEN_MILLER_LOOP2_MEM_SLOTS * kSlotBytes,
-                                     PA_GEN_FINAL_EXP2_MEM_SLOTS * kSlotBytes, PA_GEN_FE_NORM_MEM_SLOTS * kSlotBytes,
-                                     PA_GEN_FE_INV_MEM_SLOTS * kSlotBytes};
-const int kLanes[kKernels] = {1, 1, 2, 2, 1, 1};
+                                     PA_GEN_FINAL_EXP2_MEM_SLOTS * kSlotBytes};
+const int kLanes[kKernels] = {1, 1, 2, 2};
 
 // PA_GEN_DIR (A/B experiments with alternative generated code objects) overrides
 // the directory of libpairing_amd.so; PA_GEN_WS_SLOTS raises the workspace size
@@ -236,23 +232,13 @@ hipError_t launch_miller_loop_gen(int lanes, const uint64_t* p_aff, const uint64
                                   hipStream_t stream) {
     return launch(lanes == 2 ? 2 : 0, p_aff, q_aff, out, n, stream);
 }
-// One lane: the one-kernel final exponentiation (round 3: its inversions run
-// in the kernel by binary GCD and exp_by_x squares compressed, Karabina;
-// tools/pgen/kernels.py).  PA_FE_SPLIT=1 selects round 2's split form -- norm
-// kernel (Fq 0 of out), binary-GCD inversion in place, then the Granger-Scott
-// exponentiation reading that inverse -- which needs `out` apart from `in`.
+// One kernel per final exponentiation, in place or not (round 3: its
+// inversions run in the kernel by binary GCD and exp_by_x squares compressed,
+// Karabina; tools/pgen/kernels.py).  Round 2's form split around a separate
+// inversion kernel was removed in round 4.
 hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
                                 hipStream_t stream) {
-    static const bool split = [] {
-        const char* e = getenv("PA_FE_SPLIT");
-        return e && e[0] == '1';
-    }();
-    const bool apart = out + 72 * n <= in || in + 72 * n <= out;
-    if (lanes == 2 || !split || !apart) return launch(lanes == 2 ? 3 : 1, in, out, ok, n, stream);
-    hipError_t e;
-    if ((e = launch(4, in, out, nullptr, n, stream)) != hipSuccess) return e;
-    if ((e = launch_fq_inv_strided(out, 72, n, stream)) != hipSuccess) return e;
-    return launch(5, in, out, ok, n, stream);
+    return launch(lanes == 2 ? 3 : 1, in, out, ok, n, stream);
 }
 
 }  // namespace pa

@@ -218,12 +218,13 @@ __global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict
 __global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__ table_fl,
                                                     const uint64_t* __restrict__ scalars,
                                                     uint64_t* __restrict__ out, size_t n, int w0, int w1,
-                                                    int first) {
+                                                    int first, int window) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t s[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
+    const bool flip = wnaf_wrap(s, window);   // the reference's digits spell -(2^256 - s)
     uint64_t* o = out + (size_t)kG1Jac * i;
     FlJac acc;
     bool untouched = true, changed = false;
@@ -257,7 +258,7 @@ __global__ void __launch_bounds__(64) k_g1_comb_mul(const uint64_t* __restrict__
                 ty.w[2 * k + 1] = b.y;
             }
             if (tx.w[0] != kFlInfinity) {  // adding the identity is add_assign_mixed's no-op
-                const F<2> oy = d < 0 ? neg(ty) : relax<2>(ty);
+                const F<2> oy = (d < 0) != flip ? neg(ty) : relax<2>(ty);
                 fl_jac_add_mixed(acc, untouched, tx, oy);
                 changed = true;
             }
@@ -383,12 +384,13 @@ PA_DEV void comb_add_entry(FlJac& acc, bool& untouched, bool& changed, const uin
 __global__ void __launch_bounds__(64) k_g1_glv_mul(const uint64_t* __restrict__ table_fl,
                                                    const uint64_t* __restrict__ scalars, uint64_t* __restrict__ out,
                                                    size_t n, int w0, int w1, int first,
-                                                   const uint32_t* __restrict__ gate) {
+                                                   const uint32_t* __restrict__ gate, int window) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || (gate && *gate != kGateGlv)) return;
     uint64_t s[4], rem[3], q[3];
 #pragma unroll
     for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
+    const int neg = wnaf_wrap(s, window) ? 1 : 0;   // -(2^256 - s): every digit negated
     glv_split(s, rem, q);
     uint64_t* o = out + (size_t)kG1Jac * i;
     FlJac acc;
@@ -421,7 +423,8 @@ __global__ void __launch_bounds__(64) k_g1_glv_mul(const uint64_t* __restrict__ 
         } else {
             d = dq;
         }
-        if (d != 0) comb_add_entry(acc, untouched, changed, table_fl, (step & 1) * kGlvWindows + win, d, step & 1);
+        if (d != 0)
+            comb_add_entry(acc, untouched, changed, table_fl, (step & 1) * kGlvWindows + win, d, (step & 1) ^ neg);
     }
     if (!first && !changed) return;
     if (untouched) {
@@ -441,15 +444,19 @@ __global__ void __launch_bounds__(64) k_g1_glv_mul(const uint64_t* __restrict__ 
 __global__ void __launch_bounds__(64) k_g1_fixed_base_ladder(const uint64_t* __restrict__ base,
                                                              const uint64_t* __restrict__ scalars,
                                                              uint64_t* __restrict__ out, size_t n,
-                                                             const uint32_t* __restrict__ gate) {
+                                                             const uint32_t* __restrict__ gate, int window) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || *gate != kGatePlain) return;
-    const FlJac p = fl_load_jac(base);
+    uint64_t s[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
+    FlJac p = fl_load_jac(base);
+    if (wnaf_wrap(s, window)) p.y = red(neg(p.y));   // (2^256 - s) (-P)
     FlJac acc = {fl_zero(), fl_one(), fl_zero()};
 #pragma unroll 1
     for (int bit = 255; bit >= 0; bit--) {
         if (!fl_is_zero(acc.z)) fl_jac_double(acc);
-        if ((scalars[4 * i + (bit >> 6)] >> (bit & 63)) & 1) fl_jac_add(acc, p);
+        if ((s[bit >> 6] >> (bit & 63)) & 1) fl_jac_add(acc, p);
     }
     uint64_t* o = out + (size_t)kG1Jac * i;
     if (fl_is_zero(acc.z)) {
@@ -497,10 +504,10 @@ hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_fl, uint64
 }
 
 hipError_t launch_g1_comb_mul(const uint64_t* table_fl, const uint64_t* scalars, uint64_t* out, size_t n,
-                              hipStream_t stream) {
+                              int window, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_g1_comb_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_fl, scalars, out, n, 0,
-                       kCombWindows, 1);
+                       kCombWindows, 1, window);
     return hipGetLastError();
 }
 
@@ -508,9 +515,9 @@ hipError_t launch_g1_comb_mul(const uint64_t* table_fl, const uint64_t* scalars,
 // failed the membership check (a base outside G1: the reference's types never
 // hold one, so throughput does not matter there, the launch count does)
 static hipError_t glv_fallback(const uint64_t* base, const uint64_t* workspace, const uint64_t* scalars, uint64_t* out,
-                               size_t n, hipStream_t stream) {
+                               size_t n, int window, hipStream_t stream) {
     hipLaunchKernelGGL(k_g1_fixed_base_ladder, dim3(blocks_for(n, 64)), dim3(64), 0, stream, base, scalars, out, n,
-                       glv_flag(workspace));
+                       glv_flag(workspace), window);
     return hipGetLastError();
 }
 
@@ -522,13 +529,13 @@ hipError_t launch_g1_glv_table(const uint64_t* base, uint64_t* table_fl, uint64_
 }
 
 hipError_t launch_g1_glv_mul(const uint64_t* base, const uint64_t* table_fl, const uint64_t* workspace, const uint64_t* scalars,
-                             uint64_t* out, size_t n, hipStream_t stream) {
+                             uint64_t* out, size_t n, int window, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_g1_glv_mul, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table_fl, scalars, out, n, 0,
-                       kGlvWindows, 1, glv_flag(workspace));
+                       kGlvWindows, 1, glv_flag(workspace), window);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return glv_fallback(base, workspace, scalars, out, n, stream);
+    return glv_fallback(base, workspace, scalars, out, n, window, stream);
 }
 
 // Table + multiply in one call, GLV form with the serial base chain
@@ -540,7 +547,7 @@ hipError_t launch_g1_glv_mul(const uint64_t* base, const uint64_t* table_fl, con
 // (k_g1_fixed_base_ladder), which returns at once unless the check failed.
 // Equal as points to launch_g1_comb_table + launch_g1_comb_mul.
 hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
-                                uint64_t* table_fl, uint64_t* workspace, hipStream_t stream) {
+                                uint64_t* table_fl, uint64_t* workspace, int window, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -611,12 +618,12 @@ hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, u
         for (int p = 0; p < parts && err == hipSuccess; p++) {
             if (!ck(hipStreamWaitEvent(mul, ev[2 + 2 * p], 0))) break;
             hipLaunchKernelGGL(k_g1_glv_mul, dim3(blocks_for(n, 64)), dim3(64), 0, mul, table_fl, scalars, out, n,
-                               wb[p], wb[p + 1], p == 0 ? 1 : 0, nullptr);
+                               wb[p], wb[p + 1], p == 0 ? 1 : 0, nullptr, window);
             ck(hipGetLastError());
         }
         // fallback: the double-and-add ladder, live only when the base failed the check
         if (err == hipSuccess && ck(hipStreamWaitEvent(mul, ev[1 + 2 * parts], 0)))
-            ck(glv_fallback(base, workspace, scalars, out, n, mul));
+            ck(glv_fallback(base, workspace, scalars, out, n, window, mul));
     }
     for (int k = 0; k < made; k++) (void)hipEventDestroy(ev[k]);
     return err;

@@ -273,26 +273,6 @@ __global__ void __launch_bounds__(64) k_fq12_mul_by_014(const uint64_t* __restri
     store(out + 72 * i, z);
 }
 
-// Split final exponentiation (gen_launch.hip): the base-field inversion of
-// f^-1 (fq12.rs:132-148 -> fq2.rs:138-155) by binary GCD between the two
-// generated kernels, in place on Fq 0 of each 576-byte out record -- the norm
-// kernel wrote it there, the inverse kernel reads it back as input slot 12.
-// Zero (f == 0, reference None) stays zero; the inverse kernel's ok byte
-// comes from f itself.  One lane per record, 256-lane blocks.
-__global__ void __launch_bounds__(256) k_fq_inv_strided(uint64_t* __restrict__ v, size_t stride, size_t n) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Fq x, z;
-    fq_load(x, v + stride * i);
-    if (!fq_inv(z, x)) fq_zero(z);
-    fq_store(v + stride * i, z);
-}
-hipError_t launch_fq_inv_strided(uint64_t* v, size_t stride, size_t n, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fq_inv_strided, dim3(blocks_for(n, 256)), dim3(256), 0, stream, v, stride, n);
-    return hipGetLastError();
-}
-
 hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n,
                                hipStream_t stream) {
     if (n == 0) return hipSuccess;

@@ -237,13 +237,14 @@ __global__ void __launch_bounds__(64) k_comb_pack(const uint64_t* __restrict__ t
 // next window), mixed additions from zero (madd-2007-bl, ec.rs:446-526)
 template <int G>
 __global__ void __launch_bounds__(64) k_comb_mul(const uint64_t* __restrict__ table, const uint64_t* __restrict__ scalars,
-                                                 uint64_t* __restrict__ out, size_t n) {
+                                                 uint64_t* __restrict__ out, size_t n, int window) {
     using F = typename Grp<G>::F;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t s[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
+    const bool flip = wnaf_wrap(s, window);   // the reference's digits spell -(2^256 - s)
     Jac<F> acc;
     jac_zero(acc);
     int carry = 0;
@@ -256,7 +257,7 @@ __global__ void __launch_bounds__(64) k_comb_mul(const uint64_t* __restrict__ ta
         if (d == 0) continue;
         Aff<F> t;
         load_aff(t, table + (size_t)Grp<G>::AW * (win * kCombEntries + (d < 0 ? -d : d) - 1));
-        if (d < 0 && !t.inf) neg(t.y, t.y);
+        if ((d < 0) != flip && !t.inf) neg(t.y, t.y);
         jac_add_mixed(acc, t);
     }
     store_jac(out + (size_t)Grp<G>::JW * i, acc);
@@ -293,9 +294,9 @@ hipError_t launch_g2_comb_table(const uint64_t* base, uint64_t* table, uint64_t*
 }
 
 hipError_t launch_g2_comb_mul(const uint64_t* table, const uint64_t* scalars, uint64_t* out, size_t n,
-                              hipStream_t stream) {
+                              int window, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_comb_mul<2>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table, scalars, out, n);
+    hipLaunchKernelGGL(k_comb_mul<2>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table, scalars, out, n, window);
     return hipGetLastError();
 }
 

@@ -76,9 +76,6 @@ const char* gen_error_detail();
 // event, so concurrent launches on different streams never share one.
 hipError_t launch_miller_loop_gen(int lanes, const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                   hipStream_t stream);
-// in-place Fq inversion (binary GCD) of Fq 0 of n records `stride` u64 apart
-// (the split final exponentiation's middle step; zero stays zero)
-hipError_t launch_fq_inv_strided(uint64_t* v, size_t stride, size_t n, hipStream_t stream);
 hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
                                 hipStream_t stream);
 // Cooperative kernels (kernels_coop.hip): a workgroup per pairing, for small
@@ -109,20 +106,21 @@ hipError_t launch_sqrt(int degree, const uint64_t* in, size_t n, uint64_t* out, 
 hipError_t launch_g1_batch_normalize(uint64_t* v, size_t n, hipStream_t stream);
 // fixed-base comb: table (g1_comb_table_words() u64) built from `base` using
 // `workspace` (g1_comb_workspace_words() u64); then out[i] = scalars[i] * base
+// -- the wNAF point of window `window` (wnaf_wrap in curve.h; 0 = exact s * base)
 size_t g1_comb_table_words();
 size_t g1_comb_workspace_words();
 hipError_t launch_g1_comb_table(const uint64_t* base, uint64_t* table_aff, uint64_t* workspace, hipStream_t stream);
 hipError_t launch_g1_comb_mul(const uint64_t* table_aff, const uint64_t* scalars, uint64_t* out, size_t n,
-                              hipStream_t stream);
+                              int window, hipStream_t stream);
 // GLV form as two stages on one stream (table rows + phi rows + membership
 // flag; multiply, with a double-and-add fallback for a base that failed the check)
 hipError_t launch_g1_glv_table(const uint64_t* base, uint64_t* table, uint64_t* workspace, hipStream_t stream);
 hipError_t launch_g1_glv_mul(const uint64_t* base, const uint64_t* table, const uint64_t* workspace, const uint64_t* scalars,
-                             uint64_t* out, size_t n, hipStream_t stream);
+                             uint64_t* out, size_t n, int window, hipStream_t stream);
 // both in one call, the GLV table's serial base chain overlapped with the
 // multiply (side streams per device; equal as points)
 hipError_t launch_g1_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n,
-                                uint64_t* table, uint64_t* workspace, hipStream_t stream);
+                                uint64_t* table, uint64_t* workspace, int window, hipStream_t stream);
 
 // CurveProjective / CurveAffine per-op batches for G1 (group 1) and G2
 // (group 2), kernels_group.hip.  Records: Jacobian 18 / 36 u64, affine
@@ -149,7 +147,7 @@ size_t g2_comb_table_words();
 size_t g2_comb_workspace_words();
 hipError_t launch_g2_comb_table(const uint64_t* base, uint64_t* table, uint64_t* workspace, hipStream_t stream);
 hipError_t launch_g2_comb_mul(const uint64_t* table, const uint64_t* scalars, uint64_t* out, size_t n,
-                              hipStream_t stream);
+                              int window, hipStream_t stream);
 
 // Scalar field Fr (kernels_fr.hip).  `flag` receives the Option / Result byte
 // (inverse, from_repr, sqrt) or the LegendreSymbol as int8 (0, 1, -1);

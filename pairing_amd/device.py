@@ -166,14 +166,19 @@ def g1_fixed_base_glv_mul(base, table, ws, scalars, out, stream=None):
     call("pa_g1_fixed_base_glv_mul_device", *args, n, _stream_ptr(stream))
 
 
-def g1_wnaf_fixed_base(base, scalars, out, table, ws, stream=None):
-    """out[i] = scalars[i] * base with the table built in the same call (its
-    serial base chain overlapped with the multiply); table / ws as returned by
-    fixed_base_buffers()."""
+def g1_wnaf_fixed_base(base, scalars, out, table, ws, stream=None, window=None):
+    """out[i] = the reference's wNAF product scalars[i] * base (its wnaf_form
+    wrap included; `window` default recommended_wnaf_for_num_scalars(n)) with
+    the table built in the same call (its serial base chain overlapped with the
+    multiply); table / ws as returned by fixed_base_buffers()."""
     n = scalars.shape[0]
     args = (_dptr(base, W_G1, "base"), _dptr(scalars, 4, "scalars"), _dptr(out, W_G1, "out"))
     _rows(out, n, "out")
-    call("pa_g1_wnaf_fixed_base_device", *args, n, *_fb_table(table, ws), _stream_ptr(stream))
+    if window is None:
+        call("pa_g1_wnaf_fixed_base_device", *args, n, *_fb_table(table, ws), _stream_ptr(stream))
+    else:
+        call("pa_g1_wnaf_fixed_base_window_device", *args, n, int(window), *_fb_table(table, ws),
+             _stream_ptr(stream))
 
 
 def fixed_base_buffers(dev):
@@ -198,14 +203,18 @@ def g2_fixed_base_buffers(dev):
     return table, ws
 
 
-def g2_wnaf_fixed_base(base, scalars, out, table, ws, stream=None):
-    """out[i] = scalars[i] * base for G2 (base a (1,36) Jacobian record)."""
+def g2_wnaf_fixed_base(base, scalars, out, table, ws, stream=None, window=None):
+    """out[i] = the reference's wNAF product scalars[i] * base for G2 (base a
+    (1,36) Jacobian record; `window` as in g1_wnaf_fixed_base)."""
     n = scalars.shape[0]
     args = (_dptr(base, W_G2, "base"), _dptr(scalars, 4, "scalars"), _dptr(out, W_G2, "out"))
     _rows(out, n, "out")
-    call("pa_g2_wnaf_fixed_base_device", *args, n,
-         _words(table, int(_lib.pa_g2_fixed_base_table_words()), "table"),
-         _words(ws, int(_lib.pa_g2_fixed_base_workspace_words()), "ws"), _stream_ptr(stream))
+    tw = (_words(table, int(_lib.pa_g2_fixed_base_table_words()), "table"),
+          _words(ws, int(_lib.pa_g2_fixed_base_workspace_words()), "ws"))
+    if window is None:
+        call("pa_g2_wnaf_fixed_base_device", *args, n, *tw, _stream_ptr(stream))
+    else:
+        call("pa_g2_wnaf_fixed_base_window_device", *args, n, int(window), *tw, _stream_ptr(stream))
 
 
 def group_add(group, a, b, out, stream=None):

@@ -327,6 +327,19 @@ static void curve_tests(int iters) {
             EXPECT(Wnaf::new_().scalar(sc[k]).base(g) == e);
         }
         EXPECT(P::recommended_wnaf_for_num_scalars(1 << 18) >= 15);
+        // wnaf.rs:30-35: an odd repr with bits w..255 set wraps to s - 2^256
+        const uint64_t ones = ~0ULL;
+        const size_t w = wb.window();
+        P neg_g = g;
+        neg_g.negate();
+        const FrRepr all_ones(ones, ones, ones, ones);
+        const FrRepr no_wrap(ones << (w + 1) | 1, ones, ones, ones);   // bit w clear: plain s * g
+        auto edge = shared.scalars({all_ones, no_wrap});
+        EXPECT(edge[0] == neg_g);
+        P e = g;
+        e.mul_assign(no_wrap);
+        EXPECT(edge[1] == e);
+        EXPECT(Wnaf::new_().scalar(all_ones).base(g) == neg_g);
     }
 }
 

@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import Q, R_ORDER, limbs, rng
+from helpers import Q, R_ORDER, limbs, random_scalars, rng
 
 pytestmark = pytest.mark.gpu
 
@@ -296,14 +296,15 @@ def test_g1_glv_stages_device_match_oracle(gpu, oracle, which):
     np.testing.assert_array_equal(oracle.g1_batch_normalization(got1), oracle.g1_batch_normalization(got2))
 
 
-def test_final_exp_split_and_in_place_agree(gpu, oracle):
-    """out apart from in runs the split final exponentiation (norm kernel,
-    binary-GCD inversion, rest); out == in runs the one-kernel form.  Both
-    equal the oracle, including f == 0 (reference None: zero, ok = 0)."""
+def test_final_exp_apart_and_in_place_agree(gpu, oracle):
+    """pa_final_exponentiation_batch_device with out apart from in and with
+    out == in (both run the one generated kernel, pa_gen_final_exp, at this
+    size on variant 3): both equal the oracle, including f == 0 (reference
+    None: zero, ok = 0), and `in` is left unchanged when apart."""
     import torch
     import pairing_amd.device as pdev
     n = 2300
-    gpu.set_pairing_kernel(3)   # the one-lane generated kernels, whose FE has the split form
+    gpu.set_pairing_kernel(3)   # the one-lane generated kernels
     try:
         f = _field_rows(41, n * 12, 6, FQ_TOP, [1]).reshape(n, 72)
         f[7] = 0
@@ -319,6 +320,7 @@ def test_final_exp_split_and_in_place_agree(gpu, oracle):
     finally:
         gpu.set_pairing_kernel(0)
     np.testing.assert_array_equal(_host(out), exp)
+    np.testing.assert_array_equal(_host(d_in), f)
     np.testing.assert_array_equal(_host(d_same), exp)
     np.testing.assert_array_equal(ok.cpu().numpy(), np.asarray(ok_exp, np.uint8))
     np.testing.assert_array_equal(ok2.cpu().numpy(), np.asarray(ok_exp, np.uint8))
@@ -375,27 +377,87 @@ def test_config3_full_size_bit_exact(gpu, oracle):
     np.testing.assert_array_equal(_host(out), exp)
 
 
-def test_fixed_base_wrapping_reprs_documented_divergence(gpu, oracle):
-    """the one documented divergence of pa_g1_wnaf_fixed_base (pairing_amd.h):
-    for raw 256-bit reprs within 2^w of 2^256 the reference's wnaf_form wraps in
-    add_nocarry (wnaf.rs:30-35) -- s = 2^256 - 1 becomes the digit string [-1],
-    i.e. -g -- while the GPU multiplies exactly, s g = (s mod r) g.  No
-    Fr::into_repr output is that large.  Pinned here on both sides."""
+def _wrap_scalars(w, g):
+    """reprs at the edge of wnaf_form's add_nocarry wrap for window w
+    (wnaf.rs:24-35: an odd s with bits w..255 all ones wraps to s - 2^256),
+    both sides of it, and random reprs"""
+    top = 1 << 256
+    vals = [top - 1, top - 2, top - (1 << w) - 1, top - (1 << (w + 1)) + 1, top - (1 << w) + 1,
+            top - (1 << w) + 3, top - 3, top - (1 << w), R_ORDER - 1, 0, 1]
+    s = np.array([limbs(v, 4) for v in vals], np.uint64)
+    return np.concatenate([s, random_scalars(g, 21, bits=256)])
+
+
+def _wraps(v, w):
+    return v & 1 and (v >> w) == (1 << (256 - w)) - 1
+
+
+@pytest.mark.parametrize("w", [4, 9, 16])
+def test_fixed_base_wrapping_reprs_equal_reference(gpu, oracle, w):
+    """pa_g1_wnaf_fixed_base_window_device reproduces the reference's wnaf_form
+    wrap (wnaf.rs:24-35, 93-107, 169-178): where the first negative digit's
+    add_nocarry overflows 2^256 the reference multiplies by s - 2^256 (e.g. -g
+    for s = 2^256 - 1).  Equal as points to the oracle's Wnaf::base(g, .)
+    .scalar(s) with the same window -- w = 16 is the window of the benched
+    2^18 batch -- for a base in G1 (GLV comb) and one outside (the
+    double-and-add fallback); the default-window entry at its own n, the
+    two-stage GLV and plain-comb entries too."""
     import torch
     import pairing_amd.device as pdev
-    base_np, _ = _config3_inputs(1)
-    s = np.array([limbs((1 << 256) - 1, 4), limbs((1 << 256) - 2, 4), limbs(R_ORDER - 1, 4)], np.uint64)
-    out = pdev.empty_records(3, 18, "cuda:0")
+    import decode_cases as D
+    from helpers import mont, Q
+    g = rng(70 + w)
+    s = _wrap_scalars(w, g)
+    vals = [sum(int(x) << (64 * k) for k, x in enumerate(r)) for r in s]
+    assert sum(_wraps(v, w) for v in vals) == 4
+    base_in, _ = _config3_inputs(1)
+    pts, truth = D.subgroup_points(1, seed=61, n=2)
+    x, y = next(P for P, t in zip(pts, truth) if not t)
+    z = 0x1234567
+    base_out = np.array([mont(x * z * z % Q) + mont(y * z * z * z % Q) + mont(z)], np.uint64)
     table, ws = pdev.fixed_base_buffers("cuda:0")
-    pdev.g1_wnaf_fixed_base(_dev(base_np), _dev(s), out, table, ws)
+    for base_np in (base_in, base_out):
+        out = pdev.empty_records(len(s), 18, "cuda:0")
+        pdev.g1_wnaf_fixed_base(_dev(base_np), _dev(s), out, table, ws, window=w)
+        torch.cuda.synchronize()
+        exp = oracle.g1_wnaf_fixed_base(base_np, s, window=w)
+        assert oracle.g1_eq(_host(out), exp).all()
+    neg_g = oracle.g1_mul(base_in, np.array([limbs(R_ORDER - 1, 4)], np.uint64))
+    assert oracle.g1_eq(oracle.g1_wnaf_fixed_base(base_in, s[:1], window=w), neg_g).all()   # s = 2^256 - 1: -g
+    # default window (recommended_wnaf_for_num_scalars(n)) through every G1 fixed-base entry
+    n = len(s)
+    wd = oracle.lib().o_g1_recommended_wnaf_for_num_scalars(n)
+    sd = _wrap_scalars(wd, g)
+    exp = oracle.g1_wnaf_fixed_base(base_in, sd)
+    b, sc = _dev(base_in), _dev(sd)
+    outs = [pdev.empty_records(n, 18, "cuda:0") for _ in range(3)]
+    pdev.g1_wnaf_fixed_base(b, sc, outs[0], table, ws)
+    pdev.g1_fixed_base_glv_table(b, table, ws)
+    pdev.g1_fixed_base_glv_mul(b, table, ws, sc, outs[1])
+    table2, _ = pdev.g1_fixed_base_table(b)
+    pdev.g1_fixed_base_mul(table2, sc, outs[2])
     torch.cuda.synchronize()
-    got = _host(out)
-    ref = oracle.g1_wnaf_fixed_base(base_np, s)
-    exact = oracle.g1_mul(np.repeat(base_np, 3, axis=0),
-                          np.array([limbs(((1 << 256) - 1) % R_ORDER, 4), limbs(((1 << 256) - 2) % R_ORDER, 4),
-                                    limbs(R_ORDER - 1, 4)], np.uint64))
-    assert oracle.g1_eq(got, exact).all()
-    neg_g = oracle.g1_mul(base_np, np.array([limbs(R_ORDER - 1, 4)], np.uint64))
-    assert oracle.g1_eq(ref[:1], neg_g).all()          # the reference's wrap: -g
-    assert not oracle.g1_eq(got[:1], ref[:1]).any()     # ... which the GPU does not reproduce
-    assert oracle.g1_eq(got[2:], ref[2:]).all()         # r - 1 is an ordinary repr: equal
+    for o in outs:
+        assert oracle.g1_eq(_host(o), exp).all()
+
+
+@pytest.mark.parametrize("w", [4, 15])
+def test_g2_fixed_base_wrapping_reprs_equal_reference(gpu, oracle, w):
+    """G2: the same wrap through pa_g2_wnaf_fixed_base_window_device (w = 15 is
+    the G2 window at 2^18) and the default-window pa_g2_wnaf_fixed_base_device"""
+    import torch
+    import pairing_amd.device as pdev
+    g = rng(80 + w)
+    base = oracle.g2_from_affine(oracle.g2_mul_generator(np.array([limbs(5, 4)], np.uint64)))
+    s = _wrap_scalars(w, g)
+    table, ws = pdev.g2_fixed_base_buffers("cuda:0")
+    out = pdev.empty_records(len(s), 36, "cuda:0")
+    pdev.g2_wnaf_fixed_base(_dev(base), _dev(s), out, table, ws, window=w)
+    torch.cuda.synchronize()
+    assert oracle.g2_eq(_host(out), oracle.g2_wnaf_fixed_base(base, s, window=w)).all()
+    wd = oracle.lib().o_g2_recommended_wnaf_for_num_scalars(len(s))
+    sd = _wrap_scalars(wd, g)
+    out2 = pdev.empty_records(len(sd), 36, "cuda:0")
+    pdev.g2_wnaf_fixed_base(_dev(base), _dev(sd), out2, table, ws)
+    torch.cuda.synchronize()
+    assert oracle.g2_eq(_host(out2), oracle.g2_wnaf_fixed_base(base, sd)).all()

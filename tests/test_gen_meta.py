@@ -14,8 +14,7 @@ from elfsym import read_u32, symbol_offset
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "pairing_amd", "lib")
-KERNELS = ["pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2", "pa_gen_final_exp2",
-           "pa_gen_fe_norm", "pa_gen_fe_inv"]
+KERNELS = ["pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2", "pa_gen_final_exp2"]
 
 
 def meta_slots():

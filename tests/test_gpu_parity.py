@@ -329,10 +329,8 @@ def test_g1_fixed_base_overlapped_halves(gpu, oracle, zero_base):
     s[0] = 0
     s[1] = limbs(1, 4)
     s[2] = limbs(R_ORDER - 1, 4)
-    # (not 2^256 - 1: the reference's wnaf_form adds 2^w to the repr with
-    # add_nocarry, which wraps for reprs this close to 2^256 -- a value no
-    # Fr::into_repr produces; the GPU computes s * base there)
     s[3] = limbs((1 << 255) - 1, 4)
+    s[8] = limbs((1 << 256) - 1, 4)    # wnaf_form's add_nocarry wraps (wnaf.rs:30-35): -base
     s[4] = limbs(1 << 200, 4)          # only the high half
     s[5] = limbs((1 << 130) - 1, 4)    # low half + carry into window 17
     s[6] = limbs(0x80 << 128, 4)       # digit 128 at window 16, no carry

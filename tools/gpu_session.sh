@@ -36,12 +36,10 @@ for step in "$@"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         benchnc) run bench_nc 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
-        benchsplit) run bench_split 300 env PA_FE_SPLIT=1 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         verifybench) run bench_verify 300 python bench.py --workload verify --steps 10 --warmup 2 --no-cpu-baseline ;;
         fqsoa) run bench_fq_soa 300 python bench.py --workload fq_mul --layout soa --steps 20 --warmup 3 --no-cpu-baseline ;;
         proffqsoa) run prof_fq_soa 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fq_soa -o run -- python bench.py --workload fq_mul --layout soa --steps 10 --warmup 2 --no-cpu-baseline ;;
         soatests) run pytest_soa 300 python -u -m pytest tests/test_bench_sizes.py -m gpu -k "soa or fq_mul" -v --timeout 120 --timeout-method thread ;;
-        benchnosplit) run bench_nosplit 600 env PA_FE_SPLIT=0 python bench.py --no-cpu-baseline ;;
         rcclbench) run bench_rccl1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --no-cpu-baseline ;;
         benchgen2) run bench_gen2 600 env PA_PAIRING_KERNEL=1 python bench.py --no-cpu-baseline ;;
         wnafbench) run bench_wnaf 300 python bench.py --workload wnaf --steps 5 --warmup 1 ;;

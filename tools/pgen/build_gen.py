@@ -87,8 +87,8 @@ PROGRAMS = {
     # PGEN_FE_LAZY=0 / 1 builds the plain / fully lazy tower instead (A/B experiments)
     "fe": _mk(lambda: kernels.final_exp_prog(lazy={"sq": "sq", "0": False, "1": True}[os.environ.get("PGEN_FE_LAZY", "sq")]),
               kcfg.FinalExpCfg, "pa_gen_final_exp"),
-    # the final exponentiation split around a binary-GCD base-field inversion
-    # (gen_launch.hip: norm kernel -> k_fq_inv_strided -> inv kernel)
+    # round 2's final exponentiation split around a separate base-field
+    # inversion (no longer loaded by gen_launch.hip; built only on request)
     "fen": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="norm"), kcfg.FinalExpCfg, "pa_gen_fe_norm"),
     "fei": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="inv"), kcfg.FinalExpCfg, "pa_gen_fe_inv"),
     "ml2": _mk(lambda: kernels.miller_loop_prog(lanes=2), kcfg.MillerLoopCfg2, "pa_gen_miller_loop2"),
@@ -172,17 +172,16 @@ def main():
         del args[i:i + 2]
     os.makedirs(outdir, exist_ok=True)
     meta = {}
-    for w in args or ["ml", "fe", "fen", "fei", "ml2", "fe2"]:
+    for w in args or ["ml", "fe", "ml2", "fe2"]:
         build(w, outdir)
         meta[w] = PROGRAMS[w].cache["r"][3]
     if "ml" in meta and "fe" in meta:
         write_work_json(outdir)
-    if all(k in meta for k in ("ml", "fe", "fen", "fei", "ml2", "fe2")):
+    if all(k in meta for k in ("ml", "fe", "ml2", "fe2")):
         hdr = os.path.join(ROOT, "pairing_amd", "csrc", "pa_gen_meta.h")
         with open(hdr, "w") as f:
             f.write("// GENERATED by tools/pgen/build_gen.py -- spill workspace per wave (M slots)\n#pragma once\n")
-            for k, name in (("ml", "MILLER_LOOP"), ("fe", "FINAL_EXP"), ("ml2", "MILLER_LOOP2"), ("fe2", "FINAL_EXP2"),
-                            ("fen", "FE_NORM"), ("fei", "FE_INV")):
+            for k, name in (("ml", "MILLER_LOOP"), ("fe", "FINAL_EXP"), ("ml2", "MILLER_LOOP2"), ("fe2", "FINAL_EXP2")):
                 f.write("#define PA_GEN_%s_MEM_SLOTS %d\n" % (name, meta[k]))
 
 
