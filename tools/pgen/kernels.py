@@ -312,6 +312,40 @@ def hard_part_loop(p, T, V, r):
     return T.mul12(y1, T.frob12(V.get12("y2"), 1))
 
 
+def hard_part_loop_folded(p, T, V, r):
+    """mod.rs:125-156 as hard_part_loop, with every factor of the result folded
+    into one accumulator `u` as soon as it exists, so at most two Fq12 values
+    are parked across an exp_by_x (hard_part_loop parks up to four).  With
+    E = exp_by_x (a homomorphism on the cyclotomic subgroup, conj = inverse):
+      a: y1 = E(r^2)            b: y2 = E'(y1);  Y = conj(y1) r y2   (y1 of mod.rs:133-135)
+      c: y2 = E(Y)              d: z = E(y2)  (mod.rs' y3 = z conj(Y))
+      e: E(y3) = E(z) conj(y2)
+    result = Y^(q^3) y2^(q^2) (z conj(Y))^q E(z) conj(y2) r^3
+           = [Y^(q^3) conj(Y)^q r^3]_b [y2^(q^2) conj(y2)]_c [z^q]_d E(z)_e.
+    u holds r until b, then the accumulated product; v holds y1 from a to b."""
+    H = os.environ.get("PGEN_HP_HOME", "M")
+    for n in ("u", "v", "x"):
+        V.declare12(n, H)
+    V.set12("u", r)
+    V.set12("x", T.cyc_sqr(r))
+    with p.loop(5) as L:
+        exp_by_x_karabina(p, T, V, "x", L, first_skip=3)
+        with p.if_bit(1 << 4, L):          # after a: y1 = E(r^2)
+            V.set12("v", V.get12("x"))
+        with p.if_bit(1 << 3, L):          # after b: Y = conj(y1 conj(r)) y2; u = Y^(q^3) conj(Y)^q r^3
+            r_ = V.get12("u")
+            y = T.mul12(T.conj12(T.mul12(V.get12("v"), T.conj12(r_))), V.get12("x"))
+            V.set12("x", y)
+            r3 = T.mul12(T.cyc_sqr(r_), r_)
+            V.set12("u", T.mul12(T.mul12(T.frob12(y, 3), T.frob12(T.conj12(y), 1)), r3))
+        with p.if_bit(1 << 2, L):          # after c: u *= y2^(q^2) conj(y2)
+            y2 = V.get12("x")
+            V.set12("u", T.mul12(V.get12("u"), T.mul12(T.frob12(y2, 2), T.conj12(y2))))
+        with p.if_bit(1 << 1, L):          # after d: u *= z^q
+            V.set12("u", T.mul12(V.get12("u"), T.frob12(V.get12("x"), 1)))
+    return T.mul12(V.get12("u"), V.get12("x"))
+
+
 def _karabina():
     return os.environ.get("PGEN_KARABINA", "1") == "1"
 
@@ -358,7 +392,8 @@ def final_exp_prog(lanes=1, lazy=False, tower_cls=None, split=None):
     f2 = r
     r = T.mul12(T.frob12(r, 2), f2)
     if kara:
-        V.store12(hard_part_loop(p, T, V, r))
+        hp = hard_part_loop_folded if os.environ.get("PGEN_HP_FOLD", "0") == "1" else hard_part_loop
+        V.store12(hp(p, T, V, r))
         return p
     x = X_ABS
     y0 = T.cyc_sqr(r)
