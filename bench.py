@@ -72,6 +72,9 @@ def parse():
                     default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--decode", action="store_true",
+                    help="verify: start from the pairs' compressed encodings and decode them (checked: "
+                         "on-curve + subgroup, ec.rs:785-837, 1448-1509) before the multi_pairing")
     ap.add_argument("--layout", choices=["aos", "soa"], default="aos",
                     help="fq_mul: device layout of the operands (SURVEY.md 8(d) config 2 names SoA)")
     ap.add_argument("--cpu-stub", action="store_true",
@@ -605,10 +608,30 @@ def main():
         out = pdev.empty_records(1, 72, dev)
         okb = torch.empty(1, dtype=torch.uint8, device=dev)
         work = pdev.empty_records(n, 72, dev)
+        if args.decode:
+            # the verifier's front end: the proof's points arrive compressed;
+            # G1 decodes on a side stream beside G2, the pairing waits for both
+            enc1_np = pairing_amd.g1_encode(p_np, True)
+            enc2_np = pairing_amd.g2_encode(q_np, True)
+            enc1 = torch.from_numpy(np.ascontiguousarray(enc1_np)).to(dev)
+            enc2 = torch.from_numpy(np.ascontiguousarray(enc2_np)).to(dev)
+            st1 = torch.empty(n, dtype=torch.uint8, device=dev)
+            st2 = torch.empty(n, dtype=torch.uint8, device=dev)
+            side = torch.cuda.Stream(dev)
+            fork, join = torch.cuda.Event(), torch.cuda.Event()
 
         def step(timed):
             if timed:
                 ev[0].record(stream)
+            if args.decode:
+                fork.record(stream)
+                side.wait_event(fork)
+                pdev.decode(1, enc1, True, True, p, st1, side)
+                pdev.decode(2, enc2, True, True, q, st2, stream)
+                join.record(side)
+                stream.wait_event(join)
+                if timed:
+                    ev[2].record(stream)
             pdev.multi_pairing(p, q, out, okb, work, stream)
             if timed:
                 ev[1].record(stream)
@@ -674,6 +697,8 @@ def main():
         k_ms["a"].append(e[0].elapsed_time(e[1]))
         if args.workload in ("pairing", "prepared", "wnaf", "decode"):
             k_ms["b"].append(e[1].elapsed_time(e[2]))
+        if args.workload == "verify" and args.decode:
+            k_ms["b"].append(e[0].elapsed_time(e[2]))   # the decodes
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist_on:
@@ -749,6 +774,12 @@ def main():
             config = {"workload": "final_exponentiation(miller_loop([(P_i, Q_i)])) over %d pairs, inputs in HBM, "
                                   "cooperative kernels (quad VM: four waves per pairing, four lanes per Fq value)" % n,
                       "batch_per_gpu": n, "global_batch": n * ws, "kernel_ms": {"multi_pairing": round(dom_ms, 3)}}
+            if args.decode:
+                dec_ms = float(np.mean(k_ms["b"]))
+                metric = "decode + multi_pairing latency, %d pairs (verifier shape from compressed points)" % n
+                config["workload"] = ("G1Compressed / G2Compressed into_affine (checked) of %d + %d points, G1 beside "
+                                      "G2 on two streams, then " % (n, n)) + config["workload"]
+                config["kernel_ms"] = {"decode": round(dec_ms, 3), "multi_pairing": round(dom_ms - dec_ms, 3)}
         elif args.workload == "fr_mul":
             dom_name, dom_ms, dom_bytes = "fr_mul_batch", float(np.mean(k_ms["a"])), 96
             value = n_global * args.steps / elapsed
@@ -876,11 +907,15 @@ def main():
                 t0 = time.perf_counter()
                 reps = 20
                 for _ in range(reps):
-                    f = oracle.miller_loop(p_np, oracle.g2_prepare(q_np))
+                    pp, qq = p_np, q_np
+                    if args.decode:
+                        pp, _ = oracle.decode(1, enc1_np, True, True, 1)
+                        qq, _ = oracle.decode(2, enc2_np, True, True, 1)
+                    f = oracle.miller_loop(pp, oracle.g2_prepare(qq))
                     oracle.final_exponentiation(f[None, :].copy())
                 cpu = {"value": (time.perf_counter() - t0) / reps * 1e3, "unit": "ms", "cores": 1, "kind": "port",
-                       "sample": "%d x multi_pairing of the same %d pairs, C restatement (oracle/), 1 thread"
-                                 % (reps, n)}
+                       "sample": "%d x %smulti_pairing of the same %d pairs, C restatement (oracle/), 1 thread"
+                                 % (reps, "decode (checked) + " if args.decode else "", n)}
             else:
                 cpu = cpu_baseline_fq_mul(a_np, b_np, args.cpu_seconds)
         line = {"metric": metric, "value": value, "unit": unit, "n_gpus": ws, "steps": args.steps,

@@ -100,6 +100,13 @@ int pa_synchronize(void);
  * PA_ERR_INVALID_ARGUMENT (4 was "lazy reduction" before round 2 and is the
  * one-wave cooperative VM since round 3). */
 int pa_set_pairing_kernel(int variant);
+/* Point-decoding kernel selection (A/B, tests): 0 = by batch size (default:
+ * up to PA_DECODE_QUAD_MAX records, 4096 unless the environment says
+ * otherwise, one record per group of lane quads -- the verifier's latency
+ * form; larger batches one lane per record), 1 = one lane per record, 2 =
+ * quad groups for every size.  Same statuses and outputs.  Process-wide; not
+ * part of the reference interface. */
+int pa_set_decode_kernel(int variant);
 
 /* ---- Fq (src/bls12_381/fq.rs, Field trait src/lib.rs:267-325) ---- */
 /* Field::mul_assign, fq.rs:909-960 + mont_reduce fq.rs:1036-1122 */

@@ -17,10 +17,10 @@ Device-resident entry points for torch tensors live in `pairing_amd.device`.
 import numpy as np
 
 from ._native import (W_FQ, W_FQ2, W_FQ6, W_FQ12, W_FR, W_G1A, W_G1, W_G2A, W_G2, W_G2P, PairingError, _lib,
-                      as_rows, call, device_count, ptr, set_device, set_pairing_kernel, version)
+                      as_rows, call, device_count, ptr, set_decode_kernel, set_device, set_pairing_kernel, version)
 
 __all__ = [
-    "PairingError", "version", "device_count", "set_device", "set_pairing_kernel",
+    "PairingError", "version", "device_count", "set_device", "set_pairing_kernel", "set_decode_kernel",
     "fq_mul", "fq_square", "fq_add", "fq_sub", "fq_inverse",
     "fq2_mul", "fq2_square", "fq6_mul", "fq12_mul", "fq12_square", "fq12_inverse",
     "fq12_frobenius_map", "fq12_cyclotomic_square", "fq12_mul_by_014",

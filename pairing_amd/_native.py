@@ -74,6 +74,7 @@ _SIGS = {
     "pa_set_device": [ctypes.c_int],
     "pa_synchronize": [],
     "pa_set_pairing_kernel": [ctypes.c_int],
+    "pa_set_decode_kernel": [ctypes.c_int],
     "pa_fq_mul_batch": [_P, _P, _P, _N],
     "pa_fq_square_batch": [_P, _P, _N],
     "pa_fq_add_batch": [_P, _P, _P, _N],
@@ -210,6 +211,13 @@ def set_pairing_kernel(variant):
     cooperative for every size, 3 one lane per pairing for every size, 4
     cooperative for every size on the round-2 one-wave VM.  Identical results."""
     call("pa_set_pairing_kernel", int(variant))
+
+
+def set_decode_kernel(variant):
+    """Point-decoding kernels: 0 default by batch size (<= PA_DECODE_QUAD_MAX
+    records: one record per group of lane quads, the latency form), 1 one lane
+    per record, 2 quad groups for every size.  Identical results."""
+    call("pa_set_decode_kernel", int(variant))
 
 
 def set_device(dev):

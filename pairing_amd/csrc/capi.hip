@@ -305,6 +305,11 @@ int pa_set_pairing_kernel(int variant) {
     g_pairing_variant = variant;
     return PA_OK;
 }
+int pa_set_decode_kernel(int variant) {
+    if (variant < 0 || variant > 2) return fail(PA_ERR_INVALID_ARGUMENT, "decode kernel variant must be 0..2");
+    pa::set_decode_variant(variant);
+    return PA_OK;
+}
 int pa_synchronize(void) {
     PA_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     return PA_OK;

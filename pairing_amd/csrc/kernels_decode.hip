@@ -16,6 +16,7 @@
 #include <type_traits>
 
 #include "curve.h"
+#include "dec_quad.h"
 #include "tower_fl.h"
 #include "launch.h"
 
@@ -514,6 +515,349 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ enc, 
     status[i] = (uint8_t)st;
 }
 
+// ---------------- latency form: one record per group of quads ----------------
+// The same decode (statuses, canonical outputs) with the field arithmetic
+// spread over quads of lanes (dec_quad.h): G1 records on 4 quads (16 lanes),
+// G2 records on 8 quads (32 lanes).  The square-root exponentiations run on
+// every quad of the group at once (a quad product is ~2.5x shorter than a
+// one-lane leaf); the subgroup check's Jacobian doublings and additions run
+// their independent products side by side, one per quad (G2: one Fq2
+// coordinate per quad), three product levels per doubling instead of ~17
+// products in a row.  For a verifier's handful of points this is the path;
+// large batches keep one lane per record (k_decode).
+namespace qdec {
+using dq::Lc;
+using dq::Q;
+using dq::Q2;
+
+template <template <int> class E>
+struct Jq {
+    E<1> x, y, z;
+};
+// the fixed operand T of [|x|] T: T, Z^2, Z^3, 2T
+template <template <int> class E>
+struct Fixed {
+    Jq<E> t, t2;
+    E<1> zz, zzz;
+};
+
+template <int NQ, int UX, int UY, int M>
+PA_DEV void lev(Q<1> (&o)[M], const Q<UX> (&x)[M], const Q<UY> (&y)[M], const Lc& l) {
+    dq::level<NQ>(o, x, y, l);
+}
+template <int NQ, int UX, int UY, int M>
+PA_DEV void lev(Q2<1> (&o)[M], const Q2<UX> (&x)[M], const Q2<UY> (&y)[M], const Lc& l) {
+    dq::level2<NQ>(o, x, y, l);
+}
+template <int NQ, template <int> class E, int UX, int UY>
+PA_DEV E<1> prod(const E<UX>& x, const E<UY>& y, const Lc& l) {
+    E<1> o[1];
+    const E<UX> xs[1] = {x};
+    const E<UY> ys[1] = {y};
+    lev<NQ>(o, xs, ys, l);
+    return o[0];
+}
+
+// dbl-2009-l (ec.rs:296-354; the field values of kernels_decode.hip
+// fl_double_any): product levels {X^2, Y^2, Z Y}, {b^2, (X + b)^2, e^2},
+// {e (d - X3)}
+template <int NQ, template <int> class E>
+PA_DEV void jdbl(Jq<E>& p, const Lc& l) {
+    using namespace dq;
+    E<1> l1[3];
+    {
+        const E<1> xs[3] = {p.x, p.y, p.z}, ys[3] = {p.x, p.y, p.y};
+        lev<NQ>(l1, xs, ys, l);
+    }
+    const E<1> a = l1[0], b = l1[1], zy = l1[2];
+    const E<1> e = red(add(dbl(a), a), l);
+    E<1> l2[3];
+    {
+        const E<2> xs[3] = {relax<2>(b), add(p.x, b), relax<2>(e)};
+        lev<NQ>(l2, xs, xs, l);
+    }
+    const E<1> c = l2[0], s = l2[1], f = l2[2];
+    const E<1> d = red(dbl(sub(s, add(a, c), l)), l);
+    p.x = red(sub(f, dbl(d), l), l);
+    p.z = red(dbl(zy), l);
+    const E<1> y3 = prod<NQ, E>(e, sub(d, p.x, l), l);
+    p.y = red(sub(y3, dbl(dbl(dbl(c))), l), l);
+}
+
+PA_DEV Q<1> zero_q() {
+    Q<1> z;
+#pragma unroll
+    for (int k = 0; k < 4; k++) z.w[k] = 0;
+    return z;
+}
+template <template <int> class E>
+PA_DEV E<1> one_e(const Lc& l);
+template <>
+PA_DEV Q<1> one_e<Q>(const Lc& l) { return dq::qconst(FL_ONE, l); }
+template <>
+PA_DEV Q2<1> one_e<Q2>(const Lc& l) { return {dq::qconst(FL_ONE, l), zero_q()}; }
+template <template <int> class E>
+PA_DEV E<1> zero_e();
+template <>
+PA_DEV Q<1> zero_e<Q>() { return zero_q(); }
+template <>
+PA_DEV Q2<1> zero_e<Q2>() { return {zero_q(), zero_q()}; }
+
+// R + T by add-2007-bl (ec.rs:356-444) with T's Z^2, Z^3 and 2T precomputed:
+// product levels {Z1^2, X1 Z2^2, Y1 Z2^3, (Z1 + Z2)^2}, {X2 Z1Z1, Z1 Z1Z1},
+// {Y2 Z1^3, (2H)^2}, {H I, U1 I, r^2, (..) H}, {r (V - X3), S1 J}; R = 0 gives T,
+// R = T gives 2T, R = -T gives 0 (the reference's special cases)
+template <int NQ, template <int> class E>
+PA_DEV void jadd(Jq<E>& r, const Fixed<E>& f, const Lc& l) {
+    using namespace dq;
+    const bool rz = is_zero(r.z);
+    E<1> l1[4];
+    {
+        const E<2> zs = add(r.z, f.t.z);
+        const E<2> xs[4] = {relax<2>(r.z), relax<2>(r.x), relax<2>(r.y), zs};
+        const E<2> ys[4] = {relax<2>(r.z), relax<2>(f.zz), relax<2>(f.zzz), zs};
+        lev<NQ>(l1, xs, ys, l);
+    }
+    const E<1> z1z1 = l1[0], u1 = l1[1], s1 = l1[2], w = l1[3];
+    E<1> l2[2];
+    {
+        const E<1> xs[2] = {f.t.x, r.z}, ys[2] = {z1z1, z1z1};
+        lev<NQ>(l2, xs, ys, l);
+    }
+    const E<1> u2 = l2[0], t1 = l2[1];
+    const E<1> h = red(sub(u2, u1, l), l);
+    E<1> l3[2];
+    {
+        const E<2> xs[2] = {relax<2>(f.t.y), dbl(h)}, ys[2] = {relax<2>(t1), dbl(h)};
+        lev<NQ>(l3, xs, ys, l);
+    }
+    const E<1> s2 = l3[0], ii = l3[1];
+    const E<1> rr = red(dbl(sub(s2, s1, l)), l);
+    const E<1> zp = red(sub(sub(w, z1z1, l), f.zz, l), l);
+    E<1> l4[4];
+    {
+        const E<1> xs[4] = {h, u1, rr, zp}, ys[4] = {ii, ii, rr, h};
+        lev<NQ>(l4, xs, ys, l);
+    }
+    const E<1> j = l4[0], v = l4[1], rsq = l4[2], z3 = l4[3];
+    const E<1> x3 = red(sub(sub(rsq, j, l), dbl(v), l), l);
+    E<1> l5[2];
+    {
+        const E<1> xs[2] = {rr, s1};
+        const E<3> ys[2] = {sub(v, x3, l), relax<3>(j)};
+        lev<NQ>(l5, xs, ys, l);
+    }
+    const E<1> y3 = red(sub(l5[0], dbl(l5[1]), l), l);
+    const bool hz = is_zero(h), rzero = is_zero(rr);
+    if (rz) {
+        r = f.t;
+    } else if (hz && rzero) {
+        r = f.t2;
+    } else if (hz) {   // R = -T: the zero point
+        r.x = one_e<E>(l);
+        r.y = one_e<E>(l);
+        r.z = zero_e<E>();
+    } else {
+        r.x = x3;
+        r.y = y3;
+        r.z = z3;
+    }
+}
+
+template <int NQ, template <int> class E>
+PA_DEV Fixed<E> make_fixed(const Jq<E>& t, const Lc& l) {
+    Fixed<E> f;
+    f.t = t;
+    f.zz = prod<NQ, E>(t.z, t.z, l);
+    f.zzz = prod<NQ, E>(f.zz, t.z, l);
+    f.t2 = t;
+    jdbl<NQ>(f.t2, l);
+    return f;
+}
+// [|x|] T, |x| = 0xd201000000010000 (mod.rs:23-25): MSB-first double-and-add
+template <int NQ, template <int> class E>
+PA_DEV Jq<E> mul_abs_x(const Fixed<E>& f, const Lc& l) {
+    Jq<E> r = f.t;   // bit 63
+#pragma unroll 1
+    for (int bit = 62; bit >= 0; bit--) {
+        jdbl<NQ>(r, l);
+        if ((kAbsX >> bit) & 1) jadd<NQ>(r, f, l);
+    }
+    return r;
+}
+
+PA_DEV Q<1> qconst_abi(const uint64_t* c, const Lc& l) {
+    Fq v;
+    fq_const(v, c);
+    return dq::from_abi(v, l);
+}
+
+// some square root of a (decoding keeps the root the flag asks for, so any
+// root decodes to the same point); false if a is not a square.  Fq: a^((q+1)/4)
+// (fq.rs:1147-1170's value), checked by squaring.
+PA_DEV bool qsqrt(Q<1>& y, const Q<1>& a, const Lc& l) {
+    const Q<1> w = dq::pow_fixed(a, kQm3Div4, 378, l);
+    y = dq::mul(w, a, l);
+    return dq::eq(dq::sqr(y, l), a, l);
+}
+// Fq2, complex method with no inversion and no third exponentiation (q = 3
+// mod 4): n = a0^2 + a1^2, s = n^((q+1)/4), t = (a0 + s) / 2 (or (a0 - s) / 2
+// if that is 0), w = t^((q-3)/4), x0 = t w.  If x0^2 == t, y = x0 + (a1 w / 2) u
+// (1/x0 = w); otherwise x0^2 == -t and y = -(a1 w / 2) + x0 u.  Any failure
+// (a not a square) shows in the final check y^2 == a.
+template <int NQ>
+PA_DEV bool qsqrt(Q2<1>& y, const Q2<1>& a, const Q<1>& half, const Lc& l) {
+    using namespace dq;
+    const Q<1> n = sop(a.c0, a.c0, a.c1, a.c1, l);
+    const Q<1> s = mul(pow_fixed(n, kQm3Div4, 378, l), n, l);
+    const Q<1> tp = mul(add(a.c0, s), half, l);
+    const Q<1> tm = mul(sub(a.c0, s, l), half, l);
+    const Q<1> t = sel(is_zero(tp), tm, tp);
+    const Q<1> w = pow_fixed(t, kQm3Div4, 378, l);
+    const Q<1> x0 = mul(t, w, l);
+    const bool qr = eq(sqr(x0, l), t, l);
+    const Q<1> h = mul(mul(a.c1, w, l), half, l);
+    y.c0 = sel(qr, x0, red(neg(h, l), l));
+    y.c1 = sel(qr, h, x0);
+    return eq(prod<NQ, Q2>(y, y, l), a, l);
+}
+
+// is_in_correct_subgroup_assuming_on_curve (ec.rs:142-144) by the endomorphism
+// identities of in_subgroup_endo above: G1 phi(P) == -[x^2] P
+template <int NQ>
+PA_DEV bool in_g1(const Q<1>& x, const Q<1>& y, const Lc& l) {
+    using namespace dq;
+    const Jq<Q> p{x, y, one_e<Q>(l)};
+    const Jq<Q> t = mul_abs_x<NQ>(make_fixed<NQ>(p, l), l);
+    if (is_zero(t.z)) return false;
+    const Jq<Q> q = mul_abs_x<NQ>(make_fixed<NQ>(t, l), l);
+    if (is_zero(q.z)) return false;
+    const Q<1> bx = mul(qconst_abi(kBeta, l), x, l);
+    const Q<1> zz = prod<NQ, Q>(q.z, q.z, l);
+    const Q<1> zzz = prod<NQ, Q>(zz, q.z, l);
+    if (!eq(prod<NQ, Q>(bx, zz, l), q.x, l)) return false;
+    return is_zero(add(prod<NQ, Q>(y, zzz, l), q.y));
+}
+// G2: psi(P) == [x] P = -[|x|] P, psi(x, y) = (conj(x) cx, conj(y) cy)
+template <int NQ>
+PA_DEV bool in_g2(const Q2<1>& x, const Q2<1>& y, const Lc& l) {
+    using namespace dq;
+    const Jq<Q2> p{x, y, one_e<Q2>(l)};
+    const Jq<Q2> q = mul_abs_x<NQ>(make_fixed<NQ>(p, l), l);
+    if (is_zero(q.z)) return false;
+    const Q<1> cx1 = qconst_abi(kPsiX1, l);
+    const Q2<1> ex{mul(x.c1, cx1, l), mul(x.c0, cx1, l)};   // conj(x) * (0, cx1)
+    const Q2<1> cy{qconst_abi(kPsiY0, l), qconst_abi(kPsiY1, l)};
+    const Q2<1> ycj{y.c0, red(neg(y.c1, l), l)};
+    const Q2<1> ey = prod<NQ, Q2>(ycj, cy, l);
+    const Q2<1> zz = prod<NQ, Q2>(q.z, q.z, l);
+    const Q2<1> zzz = prod<NQ, Q2>(zz, q.z, l);
+    if (!eq(prod<NQ, Q2>(ex, zz, l), q.x, l)) return false;
+    return is_zero(add(prod<NQ, Q2>(ey, zzz, l), q.y));
+}
+
+// decode_one's statuses and outputs, computed by the record's group
+template <int G, bool COMPRESSED>
+PA_DEV int decode_group(Aff<typename std::conditional<G == 1, Fq, Fq2>::type>& out, const uint8_t* rec,
+                        bool checked, const Lc& l) {
+    using namespace dq;
+    using F = typename std::conditional<G == 1, Fq, Fq2>::type;
+    constexpr int NQ = G == 1 ? 4 : 8;
+    constexpr int coords = (G == 1 ? 1 : 2) * (COMPRESSED ? 1 : 2);
+    constexpr int nwords = 12 * coords;
+    uint32_t b[nwords];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(rec);
+#pragma unroll
+    for (int j = 0; j < nwords; j++) b[j] = __builtin_bswap32(src[j]);
+    bool greatest;
+    const int st = check_flags(b, nwords, COMPRESSED, greatest);
+    aff_zero(out);
+    if (st >= 0) return st;
+    uint32_t w[12];
+    F x, y;
+    if constexpr (G == 1) {
+        chunk(w, b, 0);
+        if (!from_repr(x, w)) return DEC_X_C0;
+        if (!COMPRESSED) {
+            chunk(w, b, 1);
+            if (!from_repr(y, w)) return DEC_Y_C0;
+        }
+        const Q<1> xq = from_abi(x, l);
+        const Q<1> rhs = red(add(mul(sqr(xq, l), xq, l), qconst_abi(kB, l)), l);
+        Q<1> yq;
+        if (COMPRESSED) {
+            if (!qsqrt(yq, rhs, l)) return DEC_NOT_ON_CURVE;
+            y = to_abi(yq);
+            Fq negy;
+            fq_neg(negy, y);
+            if ((cmp(y, negy) < 0) == greatest) {
+                y = negy;
+                yq = red(neg(yq, l), l);
+            }
+        } else {
+            yq = from_abi(y, l);
+            if (checked && !eq(sqr(yq, l), rhs, l)) return DEC_NOT_ON_CURVE;
+        }
+        if (checked && !in_g1<NQ>(xq, yq, l)) return DEC_NOT_IN_SUBGROUP;
+    } else {
+        chunk(w, b, 1);
+        if (!from_repr(x.c0, w)) return DEC_X_C0;
+        chunk(w, b, 0);
+        if (!from_repr(x.c1, w)) return DEC_X_C1;
+        if (!COMPRESSED) {
+            chunk(w, b, 3);
+            if (!from_repr(y.c0, w)) return DEC_Y_C0;
+            chunk(w, b, 2);
+            if (!from_repr(y.c1, w)) return DEC_Y_C1;
+        }
+        const Q2<1> xq{from_abi(x.c0, l), from_abi(x.c1, l)};
+        const Q<1> b4 = qconst_abi(kB, l);
+        const Q2<1> x3 = prod<NQ, Q2>(prod<NQ, Q2>(xq, xq, l), xq, l);
+        const Q2<1> rhs{red(add(x3.c0, b4), l), red(add(x3.c1, b4), l)};
+        Q2<1> yq;
+        if (COMPRESSED) {
+            if (!qsqrt<NQ>(yq, rhs, qconst_abi(kHalfMont, l), l)) return DEC_NOT_ON_CURVE;
+            y.c0 = to_abi(yq.c0);
+            y.c1 = to_abi(yq.c1);
+            Fq2 negy;
+            neg(negy, y);
+            if ((cmp(y, negy) < 0) == greatest) {
+                y = negy;
+                yq = red(neg(yq, l), l);
+            }
+        } else {
+            yq = Q2<1>{from_abi(y.c0, l), from_abi(y.c1, l)};
+            if (checked && !eq(prod<NQ, Q2>(yq, yq, l), rhs, l)) return DEC_NOT_ON_CURVE;
+        }
+        if (checked && !in_g2<NQ>(xq, yq, l)) return DEC_NOT_IN_SUBGROUP;
+    }
+    out.x = x;
+    out.y = y;
+    out.inf = false;
+    return DEC_OK;
+}
+
+}  // namespace qdec
+
+template <int G, bool COMPRESSED>
+__global__ void __launch_bounds__(64) k_decode_quad(const uint8_t* __restrict__ enc, size_t n, int checked,
+                                                    uint64_t* __restrict__ out, uint8_t* __restrict__ status) {
+    using F = typename std::conditional<G == 1, Fq, Fq2>::type;
+    constexpr int NQ = G == 1 ? 4 : 8, L = 4 * NQ, PER = 64 / L;
+    constexpr int size = (G == 1 ? 48 : 96) * (COMPRESSED ? 1 : 2);
+    constexpr int W = FieldWords<F>::n;
+    const int lane = threadIdx.x;
+    const size_t i = (size_t)blockIdx.x * PER + lane / L;
+    if (i >= n) return;   // whole groups leave together
+    const dq::Lc l = dq::lctx(lane, NQ);
+    Aff<F> a;
+    const int st = qdec::decode_group<G, COMPRESSED>(a, enc + (size_t)size * i, checked != 0, l);
+    if (lane % L == 0) {
+        store_aff(out + (size_t)(2 * W + 1) * i, a);
+        status[i] = (uint8_t)st;
+    }
+}
+
 // EncodedPoint::from_affine
 template <int G, bool COMPRESSED>
 __global__ void __launch_bounds__(64) k_encode(const uint64_t* __restrict__ in, size_t n, uint8_t* __restrict__ enc) {
@@ -578,9 +922,34 @@ unsigned blocks_for(size_t n) { return (unsigned)((n + 63) / 64); }
 
 }  // namespace
 
+namespace {
+int g_decode_variant = 0;   // pa_set_decode_kernel: 0 by batch size, 1 one lane per record, 2 quad groups
+size_t decode_quad_max() {
+    static const size_t v = [] {
+        const char* e = getenv("PA_DECODE_QUAD_MAX");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
+    }();
+    return v;
+}
+}  // namespace
+void set_decode_variant(int v) { g_decode_variant = v; }
+
 hipError_t launch_decode(int group, int compressed, int checked, const uint8_t* enc, size_t n, uint64_t* out,
                          uint8_t* status, hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    // the latency form for small batches with field work (an uncompressed
+    // unchecked decode is byte handling only: one lane per record)
+    const bool quad = (compressed || checked) &&
+                      (g_decode_variant == 2 || (g_decode_variant == 0 && n <= decode_quad_max()));
+    if (quad) {
+        const unsigned per = group == 1 ? 4 : 2;   // records per 64-lane block
+        const unsigned bq = (unsigned)((n + per - 1) / per);
+        if (group == 1 && compressed) k_decode_quad<1, true><<<bq, 64, 0, stream>>>(enc, n, checked, out, status);
+        else if (group == 1) k_decode_quad<1, false><<<bq, 64, 0, stream>>>(enc, n, checked, out, status);
+        else if (compressed) k_decode_quad<2, true><<<bq, 64, 0, stream>>>(enc, n, checked, out, status);
+        else k_decode_quad<2, false><<<bq, 64, 0, stream>>>(enc, n, checked, out, status);
+        return hipGetLastError();
+    }
     const unsigned b = blocks_for(n);
     if (group == 1 && compressed) k_decode<1, true><<<b, 64, 0, stream>>>(enc, n, checked, out, status);
     else if (group == 1) k_decode<1, false><<<b, 64, 0, stream>>>(enc, n, checked, out, status);

@@ -99,6 +99,9 @@ hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStrea
 // square roots (degree 1: Fq, 2: Fq2), kernels_decode.hip
 hipError_t launch_decode(int group, int compressed, int checked, const uint8_t* enc, size_t n, uint64_t* out,
                          uint8_t* status, hipStream_t stream);
+// 0: by batch size (<= PA_DECODE_QUAD_MAX records: the quad-group latency
+// kernel), 1: one lane per record, 2: quad groups for every size
+void set_decode_variant(int v);
 hipError_t launch_encode(int group, int compressed, const uint64_t* in, size_t n, uint8_t* enc, hipStream_t stream);
 hipError_t launch_sqrt(int degree, const uint64_t* in, size_t n, uint64_t* out, uint8_t* ok, hipStream_t stream);
 

@@ -8,7 +8,10 @@ same bytes; Fq sqrt equals a^((q+1)/4) computed with Python integers.
 
 GPU (-m gpu): the HIP kernels behind pa_g{1,2}_{decode,encode}_batch and
 pa_fq{,2}_sqrt_batch equal the oracle bit for bit (points, status bytes,
-encodings, roots) on the same records, checked and unchecked.
+encodings, roots) on the same records, checked and unchecked.  Every decode
+test runs on both decode kernels (pa_set_decode_kernel): one lane per record
+(k_decode, large batches) and one record per group of lane quads
+(k_decode_quad, the latency form small batches take by default).
 """
 import numpy as np
 import pytest
@@ -94,10 +97,17 @@ def test_oracle_fq2_sqrt_matches_integer_model(oracle):
 
 
 # ---------------- GPU parity ----------------
+@pytest.fixture(params=[1, 2], ids=["one_lane", "quad"])
+def decode_kernel(request, gpu):
+    gpu.set_decode_kernel(request.param)
+    yield request.param
+    gpu.set_decode_kernel(0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("group,compressed", FORMATS)
 @pytest.mark.parametrize("checked", [True, False])
-def test_gpu_decode_matches_oracle(gpu, oracle, group, compressed, checked):
+def test_gpu_decode_matches_oracle(gpu, oracle, decode_kernel, group, compressed, checked):
     enc = _mixed_records(oracle, group, compressed, seed=10 * group + compressed)
     want_pts, want_st = oracle.decode(group, enc, compressed, checked=checked, nthreads=16)
     dec = gpu.g1_decode if group == 1 else gpu.g2_decode
@@ -108,7 +118,7 @@ def test_gpu_decode_matches_oracle(gpu, oracle, group, compressed, checked):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("group,compressed", FORMATS)
-def test_gpu_decode_reference_suites(gpu, group, compressed):
+def test_gpu_decode_reference_suites(gpu, decode_kernel, group, compressed):
     enc, want = _cases(group, compressed)
     dec = gpu.g1_decode if group == 1 else gpu.g2_decode
     _, st = dec(enc, compressed)
@@ -126,7 +136,7 @@ def test_gpu_encode_reproduces_kg_vectors(gpu, oracle, group, compressed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("group", [1, 2])
-def test_gpu_encode_decode_round_trip_random_points(gpu, oracle, group):
+def test_gpu_encode_decode_round_trip_random_points(gpu, oracle, decode_kernel, group):
     from helpers import random_scalars
     s = random_scalars(rng(20 + group), 300)
     pts = oracle.g1_mul_generator(s, 16) if group == 1 else oracle.g2_mul_generator(s, 16)
@@ -184,9 +194,26 @@ def test_oracle_subgroup_check_matches_integer_model(oracle, subgroup_case):
 
 
 @pytest.mark.gpu
-def test_gpu_subgroup_check_matches_oracle(gpu, oracle, subgroup_case):
+def test_gpu_subgroup_check_matches_oracle(gpu, oracle, decode_kernel, subgroup_case):
     group, enc, truth = subgroup_case
     want_pts, want_st = oracle.decode(group, enc, False, checked=True, nthreads=4)
     pts, st = (gpu.g1_decode if group == 1 else gpu.g2_decode)(enc, False, True)
     assert st.tolist() == want_st.tolist()
     assert np.array_equal(pts, want_pts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", [1, 2])
+def test_gpu_subgroup_check_compressed(gpu, oracle, decode_kernel, group):
+    """the same points (in and outside the subgroup, small-order components
+    included) compressed: square root, flag-selected root, then the subgroup
+    check; each x with both sign flags"""
+    pts, truth = D.subgroup_points(group, seed=50 + group, n=3)
+    enc_f = D.enc_g1 if group == 1 else D.enc_g2
+    recs = [enc_f(x, y, True, greatest) for greatest in (False, True) for x, y in pts]
+    enc = np.frombuffer(b"".join(recs), np.uint8).reshape(-1, 48 if group == 1 else 96).copy()
+    want_pts, want_st = oracle.decode(group, enc, True, checked=True, nthreads=4)
+    assert want_st.tolist() == [D.OK if t else D.NOT_IN_SUBGROUP for t in list(truth) * 2]
+    pts_g, st = (gpu.g1_decode if group == 1 else gpu.g2_decode)(enc, True, True)
+    assert st.tolist() == want_st.tolist()
+    assert np.array_equal(pts_g, want_pts)
