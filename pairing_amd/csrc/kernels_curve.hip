@@ -21,6 +21,7 @@
 #include <mutex>
 
 #include "curve_fl.h"
+#include "dec_quad.h"
 #include "launch.h"
 #include "pairing.h"
 
@@ -190,21 +191,23 @@ __global__ void __launch_bounds__(64) k_g1_comb_bases(const uint64_t* __restrict
             for (int i = w0; i < w1; i++) store_jac(bases + kG1Jac * i, p0);
         return;
     }
-    FlJac p;
-    p.x = fl_from_abi(p0.x);
-    p.y = fl_from_abi(p0.y);
-    p.z = fl_from_abi(p0.z);
+    // the doublings on a group of four lane quads (dec_quad.h: three levels of
+    // side-by-side quad products per doubling); lanes 16..63 idle
+    if (lane >= 16) return;
+    const dq::Lc l = dq::lctx(lane, 4);
+    dq::Jq<dq::Q> p{dq::from_abi(p0.x, l), dq::from_abi(p0.y, l), dq::from_abi(p0.z, l)};
 #pragma unroll 1
     for (int i = w0; i < w1; i++) {
         if (i > 0) {
 #pragma unroll 1
-            for (int k = 0; k < 8; k++) fl_jac_double_3lane(p, lane);
+            for (int k = 0; k < 8; k++) dq::jdbl<4>(p, l);
         }
+        const Fq x = dq::to_abi(p.x), y = dq::to_abi(p.y), z = dq::to_abi(p.z);
         if (lane == 0) {
             uint64_t* o = bases + kG1Jac * i;
-            fl_store(o, p.x);
-            fl_store(o + 6, p.y);
-            fl_store(o + 12, p.z);
+            fq_store(o, x);
+            fq_store(o + 6, y);
+            fq_store(o + 12, z);
         }
     }
 }

@@ -530,150 +530,16 @@ using dq::Lc;
 using dq::Q;
 using dq::Q2;
 
-template <template <int> class E>
-struct Jq {
-    E<1> x, y, z;
-};
-// the fixed operand T of [|x|] T: T, Z^2, Z^3, 2T
-template <template <int> class E>
-struct Fixed {
-    Jq<E> t, t2;
-    E<1> zz, zzz;
-};
+using dq::Fixed;
+using dq::Jq;
+using dq::jadd;
+using dq::jdbl;
+using dq::lev;
+using dq::make_fixed;
+using dq::one_e;
+using dq::prod;
+using dq::zero_e;
 
-template <int NQ, int UX, int UY, int M>
-PA_DEV void lev(Q<1> (&o)[M], const Q<UX> (&x)[M], const Q<UY> (&y)[M], const Lc& l) {
-    dq::level<NQ>(o, x, y, l);
-}
-template <int NQ, int UX, int UY, int M>
-PA_DEV void lev(Q2<1> (&o)[M], const Q2<UX> (&x)[M], const Q2<UY> (&y)[M], const Lc& l) {
-    dq::level2<NQ>(o, x, y, l);
-}
-template <int NQ, template <int> class E, int UX, int UY>
-PA_DEV E<1> prod(const E<UX>& x, const E<UY>& y, const Lc& l) {
-    E<1> o[1];
-    const E<UX> xs[1] = {x};
-    const E<UY> ys[1] = {y};
-    lev<NQ>(o, xs, ys, l);
-    return o[0];
-}
-
-// dbl-2009-l (ec.rs:296-354; the field values of kernels_decode.hip
-// fl_double_any): product levels {X^2, Y^2, Z Y}, {b^2, (X + b)^2, e^2},
-// {e (d - X3)}
-template <int NQ, template <int> class E>
-PA_DEV void jdbl(Jq<E>& p, const Lc& l) {
-    using namespace dq;
-    E<1> l1[3];
-    {
-        const E<1> xs[3] = {p.x, p.y, p.z}, ys[3] = {p.x, p.y, p.y};
-        lev<NQ>(l1, xs, ys, l);
-    }
-    const E<1> a = l1[0], b = l1[1], zy = l1[2];
-    const E<1> e = red(add(dbl(a), a), l);
-    E<1> l2[3];
-    {
-        const E<2> xs[3] = {relax<2>(b), add(p.x, b), relax<2>(e)};
-        lev<NQ>(l2, xs, xs, l);
-    }
-    const E<1> c = l2[0], s = l2[1], f = l2[2];
-    const E<1> d = red(dbl(sub(s, add(a, c), l)), l);
-    p.x = red(sub(f, dbl(d), l), l);
-    p.z = red(dbl(zy), l);
-    const E<1> y3 = prod<NQ, E>(e, sub(d, p.x, l), l);
-    p.y = red(sub(y3, dbl(dbl(dbl(c))), l), l);
-}
-
-PA_DEV Q<1> zero_q() {
-    Q<1> z;
-#pragma unroll
-    for (int k = 0; k < 4; k++) z.w[k] = 0;
-    return z;
-}
-template <template <int> class E>
-PA_DEV E<1> one_e(const Lc& l);
-template <>
-PA_DEV Q<1> one_e<Q>(const Lc& l) { return dq::qconst(FL_ONE, l); }
-template <>
-PA_DEV Q2<1> one_e<Q2>(const Lc& l) { return {dq::qconst(FL_ONE, l), zero_q()}; }
-template <template <int> class E>
-PA_DEV E<1> zero_e();
-template <>
-PA_DEV Q<1> zero_e<Q>() { return zero_q(); }
-template <>
-PA_DEV Q2<1> zero_e<Q2>() { return {zero_q(), zero_q()}; }
-
-// R + T by add-2007-bl (ec.rs:356-444) with T's Z^2, Z^3 and 2T precomputed:
-// product levels {Z1^2, X1 Z2^2, Y1 Z2^3, (Z1 + Z2)^2}, {X2 Z1Z1, Z1 Z1Z1},
-// {Y2 Z1^3, (2H)^2}, {H I, U1 I, r^2, (..) H}, {r (V - X3), S1 J}; R = 0 gives T,
-// R = T gives 2T, R = -T gives 0 (the reference's special cases)
-template <int NQ, template <int> class E>
-PA_DEV void jadd(Jq<E>& r, const Fixed<E>& f, const Lc& l) {
-    using namespace dq;
-    const bool rz = is_zero(r.z);
-    E<1> l1[4];
-    {
-        const E<2> zs = add(r.z, f.t.z);
-        const E<2> xs[4] = {relax<2>(r.z), relax<2>(r.x), relax<2>(r.y), zs};
-        const E<2> ys[4] = {relax<2>(r.z), relax<2>(f.zz), relax<2>(f.zzz), zs};
-        lev<NQ>(l1, xs, ys, l);
-    }
-    const E<1> z1z1 = l1[0], u1 = l1[1], s1 = l1[2], w = l1[3];
-    E<1> l2[2];
-    {
-        const E<1> xs[2] = {f.t.x, r.z}, ys[2] = {z1z1, z1z1};
-        lev<NQ>(l2, xs, ys, l);
-    }
-    const E<1> u2 = l2[0], t1 = l2[1];
-    const E<1> h = red(sub(u2, u1, l), l);
-    E<1> l3[2];
-    {
-        const E<2> xs[2] = {relax<2>(f.t.y), dbl(h)}, ys[2] = {relax<2>(t1), dbl(h)};
-        lev<NQ>(l3, xs, ys, l);
-    }
-    const E<1> s2 = l3[0], ii = l3[1];
-    const E<1> rr = red(dbl(sub(s2, s1, l)), l);
-    const E<1> zp = red(sub(sub(w, z1z1, l), f.zz, l), l);
-    E<1> l4[4];
-    {
-        const E<1> xs[4] = {h, u1, rr, zp}, ys[4] = {ii, ii, rr, h};
-        lev<NQ>(l4, xs, ys, l);
-    }
-    const E<1> j = l4[0], v = l4[1], rsq = l4[2], z3 = l4[3];
-    const E<1> x3 = red(sub(sub(rsq, j, l), dbl(v), l), l);
-    E<1> l5[2];
-    {
-        const E<1> xs[2] = {rr, s1};
-        const E<3> ys[2] = {sub(v, x3, l), relax<3>(j)};
-        lev<NQ>(l5, xs, ys, l);
-    }
-    const E<1> y3 = red(sub(l5[0], dbl(l5[1]), l), l);
-    const bool hz = is_zero(h), rzero = is_zero(rr);
-    if (rz) {
-        r = f.t;
-    } else if (hz && rzero) {
-        r = f.t2;
-    } else if (hz) {   // R = -T: the zero point
-        r.x = one_e<E>(l);
-        r.y = one_e<E>(l);
-        r.z = zero_e<E>();
-    } else {
-        r.x = x3;
-        r.y = y3;
-        r.z = z3;
-    }
-}
-
-template <int NQ, template <int> class E>
-PA_DEV Fixed<E> make_fixed(const Jq<E>& t, const Lc& l) {
-    Fixed<E> f;
-    f.t = t;
-    f.zz = prod<NQ, E>(t.z, t.z, l);
-    f.zzz = prod<NQ, E>(f.zz, t.z, l);
-    f.t2 = t;
-    jdbl<NQ>(f.t2, l);
-    return f;
-}
 // [|x|] T, |x| = 0xd201000000010000 (mod.rs:23-25): MSB-first double-and-add
 template <int NQ, template <int> class E>
 PA_DEV Jq<E> mul_abs_x(const Fixed<E>& f, const Lc& l) {

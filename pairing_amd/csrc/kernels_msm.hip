@@ -33,6 +33,7 @@
 // Work: n*W mixed additions + ~2*W*2^(c-1) additions + ~256 doublings.
 
 #include "curve_fl.h"
+#include "dec_quad.h"
 #include "launch_msm.h"
 
 #include <utility>
@@ -745,6 +746,65 @@ __global__ void __launch_bounds__(64) k_msm_horner_fl(const uint64_t* __restrict
     if (lane == 0) fl_store_jac(out, acc);
 }
 
+// Horner on a group of lane quads (dec_quad.h; G1: 4 quads, G2: 8 quads): each
+// doubling is three levels of side-by-side products (one per quad, G2 one
+// Fq2 coordinate per quad) instead of the three-lane doubling's chain, and a
+// quad product is ~2.5x shorter than a one-lane leaf: the 256 doublings of the
+// top window are the MSM's longest dependent chain.  Same sum as a point.
+PA_DEV void load_jac_q(dq::Jq<dq::Q>& r, const uint64_t* p, const dq::Lc& l) {
+    Fq x, y, z;
+    fq_load(x, p);
+    fq_load(y, p + 6);
+    fq_load(z, p + 12);
+    r = {dq::from_abi(x, l), dq::from_abi(y, l), dq::from_abi(z, l)};
+}
+PA_DEV void load_jac_q(dq::Jq<dq::Q2>& r, const uint64_t* p, const dq::Lc& l) {
+    Fq v[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) fq_load(v[k], p + 6 * k);
+    r.x = {dq::from_abi(v[0], l), dq::from_abi(v[1], l)};
+    r.y = {dq::from_abi(v[2], l), dq::from_abi(v[3], l)};
+    r.z = {dq::from_abi(v[4], l), dq::from_abi(v[5], l)};
+}
+PA_DEV void store_jac_q(uint64_t* p, const dq::Jq<dq::Q>& a, bool lead) {
+    const Fq x = dq::to_abi(a.x), y = dq::to_abi(a.y), z = dq::to_abi(a.z);
+    if (lead) {
+        fq_store(p, x);
+        fq_store(p + 6, y);
+        fq_store(p + 12, z);
+    }
+}
+PA_DEV void store_jac_q(uint64_t* p, const dq::Jq<dq::Q2>& a, bool lead) {
+    const Fq v[6] = {dq::to_abi(a.x.c0), dq::to_abi(a.x.c1), dq::to_abi(a.y.c0),
+                     dq::to_abi(a.y.c1), dq::to_abi(a.z.c0), dq::to_abi(a.z.c1)};
+    if (lead)
+#pragma unroll
+        for (int k = 0; k < 6; k++) fq_store(p + 6 * k, v[k]);
+}
+template <int G>
+__global__ void __launch_bounds__(64) k_msm_horner_q(const uint64_t* __restrict__ wsum, uint32_t W, uint32_t c,
+                                                     uint64_t* __restrict__ out) {
+    constexpr int NQ = G == 1 ? 4 : 8;
+    constexpr int JW = Grp<G>::JW;
+    using E = typename std::conditional<G == 1, dq::Jq<dq::Q>, dq::Jq<dq::Q2>>::type;
+    const int lane = threadIdx.x;
+    if (blockIdx.x != 0 || lane >= 4 * NQ) return;   // one group
+    const dq::Lc l = dq::lctx(lane, NQ);
+    E acc;
+    load_jac_q(acc, wsum + (size_t)JW * (W - 1), l);
+#pragma unroll 1
+    for (int w = (int)W - 2; w >= 0; w--) {
+        if (!dq::is_zero(acc.z)) {
+#pragma unroll 1
+            for (uint32_t k = 0; k < c; k++) dq::jdbl<NQ>(acc, l);
+        }
+        E x;
+        load_jac_q(x, wsum + (size_t)JW * w, l);
+        if (!dq::is_zero(x.z)) dq::jadd<NQ>(acc, dq::make_fixed<NQ>(x, l), l);
+    }
+    store_jac_q(out, acc, lane == 0);
+}
+
 // k_msm_segments<1> on the lazy core (same sums, same formulas)
 __global__ void __launch_bounds__(64) k_msm_segments_fl(const uint64_t* __restrict__ buckets, uint32_t B, uint32_t L,
                                                         size_t nseg, uint64_t* __restrict__ segs) {
@@ -892,7 +952,12 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
         src = dst;
         dst = t;
     }
-    if constexpr (G == 1)
+    // the window sums' Horner on a group of lane quads (PA_MSM_HORNER=1: the
+    // round-3 one-wave kernels: three-lane doublings, G1 on the lazy core)
+    static const bool horner_wave = getenv("PA_MSM_HORNER") && atoi(getenv("PA_MSM_HORNER")) == 1;
+    if (!horner_wave)
+        hipLaunchKernelGGL(k_msm_horner_q<G>, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
+    else if constexpr (G == 1)
         hipLaunchKernelGGL(k_msm_horner_fl, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
     else
         hipLaunchKernelGGL(k_msm_horner<G>, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
