@@ -101,7 +101,7 @@ int pa_synchronize(void);
  * one-wave cooperative VM since round 3). */
 int pa_set_pairing_kernel(int variant);
 /* Point-decoding kernel selection (A/B, tests): 0 = by batch size (default:
- * up to PA_DECODE_QUAD_MAX records, 4096 unless the environment says
+ * up to PA_DECODE_QUAD_MAX records, 8192 unless the environment says
  * otherwise, one record per group of lane quads -- the verifier's latency
  * form; larger batches one lane per record), 1 = one lane per record, 2 =
  * quad groups for every size.  Same statuses and outputs.  Process-wide; not

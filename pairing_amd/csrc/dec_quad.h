@@ -455,5 +455,16 @@ PA_DEV Fixed<E> make_fixed(const Jq<E>& t, const Lc& l) {
     return f;
 }
 
+// Fq2 square x^2 (fq2.rs:87-101) on two quads with ONE product each: quad 0
+// c0 = (x0 + x1)(x0 - x1), quad 1 c1 = (2 x0) x1 (both quads run mul)
+template <int NQ>
+PA_DEV Q2<1> sqr2(const Q2<1>& x, const Lc& l) {
+    const bool odd = (l.j & 1) != 0;
+    const Q<2> a = sel(odd, dbl(x.c0), add(x.c0, x.c1));
+    const Q<3> b = sel(odd, relax<3>(x.c1), sub(x.c0, x.c1, l));
+    const Q<1> p = mul(a, b, l);
+    return {bq<NQ, 0>(p), bq<NQ, 1>(p)};
+}
+
 }  // namespace dq
 }  // namespace pa

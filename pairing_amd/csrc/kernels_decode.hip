@@ -17,6 +17,7 @@
 
 #include "curve.h"
 #include "dec_quad.h"
+#include "dec_sqrt_sched.h"
 #include "tower_fl.h"
 #include "launch.h"
 
@@ -588,6 +589,61 @@ PA_DEV bool qsqrt(Q2<1>& y, const Q2<1>& a, const Q<1>& half, const Lc& l) {
     return eq(prod<NQ, Q2>(y, y, l), a, l);
 }
 
+// Fq2 with one exponentiation (tools/gen_sqrt_sched.py): q^2 = 9 mod 16, so
+// r = a^((q^2 + 7) / 16) has r^2 = a z, z = a^((q^2 - 1) / 8) a fourth root of
+// unity for a square a; y = r c(z) with c(1) = 1, c(-1) = u, c(u) = w^3,
+// c(-u) = w (w^2 = u).  The exponent is e0 + e1 q and a^q = conj(a), so one run
+// of 380 Fq2 squarings serves both halves (Straus, 4-bit windows over a, a^3,
+// .., a^15): ~545 Fq2 products, each one level on two quads (a squaring one
+// plain product per quad), against the complex method's 2 x 466 Fq products.  No z matches: a is not a square.
+template <int NQ>
+PA_DEV bool qsqrt_frob(Q2<1>& y, const Q2<1>& a, const Lc& l) {
+    using namespace dq;
+    // the odd powers a^(2k+1), k < 8, parked in LDS (16 KB per wave; in
+    // registers they would push the kernel into scratch): this lane's pieces
+    // at tab[k][coordinate][lane]
+    __shared__ uint4 tab[8][2][64];
+    const int lane = threadIdx.x & 63;
+    auto park = [&](int k, const Q2<1>& v) {
+        tab[k][0][lane] = make_uint4(v.c0.w[0], v.c0.w[1], v.c0.w[2], v.c0.w[3]);
+        tab[k][1][lane] = make_uint4(v.c1.w[0], v.c1.w[1], v.c1.w[2], v.c1.w[3]);
+    };
+    {
+        const Q2<1> a2 = dq::sqr2<NQ>(a, l);
+        Q2<1> t = a;
+        park(0, t);
+#pragma unroll 1
+        for (int k = 1; k < 8; k++) {
+            t = prod<NQ, Q2>(t, a2, l);
+            park(k, t);
+        }
+    }
+    auto factor = [&](int op) -> Q2<2> {   // op 1..8: a^(2k+1), 9..16: its conjugate
+        const int k = (op - 1) & 7;
+        const uint4 u0 = tab[k][0][lane], u1 = tab[k][1][lane];
+        const Q2<1> f{Q<1>{{u0.x, u0.y, u0.z, u0.w}}, Q<1>{{u1.x, u1.y, u1.z, u1.w}}};
+        return op >= 9 ? Q2<2>{relax<2>(f.c0), neg(f.c1, l)} : relax<2>(f);
+    };
+    Q2<1> r = red(factor(kSqrtSched[0]), l);
+#pragma unroll 1
+    for (int i = 1; i < kSqrtOps; i++) {
+        const int op = kSqrtSched[i];
+        r = op == 0 ? dq::sqr2<NQ>(r, l) : prod<NQ, Q2>(r, factor(op), l);
+    }
+    const Q2<1> r2 = prod<NQ, Q2>(r, r, l);
+    const bool z1 = eq(r2, a, l);
+    const bool zm1 = is_zero(add(r2, a));
+    const bool zu = is_zero(add(r2.c0, a.c1)) && eq(r2.c1, a.c0, l);    // r^2 = a u = (-a1, a0)
+    const bool zmu = eq(r2.c0, a.c1, l) && is_zero(add(r2.c1, a.c0));   // r^2 = -a u = (a1, -a0)
+    const Q2<1> one{qconst(FL_ONE, l), zero_e<Q>()};
+    const Q2<1> uu{zero_e<Q>(), qconst(FL_ONE, l)};
+    const Q2<1> w{qconst_abi(kSqrtW[0], l), qconst_abi(kSqrtW[1], l)};
+    const Q2<1> w3{qconst_abi(kSqrtW3[0], l), qconst_abi(kSqrtW3[1], l)};
+    const Q2<1> c = sel(z1, one, sel(zm1, uu, sel(zu, w3, w)));
+    y = prod<NQ, Q2>(r, c, l);
+    return z1 || zm1 || zu || zmu;
+}
+
 // is_in_correct_subgroup_assuming_on_curve (ec.rs:142-144) by the endomorphism
 // identities of in_subgroup_endo above: G1 phi(P) == -[x^2] P
 template <int NQ>
@@ -682,7 +738,9 @@ PA_DEV int decode_group(Aff<typename std::conditional<G == 1, Fq, Fq2>::type>& o
         const Q2<1> rhs{red(add(x3.c0, b4), l), red(add(x3.c1, b4), l)};
         Q2<1> yq;
         if (COMPRESSED) {
-            if (!qsqrt<NQ>(yq, rhs, qconst_abi(kHalfMont, l), l)) return DEC_NOT_ON_CURVE;
+            static constexpr bool kComplex = false;   // A/B: the complex method (two Fq exponentiations)
+            if (kComplex ? !qsqrt<NQ>(yq, rhs, qconst_abi(kHalfMont, l), l) : !qsqrt_frob<NQ>(yq, rhs, l))
+                return DEC_NOT_ON_CURVE;
             y.c0 = to_abi(yq.c0);
             y.c1 = to_abi(yq.c1);
             Fq2 negy;
@@ -793,7 +851,7 @@ int g_decode_variant = 0;   // pa_set_decode_kernel: 0 by batch size, 1 one lane
 size_t decode_quad_max() {
     static const size_t v = [] {
         const char* e = getenv("PA_DECODE_QUAD_MAX");
-        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)8192;
     }();
     return v;
 }

@@ -26,7 +26,8 @@ def dev_ms(group, enc_t, n, reps=7):
     out = torch.empty((n, w), dtype=torch.int64, device="cuda")
     st = torch.empty(n, dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream()
-    pdev.decode(group, enc_t, True, True, out, st)
+    for _ in range(2):
+        pdev.decode(group, enc_t, True, True, out, st)
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
