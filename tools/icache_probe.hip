@@ -1,7 +1,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
-#define BODY asm volatile("s_mov_b32 s80, 0xfffaaab\ns_mov_b32 s81, 0xfefffff\ns_mov_b32 s82, 0x3ffffb9\ns_mov_b32 s83, 0xfffeb15\ns_mov_b32 s84, 0x6241eab\ns_mov_b32 s85, 0xa0f6b0f\ns_mov_b32 s86, 0xf6730d2\ns_mov_b32 s87, 0xf38512b\ns_mov_b32 s88, 0x4774b84\ns_mov_b32 s89, 0x4bacd76\ns_mov_b32 s90, 0xba7b643\ns_mov_b32 s91, 0xe69a4b1\ns_mov_b32 s92, 0x1ea397f\ns_mov_b32 s93, 0x1a011\ns_mov_b32 s94, 0xffcfffd\nv_mad_u64_u32 v[42:43], vcc, v0, v14, 0\nv_mul_lo_u32 v44, v42, s94\nv_and_b32 v44, 0xfffffff, v44\nv_mad_u64_u32 v[42:43], vcc, v44, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s81, v[42:43]\nv_mul_lo_u32 v45, v42, s94\nv_and_b32 v45, 0xfffffff, v45\nv_mad_u64_u32 v[42:43], vcc, v45, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s81, v[42:43]\nv_mul_lo_u32 v46, v42, s94\nv_and_b32 v46, 0xfffffff, v46\nv_mad_u64_u32 v[42:43], vcc, v46, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s81, v[42:43]\nv_mul_lo_u32 v47, v42, s94\nv_and_b32 v47, 0xfffffff, v47\nv_mad_u64_u32 v[42:43], vcc, v47, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s81, v[42:43]\nv_mul_lo_u32 v48, v42, s94\nv_and_b32 v48, 0xfffffff, v48\nv_mad_u64_u32 v[42:43], vcc, v48, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s81, v[42:43]\nv_mul_lo_u32 v49, v42, s94\nv_and_b32 v49, 0xfffffff, v49\nv_mad_u64_u32 v[42:43], vcc, v49, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s81, v[42:43]\nv_mul_lo_u32 v50, v42, s94\nv_and_b32 v50, 0xfffffff, v50\nv_mad_u64_u32 v[42:43], vcc, v50, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s81, v[42:43]\nv_mul_lo_u32 v51, v42, s94\nv_and_b32 v51, 0xfffffff, v51\nv_mad_u64_u32 v[42:43], vcc, v51, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s81, v[42:43]\nv_mul_lo_u32 v52, v42, s94\nv_and_b32 v52, 0xfffffff, v52\nv_mad_u64_u32 v[42:43], vcc, v52, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s81, v[42:43]\nv_mul_lo_u32 v53, v42, s94\nv_and_b32 v53, 0xfffffff, v53\nv_mad_u64_u32 v[42:43], vcc, v53, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s81, v[42:43]\nv_mul_lo_u32 v54, v42, s94\nv_and_b32 v54, 0xfffffff, v54\nv_mad_u64_u32 v[42:43], vcc, v54, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s81, v[42:43]\nv_mul_lo_u32 v55, v42, s94\nv_and_b32 v55, 0xfffffff, v55\nv_mad_u64_u32 v[42:43], vcc, v55, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s81, v[42:43]\nv_mul_lo_u32 v56, v42, s94\nv_and_b32 v56, 0xfffffff, v56\nv_mad_u64_u32 v[42:43], vcc, v56, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s81, v[42:43]\nv_mul_lo_u32 v57, v42, s94\nv_and_b32 v57, 0xfffffff, v57\nv_mad_u64_u32 v[42:43], vcc, v57, s80, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s82, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s81, v[42:43]\nv_and_b32 v28, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s83, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s82, v[42:43]\nv_and_b32 v29, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s84, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s83, v[42:43]\nv_and_b32 v30, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s85, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s84, v[42:43]\nv_and_b32 v31, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s86, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s85, v[42:43]\nv_and_b32 v32, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s87, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s86, v[42:43]\nv_and_b32 v33, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s88, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s87, v[42:43]\nv_and_b32 v34, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s89, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s88, v[42:43]\nv_and_b32 v35, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s90, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s89, v[42:43]\nv_and_b32 v36, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s91, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s90, v[42:43]\nv_and_b32 v37, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s92, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s91, v[42:43]\nv_and_b32 v38, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s93, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s92, v[42:43]\nv_and_b32 v39, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s93, v[42:43]\nv_and_b32 v40, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mov_b32 v41, v42" ::: "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "vcc");
+#define BODY asm volatile("s_mov_b32 s40, 0xfffaaab\ns_mov_b32 s41, 0xfefffff\ns_mov_b32 s42, 0x3ffffb9\ns_mov_b32 s43, 0xfffeb15\ns_mov_b32 s44, 0x6241eab\ns_mov_b32 s45, 0xa0f6b0f\ns_mov_b32 s46, 0xf6730d2\ns_mov_b32 s47, 0xf38512b\ns_mov_b32 s48, 0x4774b84\ns_mov_b32 s49, 0x4bacd76\ns_mov_b32 s50, 0xba7b643\ns_mov_b32 s51, 0xe69a4b1\ns_mov_b32 s52, 0x1ea397f\ns_mov_b32 s53, 0x1a011\ns_mov_b32 s54, 0xffcfffd\nv_mad_u64_u32 v[42:43], vcc, v0, v14, 0\nv_mul_lo_u32 v44, v42, s54\nv_and_b32 v44, 0xfffffff, v44\nv_mad_u64_u32 v[42:43], vcc, v44, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s41, v[42:43]\nv_mul_lo_u32 v45, v42, s54\nv_and_b32 v45, 0xfffffff, v45\nv_mad_u64_u32 v[42:43], vcc, v45, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s41, v[42:43]\nv_mul_lo_u32 v46, v42, s54\nv_and_b32 v46, 0xfffffff, v46\nv_mad_u64_u32 v[42:43], vcc, v46, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s41, v[42:43]\nv_mul_lo_u32 v47, v42, s54\nv_and_b32 v47, 0xfffffff, v47\nv_mad_u64_u32 v[42:43], vcc, v47, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s41, v[42:43]\nv_mul_lo_u32 v48, v42, s54\nv_and_b32 v48, 0xfffffff, v48\nv_mad_u64_u32 v[42:43], vcc, v48, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s41, v[42:43]\nv_mul_lo_u32 v49, v42, s54\nv_and_b32 v49, 0xfffffff, v49\nv_mad_u64_u32 v[42:43], vcc, v49, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s41, v[42:43]\nv_mul_lo_u32 v50, v42, s54\nv_and_b32 v50, 0xfffffff, v50\nv_mad_u64_u32 v[42:43], vcc, v50, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s41, v[42:43]\nv_mul_lo_u32 v51, v42, s54\nv_and_b32 v51, 0xfffffff, v51\nv_mad_u64_u32 v[42:43], vcc, v51, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s41, v[42:43]\nv_mul_lo_u32 v52, v42, s54\nv_and_b32 v52, 0xfffffff, v52\nv_mad_u64_u32 v[42:43], vcc, v52, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s41, v[42:43]\nv_mul_lo_u32 v53, v42, s54\nv_and_b32 v53, 0xfffffff, v53\nv_mad_u64_u32 v[42:43], vcc, v53, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s41, v[42:43]\nv_mul_lo_u32 v54, v42, s54\nv_and_b32 v54, 0xfffffff, v54\nv_mad_u64_u32 v[42:43], vcc, v54, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s41, v[42:43]\nv_mul_lo_u32 v55, v42, s54\nv_and_b32 v55, 0xfffffff, v55\nv_mad_u64_u32 v[42:43], vcc, v55, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s41, v[42:43]\nv_mul_lo_u32 v56, v42, s54\nv_and_b32 v56, 0xfffffff, v56\nv_mad_u64_u32 v[42:43], vcc, v56, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v0, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v14, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v44, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s41, v[42:43]\nv_mul_lo_u32 v57, v42, s54\nv_and_b32 v57, 0xfffffff, v57\nv_mad_u64_u32 v[42:43], vcc, v57, s40, v[42:43]\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v1, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v15, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v45, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s42, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s41, v[42:43]\nv_and_b32 v28, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v2, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v16, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v46, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s43, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s42, v[42:43]\nv_and_b32 v29, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v3, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v17, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v47, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s44, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s43, v[42:43]\nv_and_b32 v30, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v4, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v18, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v48, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s45, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s44, v[42:43]\nv_and_b32 v31, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v5, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v19, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v49, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s46, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s45, v[42:43]\nv_and_b32 v32, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v6, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v20, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v50, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s47, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s46, v[42:43]\nv_and_b32 v33, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v7, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v21, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v51, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s48, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s47, v[42:43]\nv_and_b32 v34, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v8, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v22, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v52, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s49, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s48, v[42:43]\nv_and_b32 v35, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v9, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v23, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v53, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s50, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s49, v[42:43]\nv_and_b32 v36, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v10, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v24, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v54, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s51, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s50, v[42:43]\nv_and_b32 v37, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v11, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v25, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v55, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s52, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s51, v[42:43]\nv_and_b32 v38, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v12, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v26, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v56, s53, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s52, v[42:43]\nv_and_b32 v39, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v13, v27, v[42:43]\nv_mad_u64_u32 v[42:43], vcc, v57, s53, v[42:43]\nv_and_b32 v40, 0xfffffff, v42\nv_lshrrev_b64 v[42:43], 28, v[42:43]\nv_mov_b32 v41, v42" ::: "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "vcc");
 __global__ void __launch_bounds__(64) k1(uint32_t* out, int iters) {
   for (int it = 0; it < iters; it++) {
     BODY
