@@ -86,6 +86,11 @@ CTAB_FULL = (1, 2)
 # storage configurations: (V slots, A slots, L slots)
 STORAGE = {1: (17, 18, int(os.environ.get("PGEN_NL", 11))),  # one wave per SIMD: 256 VGPR + 256 AGPR, 40 KB LDS
            2: (17, 0, 5)}       # two waves per SIMD: 256 VGPR, no AGPR, 20 KB LDS
+# PGEN_TWO_WAVES=1 (A/B experiment): one lane per pairing in the two-waves-per-SIMD
+# budget of the lane-pair kernels (no AGPRs, 5 LDS slots; render.py declares 256 registers)
+TWO_WAVES = os.environ.get("PGEN_TWO_WAVES", "0") == "1"
+if TWO_WAVES:
+    STORAGE[1] = STORAGE[2]
 
 
 def plan_ctab(hist):

@@ -2,6 +2,8 @@
 amdhsa kernel descriptor + code-object metadata, and assemble / link it
 into a code object (.hsaco) with the ROCm LLVM tools."""
 import os
+
+TWO_WAVES = os.environ.get("PGEN_TWO_WAVES", "0") == "1"   # see emit.py
 import subprocess
 
 LLVM = "/opt/rocm/lib/llvm/bin"
@@ -195,7 +197,8 @@ amdhsa.kernels:
            memsym="" if mem_slots is None else
            "\n\t.rodata\n\t.globl {n}_mem_slots\n\t.p2align 2\n\t.type {n}_mem_slots,@object\n"
            "{n}_mem_slots:\n\t.long {m}\n\t.size {n}_mem_slots, 4\n".format(n=name, m=int(mem_slots)),
-           nfree=512 if lanes == 1 else 256, aoff=nvgpr, nagpr=(512 if lanes == 1 else 256) - nvgpr)
+           nfree=512 if lanes == 1 and not TWO_WAVES else 256, aoff=nvgpr,
+           nagpr=(512 if lanes == 1 and not TWO_WAVES else 256) - nvgpr)
 
 
 def assemble(asm_text, out_hsaco, workdir):
