@@ -54,7 +54,7 @@ PA_DEV void fl_jac_add_mixed(FlJac& s, bool& untouched, const F<1>& ox, const F<
     const F<1> r = red(dbl(sub(s2, s.y)));
     const F<1> v = mul(s.x, i);
     const F<1> x3 = red(sub(sub(sub(sqr(r), j), v), v));
-    const F<1> y3 = red(sub(mul(r, sub(v, x3)), dbl(mul(j, s.y))));
+    const F<1> y3 = sop(r, sub(v, x3), j, neg(dbl(s.y)));   // r (v - x3) - 2 j y1, one reduction
     const F<1> z3 = red(sub(sub(sqr(add(s.z, red(h))), z1z1), hh));
     s.x = x3;
     s.y = y3;
@@ -82,7 +82,7 @@ PA_DEV void fl_jac_add(FlJac& s, const FlJac& o) {
     const F<1> r = red(dbl(sub(s2, s1)));
     const F<1> v = mul(u1, i);
     const F<1> x3 = red(sub(sub(sub(sqr(r), j), v), v));
-    const F<1> y3 = red(sub(mul(r, sub(v, x3)), dbl(mul(s1, j))));
+    const F<1> y3 = sop(r, sub(v, x3), j, neg(dbl(s1)));    // r (v - x3) - 2 s1 j, one reduction
     const F<1> z3 = mul(red(sub(sub(sqr(add(s.z, o.z)), z1z1), z2z2)), h);
     s.x = x3;
     s.y = y3;

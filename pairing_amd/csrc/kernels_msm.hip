@@ -22,20 +22,25 @@
 //      apart, zero digits are dropped.  Same order as a stable sort of the
 //      (w*B + |d|-1) keys, so the result is deterministic.
 //   3. k_msm_bucket_bounds: [start, end) per bucket from the sorted keys.
-//   4. k_msm_chunk_acc: one lane per 32 sorted items, mixed additions
+//   4. k_msm_chunk_acc: one lane per 64 sorted items, mixed additions
 //      (madd-2007-bl) of the affine bases gathered from HBM (y negated for
 //      negative digits), run by run; k_msm_bucket_fix folds the pieces of
 //      buckets that span chunks and zeroes empty buckets.
 //   5. k_msm_segments: per window, sum_m m*B_m by running sums over segments of
 //      L buckets (T += B_m; S += T, top down), plus a*T for the segment offset.
 //   6. k_msm_group_sum (repeated): segment results -> one sum per window.
-//   7. k_msm_horner: one wave, sum_w 2^(c*w) S_w (doublings over three lanes).
+//   7. k_msm_horner_q: one group of lane quads, sum_w 2^(c*w) S_w.
+// Steps 4-7 run per part of the windows (top windows first, msm_run): a part's
+// reduction (4's fix-up, 5, 6) and its Horner leg run on side streams while
+// the next part accumulates, so only the last part's tail is exposed.
 // Work: n*W mixed additions + ~2*W*2^(c-1) additions + ~256 doublings.
 
 #include "curve_fl.h"
 #include "dec_quad.h"
 #include "launch_msm.h"
 
+#include <cstdlib>
+#include <mutex>
 #include <utility>
 
 namespace pa {
@@ -101,10 +106,11 @@ __global__ void __launch_bounds__(64) k_proj_mul(const uint64_t* __restrict__ p,
 struct MsmPlan {
     uint32_t c, W, B, L;        // window bits, windows, buckets per window, segment length
     uint32_t passes;            // counting-sort passes over the c-1 magnitude bits
+    uint32_t T;                 // items per lane of the bucket accumulation
     uint32_t tpw;               // sort tiles per window
     size_t items;               // W * n
     size_t off_keys_in, off_keys_out, off_vals_in, off_vals_out, off_start, off_end;
-    size_t off_buckets, off_segs, off_tmp, off_hist, off_wtot, off_cont, off_basefl;
+    size_t off_buckets, off_segs, off_tmp, off_hist, off_wtot, off_cont, off_basefl, off_hacc;
     size_t total;
 };
 
@@ -123,7 +129,20 @@ static inline uint32_t msm_window_bits(size_t n) {
 }
 
 // items (sorted (bucket, term) pairs) per lane of the bucket accumulation
-constexpr uint32_t kMsmChunk = 32;
+// (PA_MSM_CHUNK to A/B, 8..512): 32 / 48 / 64 / 96 / 128 measured 167 / 162 /
+// 170 / 159 / 171 M terms/s at 2^20 with one part, 64 with two parts 175-177
+// (profiles/r04_msm_parts.txt)
+constexpr uint32_t kMsmChunk = 64;
+static uint32_t msm_chunk() {
+    static const uint32_t t = [] {
+        const char* v = getenv("PA_MSM_CHUNK");
+        const int k = v ? atoi(v) : (int)kMsmChunk;
+        return (uint32_t)(k < 8 ? 8 : (k > 512 ? 512 : k));
+    }();
+    return t;
+}
+// window parts (msm_run): at most this many, each with a Horner accumulator slot
+constexpr uint32_t kMsmMaxParts = 8;
 // counting sort: a tile is 16 rounds of one item per thread of a 256-thread block
 constexpr uint32_t kSortIpt = 16;
 constexpr uint32_t kSortTile = 256 * kSortIpt;
@@ -156,10 +175,12 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.off_buckets = off; off = align256(off + jw * nb);
     p.off_segs = off; off = align256(off + jw * nseg);
     p.off_tmp = off; off = align256(off + jw * nseg);
-    p.off_cont = off; off = align256(off + jw * ((p.items + kMsmChunk - 1) / kMsmChunk));
+    p.T = msm_chunk();
+    p.off_cont = off; off = align256(off + jw * ((p.items + p.T - 1) / p.T + 1));
     p.off_basefl = off; off = align256(off + (group == 1 ? 4 * 28 * n : 0));
     p.off_hist = off; off = align256(off + 4 * (size_t)p.W * 256 * p.tpw);
     p.off_wtot = off; off = align256(off + 4 * (size_t)p.W);
+    p.off_hacc = off; off = align256(off + jw * kMsmMaxParts);
     p.total = off;
     return hipSuccess;
 }
@@ -417,13 +438,31 @@ __global__ void __launch_bounds__(256) k_sort_scatter(const uint32_t* __restrict
 }
 
 // Bucket accumulation, load-balanced: lane k owns the sorted items
-// [k T, (k+1) T) (T = kMsmChunk) and adds their bases run by run.  A run whose
+// [k T, (k+1) T) (T = MsmPlan::T) and adds their bases run by run.  A run whose
 // bucket starts inside the chunk is written to the bucket; the chunk's first
 // run, when its bucket started in an earlier chunk, goes to cont[k] and is
 // folded in by k_msm_bucket_fix.  Every lane does at most T mixed additions
 // whatever the digit distribution (a window whose digits crowd into few
 // buckets -- the top window of scalars < r -- no longer makes a few lanes
 // walk hundreds of terms).
+#ifndef PA_MSM_ACC_ATTR
+#define PA_MSM_ACC_ATTR
+#endif
+// chunk k0 + i of the window part [w0, w1): its items [k T, (k+1) T) clipped to
+// the part's items [jlo, jhi) of the sorted (window-compacted) array, k0 =
+// floor(jlo / T).  A window's items start with a new bucket, so a chunk
+// straddling two parts is split cleanly (its second piece never writes cont[k]).
+PA_DEV bool chunk_range(size_t i, const uint32_t* __restrict__ wtot, uint32_t w0, uint32_t w1, uint32_t T,
+                        size_t& k, size_t& j0, size_t& j1) {
+    const size_t jlo = sort_wbase(wtot, w0), jhi = sort_wbase(wtot, w1);
+    k = jlo / T + i;
+    j0 = k * T;
+    j1 = j0 + T;
+    if (j0 < jlo) j0 = jlo;
+    if (j1 > jhi) j1 = jhi;
+    return j0 < j1;
+}
+
 template <int G>
 PA_DEV void msm_flush(uint32_t key, const Jac<typename Grp<G>::F>& acc, size_t j0, size_t k,
                       const uint32_t* __restrict__ start, uint64_t* __restrict__ buckets,
@@ -437,14 +476,13 @@ template <int G>
 __global__ void __launch_bounds__(64) k_msm_chunk_acc(const uint64_t* __restrict__ bases,
                                                       const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ vals,
-                                                      const uint32_t* __restrict__ start, size_t items,
-                                                      uint32_t sentinel, uint64_t* __restrict__ buckets,
+                                                      const uint32_t* __restrict__ start,
+                                                      const uint32_t* __restrict__ wtot, uint32_t w0, uint32_t w1,
+                                                      uint32_t T, uint32_t sentinel, uint64_t* __restrict__ buckets,
                                                       uint64_t* __restrict__ cont) {
     using F = typename Grp<G>::F;
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t j0 = k * kMsmChunk;
-    if (j0 >= items) return;
-    const size_t j1 = (j0 + kMsmChunk < items) ? j0 + kMsmChunk : items;
+    size_t k, j0, j1;
+    if (!chunk_range((size_t)blockIdx.x * blockDim.x + threadIdx.x, wtot, w0, w1, T, k, j0, j1)) return;
     uint32_t cur = keys[j0];
     if (cur >= sentinel) return;  // zero digits sort last
     Jac<F> acc;
@@ -503,17 +541,16 @@ PA_DEV void msm_flush_fl(uint32_t key, const FlJac& acc, bool untouched, size_t 
 
 // ... and k_msm_chunk_acc<1> with the lazy mixed addition (curve_fl.h);
 // bucket pieces leave in the ABI form the later phases read.
-__global__ void __launch_bounds__(64) k_msm_chunk_acc_fl(const uint64_t* __restrict__ bases,
+__global__ void __launch_bounds__(64) PA_MSM_ACC_ATTR k_msm_chunk_acc_fl(const uint64_t* __restrict__ bases,
                                                          const uint32_t* __restrict__ basefl,
                                                          const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals,
-                                                         const uint32_t* __restrict__ start, size_t items,
-                                                         uint32_t sentinel, uint64_t* __restrict__ buckets,
+                                                         const uint32_t* __restrict__ start,
+                                                         const uint32_t* __restrict__ wtot, uint32_t w0, uint32_t w1,
+                                                         uint32_t T, uint32_t sentinel, uint64_t* __restrict__ buckets,
                                                          uint64_t* __restrict__ cont) {
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t j0 = k * kMsmChunk;
-    if (j0 >= items) return;
-    const size_t j1 = (j0 + kMsmChunk < items) ? j0 + kMsmChunk : items;
+    size_t k, j0, j1;
+    if (!chunk_range((size_t)blockIdx.x * blockDim.x + threadIdx.x, wtot, w0, w1, T, k, j0, j1)) return;
     uint32_t cur = keys[j0];
     if (cur >= sentinel) return;
     FlJac acc;
@@ -587,13 +624,13 @@ __global__ void __launch_bounds__(64) k_msm_chunk_acc_fl(const uint64_t* __restr
 // several chunks adds the continuation pieces of the chunks after its first.
 template <int G>
 __global__ void __launch_bounds__(64) k_msm_bucket_fix(const uint32_t* __restrict__ start,
-                                                       const uint32_t* __restrict__ end, size_t nb,
-                                                       const uint64_t* __restrict__ cont,
+                                                       const uint32_t* __restrict__ end, size_t b0, size_t b1,
+                                                       uint32_t T, const uint64_t* __restrict__ cont,
                                                        uint64_t* __restrict__ buckets) {
     using F = typename Grp<G>::F;
     constexpr int JW = Grp<G>::JW;
-    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
+    const size_t b = b0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= b1) return;
     const uint32_t s = start[b], e = end[b];
     if (s == e) {
         Jac<F> z;
@@ -601,7 +638,7 @@ __global__ void __launch_bounds__(64) k_msm_bucket_fix(const uint32_t* __restric
         store_jac(buckets + (size_t)JW * b, z);
         return;
     }
-    const size_t first = s / kMsmChunk, last = (e - 1) / kMsmChunk;
+    const size_t first = s / T, last = (e - 1) / T;
     if (first == last) return;
     if constexpr (G == 1) {  // lazy core, same formulas and values
         FlJac acc = fl_load_jac(buckets + (size_t)JW * b);
@@ -624,11 +661,11 @@ __global__ void __launch_bounds__(64) k_msm_bucket_fix(const uint32_t* __restric
 // One lane per segment of L buckets of one window: sum_m m * B_m over the segment.
 template <int G>
 __global__ void __launch_bounds__(64) k_msm_segments(const uint64_t* __restrict__ buckets, uint32_t B, uint32_t L,
-                                                     size_t nseg, uint64_t* __restrict__ segs) {
+                                                     size_t t0, size_t t1, uint64_t* __restrict__ segs) {
     using F = typename Grp<G>::F;
     constexpr int JW = Grp<G>::JW;
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nseg) return;
+    const size_t t = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= t1) return;
     const uint32_t spw = B / L;
     const size_t w = t / spw;
     const uint32_t j = (uint32_t)(t % spw);
@@ -657,15 +694,16 @@ __global__ void __launch_bounds__(64) k_msm_segments(const uint64_t* __restrict_
     store_jac(segs + (size_t)JW * t, S);
 }
 
-// out[w*gpw + g] = sum_{k<G} in[w*count + g*G + k]  (indices < count)
+// out[w*stride + g] = sum_{k<G} in[w*stride + g*G + k]  (indices < count), windows
+// [w0, w1); the fixed per-window stride keeps the window parts' levels apart
 template <int G>
 __global__ void __launch_bounds__(64) k_msm_group_sum(const uint64_t* __restrict__ in, uint32_t count,
-                                                      uint32_t group, uint32_t gpw, uint32_t W,
-                                                      uint64_t* __restrict__ out) {
+                                                      uint32_t group, uint32_t gpw, uint32_t w0, uint32_t w1,
+                                                      uint32_t stride, uint64_t* __restrict__ out) {
     using F = typename Grp<G>::F;
     constexpr int JW = Grp<G>::JW;
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (size_t)W * gpw) return;
+    const size_t t = (size_t)w0 * gpw + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)w1 * gpw) return;
     const size_t w = t / gpw;
     const uint32_t g = (uint32_t)(t % gpw);
     Jac<F> acc;
@@ -675,20 +713,20 @@ __global__ void __launch_bounds__(64) k_msm_group_sum(const uint64_t* __restrict
         const uint32_t idx = g * group + k;
         if (idx >= count) break;
         Jac<F> x;
-        load_jac(x, in + (size_t)JW * (w * count + idx));
+        load_jac(x, in + (size_t)JW * (w * stride + idx));
         jac_add(acc, x);
     }
-    store_jac(out + (size_t)JW * t, acc);
+    store_jac(out + (size_t)JW * (w * stride + g), acc);
 }
 
 // k_msm_group_sum<1> on the lazy core, one quad per output (fl_jac_add_q)
 __global__ void __launch_bounds__(64) k_msm_group_sum_fl(const uint64_t* __restrict__ in, uint32_t count,
-                                                         uint32_t group, uint32_t gpw, uint32_t W,
-                                                         uint64_t* __restrict__ out) {
+                                                         uint32_t group, uint32_t gpw, uint32_t w0, uint32_t w1,
+                                                         uint32_t stride, uint64_t* __restrict__ out) {
     constexpr int JW = Grp<1>::JW;
-    const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    const size_t t = (size_t)w0 * gpw + (((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2);
     const int q = threadIdx.x & 3;
-    if (t >= (size_t)W * gpw) return;
+    if (t >= (size_t)w1 * gpw) return;
     const size_t w = t / gpw;
     const uint32_t g = (uint32_t)(t % gpw);
     FlJac acc;
@@ -699,14 +737,14 @@ __global__ void __launch_bounds__(64) k_msm_group_sum_fl(const uint64_t* __restr
     for (uint32_t k = 0; k < group; k++) {
         const uint32_t idx = g * group + k;
         if (idx >= count) break;
-        fl_jac_add_q(acc, fl_load_jac(in + (size_t)JW * (w * count + idx)), q);
+        fl_jac_add_q(acc, fl_load_jac(in + (size_t)JW * (w * stride + idx)), q);
     }
-    if (q == 0) fl_store_jac(out + (size_t)JW * t, acc);
+    if (q == 0) fl_store_jac(out + (size_t)JW * (w * stride + g), acc);
 }
 
 template <int G>
-__global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ wsum, uint32_t W, uint32_t c,
-                                                   uint64_t* __restrict__ out) {
+__global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ wsum, uint32_t stride, uint32_t W,
+                                                   uint32_t c, uint64_t* __restrict__ out) {
     using F = typename Grp<G>::F;
     constexpr int JW = Grp<G>::JW;
     // one wave; the doublings use three lanes (jac_double_3lane), every lane
@@ -714,13 +752,13 @@ __global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ 
     if (blockIdx.x != 0) return;
     const int lane = threadIdx.x;
     Jac<F> acc;
-    load_jac(acc, wsum + (size_t)JW * (W - 1));
+    load_jac(acc, wsum + (size_t)JW * stride * (W - 1));
 #pragma unroll 1
     for (int w = (int)W - 2; w >= 0; w--) {
 #pragma unroll 1
         for (uint32_t k = 0; k < c; k++) jac_double_3lane(acc, lane);
         Jac<F> x;
-        load_jac(x, wsum + (size_t)JW * w);
+        load_jac(x, wsum + (size_t)JW * stride * w);
         jac_add(acc, x);
     }
     if (lane == 0) store_jac(out, acc);
@@ -729,19 +767,19 @@ __global__ void __launch_bounds__(64) k_msm_horner(const uint64_t* __restrict__ 
 // G1 Horner entirely on the lazy core: doublings over three lanes
 // (fl_jac_double_3lane), window sums added with fl_jac_add.  #E(Fq) is odd,
 // so a nonzero accumulator never doubles to zero and a zero one is skipped.
-__global__ void __launch_bounds__(64) k_msm_horner_fl(const uint64_t* __restrict__ wsum, uint32_t W, uint32_t c,
-                                                      uint64_t* __restrict__ out) {
+__global__ void __launch_bounds__(64) k_msm_horner_fl(const uint64_t* __restrict__ wsum, uint32_t stride, uint32_t W,
+                                                      uint32_t c, uint64_t* __restrict__ out) {
     constexpr int JW = Grp<1>::JW;
     if (blockIdx.x != 0) return;
     const int lane = threadIdx.x;
-    FlJac acc = fl_load_jac(wsum + (size_t)JW * (W - 1));
+    FlJac acc = fl_load_jac(wsum + (size_t)JW * stride * (W - 1));
 #pragma unroll 1
     for (int w = (int)W - 2; w >= 0; w--) {
         if (!fl_is_zero(acc.z)) {
 #pragma unroll 1
             for (uint32_t k = 0; k < c; k++) fl_jac_double_3lane(acc, lane);
         }
-        fl_jac_add(acc, fl_load_jac(wsum + (size_t)JW * w));
+        fl_jac_add(acc, fl_load_jac(wsum + (size_t)JW * stride * w));
     }
     if (lane == 0) fl_store_jac(out, acc);
 }
@@ -781,8 +819,11 @@ PA_DEV void store_jac_q(uint64_t* p, const dq::Jq<dq::Q2>& a, bool lead) {
 #pragma unroll
         for (int k = 0; k < 6; k++) fq_store(p + 6 * k, v[k]);
 }
+// Windows [wlo, whi) top down: from acc_in (the part above, doubled c times
+// first) or, without one, from S_(whi-1).
 template <int G>
-__global__ void __launch_bounds__(64) k_msm_horner_q(const uint64_t* __restrict__ wsum, uint32_t W, uint32_t c,
+__global__ void __launch_bounds__(64) k_msm_horner_q(const uint64_t* __restrict__ wsum, uint32_t stride, int whi,
+                                                     int wlo, uint32_t c, const uint64_t* __restrict__ acc_in,
                                                      uint64_t* __restrict__ out) {
     constexpr int NQ = G == 1 ? 4 : 8;
     constexpr int JW = Grp<G>::JW;
@@ -791,15 +832,21 @@ __global__ void __launch_bounds__(64) k_msm_horner_q(const uint64_t* __restrict_
     if (blockIdx.x != 0 || lane >= 4 * NQ) return;   // one group
     const dq::Lc l = dq::lctx(lane, NQ);
     E acc;
-    load_jac_q(acc, wsum + (size_t)JW * (W - 1), l);
+    int w = whi - 1;
+    if (acc_in) {
+        load_jac_q(acc, acc_in, l);
+    } else {
+        load_jac_q(acc, wsum + (size_t)JW * stride * w, l);
+        w--;
+    }
 #pragma unroll 1
-    for (int w = (int)W - 2; w >= 0; w--) {
+    for (; w >= wlo; w--) {
         if (!dq::is_zero(acc.z)) {
 #pragma unroll 1
             for (uint32_t k = 0; k < c; k++) dq::jdbl<NQ>(acc, l);
         }
         E x;
-        load_jac_q(x, wsum + (size_t)JW * w, l);
+        load_jac_q(x, wsum + (size_t)JW * stride * w, l);
         if (!dq::is_zero(x.z)) dq::jadd<NQ>(acc, dq::make_fixed<NQ>(x, l), l);
     }
     store_jac_q(out, acc, lane == 0);
@@ -807,12 +854,12 @@ __global__ void __launch_bounds__(64) k_msm_horner_q(const uint64_t* __restrict_
 
 // k_msm_segments<1> on the lazy core (same sums, same formulas)
 __global__ void __launch_bounds__(64) k_msm_segments_fl(const uint64_t* __restrict__ buckets, uint32_t B, uint32_t L,
-                                                        size_t nseg, uint64_t* __restrict__ segs) {
+                                                        size_t t0, size_t t1, uint64_t* __restrict__ segs) {
     // one lane per segment: the kernel is throughput bound (4 k waves); a quad
     // per segment (fl_jac_add_q) measured 0.57 -> 1.29 ms (profiles/r03_msm_quad_ab.txt)
     constexpr int JW = Grp<1>::JW;
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nseg) return;
+    const size_t t = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= t1) return;
     const uint32_t spw = B / L;
     const size_t w = t / spw;
     const uint32_t j = (uint32_t)(t % spw);
@@ -857,6 +904,41 @@ size_t msm_workspace_bytes(int group, size_t n) {
     MsmPlan p;
     if (msm_plan(p, group, n) != hipSuccess) return 0;
     return p.total;
+}
+
+// window parts of one MSM (PA_MSM_PARTS, default 2; 1 = every kernel on the
+// caller's stream in order; 3 and 4 measured slower: the tails compete with the
+// next part's accumulation for SIMDs, profiles/r04_msm_parts.txt)
+static uint32_t msm_parts(uint32_t W) {
+    static const uint32_t parts = [] {
+        const char* v = getenv("PA_MSM_PARTS");
+        const int k = v ? atoi(v) : 2;
+        return (uint32_t)(k < 1 ? 1 : (k > (int)kMsmMaxParts ? (int)kMsmMaxParts : k));
+    }();
+    return parts < W ? parts : W;
+}
+
+// two non-blocking side streams per device (bucket reduction, Horner legs)
+static hipError_t msm_side_streams(hipStream_t out[2]) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    static std::mutex mu;
+    static hipStream_t side[64][2] = {};
+    std::lock_guard<std::mutex> g(mu);
+    // the side streams at the highest priority: a part's reduction waves are
+    // dispatched as the next part's accumulation frees SIMDs (PA_MSM_PRIO=0: default priority)
+    static const bool prio = !getenv("PA_MSM_PRIO") || atoi(getenv("PA_MSM_PRIO")) != 0;
+    int lo = 0, hi = 0;
+    if (prio && (e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return e;
+    for (int k = 0; k < 2; k++) {
+        if (!side[dev][k] &&
+            (e = hipStreamCreateWithPriority(&side[dev][k], hipStreamNonBlocking, prio ? hi : lo)) != hipSuccess)
+            return e;
+        out[k] = side[dev][k];
+    }
+    return hipSuccess;
 }
 
 template <int G>
@@ -909,60 +991,128 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     hipLaunchKernelGGL(k_msm_bucket_bounds, dim3(msm_blocks(p.items, 256)), dim3(256), 0, s, keys_out, p.items,
                        p.W * p.B, start, end);
     uint64_t* cont = reinterpret_cast<uint64_t*>(base + p.off_cont);
-    const size_t nchunks = (p.items + kMsmChunk - 1) / kMsmChunk;
-    if constexpr (G == 1) {
-        uint32_t* basefl = reinterpret_cast<uint32_t*>(base + p.off_basefl);
-        hipLaunchKernelGGL(k_msm_bases_fl, dim3(msm_blocks(n, 256)), dim3(256), 0, s, bases, n, basefl);
-        hipLaunchKernelGGL(k_msm_chunk_acc_fl, dim3(msm_blocks(nchunks, 64)), dim3(64), 0, s, bases, basefl,
-                           keys_out, vals_out, start, p.items, p.W * p.B, buckets, cont);
-    } else {
-        hipLaunchKernelGGL(k_msm_chunk_acc<G>, dim3(msm_blocks(nchunks, 64)), dim3(64), 0, s, bases, keys_out,
-                           vals_out, start, p.items, p.W * p.B, buckets, cont);
-    }
-    hipLaunchKernelGGL(k_msm_bucket_fix<G>, dim3(msm_blocks(nb, 64)), dim3(64), 0, s, start, end, nb, cont, buckets);
-    const uint32_t spw = p.B / p.L;
-    const size_t nseg = (size_t)p.W * spw;
+    uint64_t* hacc = reinterpret_cast<uint64_t*>(base + p.off_hacc);
+    const uint32_t* basefl = reinterpret_cast<const uint32_t*>(base + p.off_basefl);
     if constexpr (G == 1)
-        hipLaunchKernelGGL(k_msm_segments_fl, dim3(msm_blocks(nseg, 64)), dim3(64), 0, s, buckets, p.B, p.L, nseg,
-                           segs);
-    else
-        hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(nseg, 64)), dim3(64), 0, s, buckets, p.B, p.L, nseg,
-                           segs);
-    // segment sums -> one per window, 4 at a time (ping-pong segs <-> tmp)
-    uint32_t count = spw;
-    uint64_t* src = segs;
-    uint64_t* dst = tmp;
-    while (count > 1) {
-        // shallow chains: 2 additions per level, 2 / 3 / 4 / 8 measured 141.6 / 140.2 / 138.1 / 133.5 M
-        // terms/s at 2^20 (profiles/r02_msm_tuning.txt); PA_MSM_GROUP to A/B
-        static const uint32_t group = [] {
-            const char* v = getenv("PA_MSM_GROUP");
-            const int g = v ? atoi(v) : 2;
-            return (uint32_t)(g < 2 ? 2 : (g > 16 ? 16 : g));
-        }();
-        const uint32_t gpw = (count + group - 1) / group;
+        hipLaunchKernelGGL(k_msm_bases_fl, dim3(msm_blocks(n, 256)), dim3(256), 0, s, bases, n,
+                           reinterpret_cast<uint32_t*>(base + p.off_basefl));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t spw = p.B / p.L;
+    // segment sums -> one per window, `group` at a time (ping-pong segs <-> tmp);
+    // every part takes the same number of levels, so the window sums of all of
+    // them land in the same buffer
+    // shallow chains: 2 additions per level, 2 / 3 / 4 / 8 measured 141.6 / 140.2 / 138.1 / 133.5 M
+    // terms/s at 2^20 (profiles/r02_msm_tuning.txt); PA_MSM_GROUP to A/B
+    static const uint32_t group = [] {
+        const char* v = getenv("PA_MSM_GROUP");
+        const int g = v ? atoi(v) : 2;
+        return (uint32_t)(g < 2 ? 2 : (g > 16 ? 16 : g));
+    }();
+    uint64_t* wsum = segs;
+    for (uint32_t count = spw; count > 1; count = (count + group - 1) / group) wsum = wsum == segs ? tmp : segs;
+
+    // the windows' throughput kernels of one part (windows [w0, w1))
+    // (the part's item range is on the device, wtot: lanes for the most it can hold)
+    auto accumulate = [&](uint32_t w0, uint32_t w1, hipStream_t st) {
+        const size_t chunks = ((size_t)(w1 - w0) * n + p.T - 1) / p.T + 1;
         if constexpr (G == 1)
-            hipLaunchKernelGGL(k_msm_group_sum_fl, dim3(msm_blocks(4 * (size_t)p.W * gpw, 64)), dim3(64), 0, s, src,
-                               count, group, gpw, p.W, dst);
+            hipLaunchKernelGGL(k_msm_chunk_acc_fl, dim3(msm_blocks(chunks, 64)), dim3(64), 0, st, bases, basefl,
+                               keys_out, vals_out, start, wtot, w0, w1, p.T, p.W * p.B, buckets, cont);
         else
-            hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks((size_t)p.W * gpw, 64)), dim3(64), 0, s, src, count,
-                               group, gpw, p.W, dst);
-        count = gpw;
-        uint64_t* t = src;
-        src = dst;
-        dst = t;
-    }
-    // the window sums' Horner on a group of lane quads (PA_MSM_HORNER=1: the
-    // round-3 one-wave kernels: three-lane doublings, G1 on the lazy core)
+            hipLaunchKernelGGL(k_msm_chunk_acc<G>, dim3(msm_blocks(chunks, 64)), dim3(64), 0, st, bases, keys_out,
+                               vals_out, start, wtot, w0, w1, p.T, p.W * p.B, buckets, cont);
+        return hipGetLastError();
+    };
+    // ... and its bucket -> window-sum reduction
+    auto reduce = [&](uint32_t w0, uint32_t w1, hipStream_t st) {
+        const size_t b0 = (size_t)w0 * p.B, b1 = (size_t)w1 * p.B;
+        hipLaunchKernelGGL(k_msm_bucket_fix<G>, dim3(msm_blocks(b1 - b0, 64)), dim3(64), 0, st, start, end, b0, b1,
+                           p.T, cont, buckets);
+        const size_t t0 = (size_t)w0 * spw, t1 = (size_t)w1 * spw;
+        if constexpr (G == 1)
+            hipLaunchKernelGGL(k_msm_segments_fl, dim3(msm_blocks(t1 - t0, 64)), dim3(64), 0, st, buckets, p.B, p.L,
+                               t0, t1, segs);
+        else
+            hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(t1 - t0, 64)), dim3(64), 0, st, buckets, p.B, p.L,
+                               t0, t1, segs);
+        uint64_t *src = segs, *dst = tmp;
+        for (uint32_t count = spw; count > 1;) {
+            const uint32_t gpw = (count + group - 1) / group;
+            const size_t outs = (size_t)(w1 - w0) * gpw;
+            if constexpr (G == 1)
+                hipLaunchKernelGGL(k_msm_group_sum_fl, dim3(msm_blocks(4 * outs, 64)), dim3(64), 0, st, src, count,
+                                   group, gpw, w0, w1, spw, dst);
+            else
+                hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks(outs, 64)), dim3(64), 0, st, src, count, group,
+                                   gpw, w0, w1, spw, dst);
+            count = gpw;
+            std::swap(src, dst);
+        }
+        return hipGetLastError();
+    };
+
+    // the round-3 one-wave Horner kernels (PA_MSM_HORNER=1: three-lane
+    // doublings, G1 on the lazy core) run the whole MSM as one part
     static const bool horner_wave = getenv("PA_MSM_HORNER") && atoi(getenv("PA_MSM_HORNER")) == 1;
-    if (!horner_wave)
-        hipLaunchKernelGGL(k_msm_horner_q<G>, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
-    else if constexpr (G == 1)
-        hipLaunchKernelGGL(k_msm_horner_fl, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
-    else
-        hipLaunchKernelGGL(k_msm_horner<G>, dim3(1), dim3(64), 0, s, src, p.W, p.c, out);
+    const uint32_t parts = horner_wave ? 1 : msm_parts(p.W);
+    if (parts == 1) {
+        if ((e = accumulate(0, p.W, s)) != hipSuccess || (e = reduce(0, p.W, s)) != hipSuccess) return e;
+        if (!horner_wave)
+            hipLaunchKernelGGL(k_msm_horner_q<G>, dim3(1), dim3(64), 0, s, wsum, spw, (int)p.W, 0, p.c, nullptr, out);
+        else if constexpr (G == 1)
+            hipLaunchKernelGGL(k_msm_horner_fl, dim3(1), dim3(64), 0, s, wsum, spw, p.W, p.c, out);
+        else
+            hipLaunchKernelGGL(k_msm_horner<G>, dim3(1), dim3(64), 0, s, wsum, spw, p.W, p.c, out);
+        return hipGetLastError();
+    }
+    // Window parts, top windows first.  The caller's stream runs every part's
+    // bucket accumulation back to back; part q's reduction runs on a side
+    // stream behind it and its Horner leg (windows [w0, w1), continuing the
+    // part above) on a third, so the latency-bound tails (segment-sum levels,
+    // the 16 doublings per window of the Horner chain) of the upper parts
+    // hide under the next parts' accumulation.  Only the last part's reduction
+    // and Horner leg are exposed.  Same window sums, same Horner: same point.
+    hipStream_t side[2];
+    if ((e = msm_side_streams(side)) != hipSuccess) return e;
+    hipStream_t red_s = side[0], hor_s = side[1];
+    static const bool serial = getenv("PA_MSM_SERIAL") && atoi(getenv("PA_MSM_SERIAL")) != 0;
+    if (serial) red_s = hor_s = s;   // measurement / debugging: the parts in order on the caller's stream
+    hipEvent_t ev[2 * kMsmMaxParts + 1] = {};
+    int made = 0;
+    hipError_t err = hipSuccess;
+    auto ck = [&](hipError_t x) {
+        if (err == hipSuccess) err = x;
+        return err == hipSuccess;
+    };
+    const int nev = 2 * (int)parts + 1;
+    for (; made < nev; made++)
+        if (!ck(hipEventCreateWithFlags(&ev[made], hipEventDisableTiming))) break;
+    // ev[2q]: part q accumulated; ev[2q + 1]: part q reduced; ev[2 parts]: the upper Horner legs done
+    auto wlo = [&](uint32_t q) { return (uint32_t)(((uint64_t)p.W * (parts - 1 - q)) / parts); };
+    for (uint32_t q = 0; q < parts && err == hipSuccess; q++) {
+        const uint32_t w1 = q == 0 ? p.W : wlo(q - 1), w0 = wlo(q);
+        if (!ck(accumulate(w0, w1, s))) break;
+        uint64_t* leg_out = q + 1 == parts ? out : hacc + (size_t)JW * q;
+        const uint64_t* leg_in = q == 0 ? nullptr : hacc + (size_t)JW * (q - 1);
+        if (q + 1 == parts) {
+            if (!ck(reduce(w0, w1, s)) || !ck(hipStreamWaitEvent(s, ev[2 * parts], 0))) break;
+            hipLaunchKernelGGL(k_msm_horner_q<G>, dim3(1), dim3(64), 0, s, wsum, spw, (int)w1, (int)w0, p.c, leg_in,
+                               leg_out);
+            ck(hipGetLastError());
+            break;
+        }
+        if (!ck(hipEventRecord(ev[2 * q], s)) || !ck(hipStreamWaitEvent(red_s, ev[2 * q], 0)) ||
+            !ck(reduce(w0, w1, red_s)) || !ck(hipEventRecord(ev[2 * q + 1], red_s)) ||
+            !ck(hipStreamWaitEvent(hor_s, ev[2 * q + 1], 0)))
+            break;
+        hipLaunchKernelGGL(k_msm_horner_q<G>, dim3(1), dim3(64), 0, hor_s, wsum, spw, (int)w1, (int)w0, p.c, leg_in,
+                           leg_out);
+        if (!ck(hipGetLastError())) break;
+        if (q + 2 == parts) ck(hipEventRecord(ev[2 * parts], hor_s));
+    }
+    for (int k = 0; k < made; k++) (void)hipEventDestroy(ev[k]);
     (void)JW;
-    return hipGetLastError();
+    return err;
 }
 
 hipError_t launch_msm(int group, const uint64_t* bases, const uint64_t* scalars, size_t n, uint64_t* out, void* ws,

@@ -153,3 +153,40 @@ def test_g1_multiexp_deterministic(gpu, oracle):
     b = gpu.g1_multiexp(p, s)
     np.testing.assert_array_equal(a, b)
     assert oracle.g1_eq(a, oracle.g1_multiexp(p, s, NT)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts,chunk", [("1", "32"), ("3", "8"), ("8", "16"), ("2", "512")])
+def test_multiexp_window_parts(gpu, oracle, parts, chunk):
+    """The MSM's launch structure (kernels_msm.hip msm_run): the windows in
+    PA_MSM_PARTS parts on side streams, PA_MSM_CHUNK sorted items per lane
+    (read once per process, hence a subprocess): small chunks put most buckets
+    across several chunks (the continuation pieces), many parts cut chunks at
+    window boundaries; the sum stays the same point (ec.rs:45-85)"""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    g = rng(90)
+    n1, n2 = 4099, 200
+    p1 = oracle.g1_mul_generator(random_scalars(g, n1), NT)
+    s1 = random_scalars(g, n1)
+    s1[:10] = edge_scalars()
+    set_infinity(p1, [11])
+    s1[100:300] = s1[7]          # crowded buckets
+    p2 = oracle.g2_mul_generator(random_scalars(g, n2), NT)
+    s2 = random_scalars(g, n2)
+    s2[:4] = small_scalars([0, 1, R_ORDER - 1, (1 << 256) - 1])
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import pairing_amd as pa; d = sys.argv[1]; "
+            "np.save(d + '/o1.npy', pa.g1_multiexp(np.load(d + '/p1.npy'), np.load(d + '/s1.npy'))); "
+            "np.save(d + '/o2.npy', pa.g2_multiexp(np.load(d + '/p2.npy'), np.load(d + '/s2.npy')))" % root)
+    with tempfile.TemporaryDirectory() as d:
+        for name, a in (("p1", p1), ("s1", s1), ("p2", p2), ("s2", s2)):
+            np.save(os.path.join(d, name + ".npy"), a)
+        env = dict(os.environ, PA_MSM_PARTS=parts, PA_MSM_CHUNK=chunk)
+        r = subprocess.run([sys.executable, "-c", code, d], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        o1, o2 = np.load(os.path.join(d, "o1.npy")), np.load(os.path.join(d, "o2.npy"))
+    assert oracle.g1_eq(o1, oracle.g1_multiexp(p1, s1, NT)).all()
+    assert oracle.g2_eq(o2, oracle.g2_multiexp(p2, s2, NT)).all()

@@ -251,7 +251,10 @@ def exp_by_x_karabina(p, T, V, xv, L, first_skip, tag="k"):
     saved.append(kn)
     nds = [T.kdec_numden(getg(sn)) for sn in saved]
     idens = T.batch_inv2([nd[1] for nd in nds], tag)
-    F = [T.kdec_finish(getg(sn), nd[0], iv, nd[2]) for sn, nd, iv in zip(saved, nds, idens)]
+    order = os.environ.get("PGEN_KDEC_ORDER", "1")   # "0": the round-3 order (A/B)
+    fin = lambda k: T.kdec_finish(getg(saved[k]), nds[k][0], idens[k], nds[k][2])
+    if order == "0":
+        F = [fin(k) for k in range(3)]
     # top: the GS state reuses the 8 compressed-state homes (dead by now) plus
     # four more; res: 6 + 6 coordinates in AGPRs + the workspace
     V.declare12(res, os.environ.get("PGEN_KR_HOME", "AAAAAAMMMMMM"))
@@ -260,8 +263,16 @@ def exp_by_x_karabina(p, T, V, xv, L, first_skip, tag="k"):
             j = 2 * i + c
             if j >= 8:
                 p.var("%s%d_%d" % (top, i, c), 1, os.environ.get("PGEN_KT_HOME", "A"))
-    V.set12(top, F[2])
-    V.set12(res, T.mul12(T.mul12(F[0], F[1]), F[2]))
+    if order == "0":
+        V.set12(top, F[2])
+        V.set12(res, T.mul12(T.mul12(F[0], F[1]), F[2]))
+    else:
+        # (default) finish the top state first, straight into its homes, then the two
+        # snapshots one after the other into their product: 12 fewer M slots,
+        # 15% fewer workspace moves, FE 9.29 -> 9.11 ms (profiles/r04_kdec_order.txt)
+        V.set12(top, fin(2))
+        V.set12(res, T.mul12(fin(0), fin(1)))
+        V.set12(res, T.mul12(V.get12(res), V.get12(top)))
     # the top bits: squarings 1..6 above bit 57, multiply after squarings 3, 5, 6
     # (loop counter 5..0 -> bits 3, 1, 0 of the mask)
     assert [b - bits[2] for b in bits[3:]] == [3, 5, 6]
