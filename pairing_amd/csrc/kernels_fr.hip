@@ -94,10 +94,17 @@ hipError_t launch_fr_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* o
     size_t blocks = (n + 255) / 256;
     const StreamCfg c = stream_cfg();
     if (blocks > c.max_blocks) blocks = c.max_blocks;
+    // 27000 B of (unused) dynamic LDS per 256-thread block caps residency at 5
+    // waves per SIMD, as for config 2 (k_fq_mul_batch_fl): 21.2 vs 22.2-22.3 us
+    // at 2^20 uncapped (profiles/r04_fr_fq_ab.txt); PA_FR_LDS overrides it
+    static const unsigned lds = [] {
+        const char* e = getenv("PA_FR_LDS");
+        return e ? (unsigned)atoi(e) : 27000u;
+    }();
     if (c.prefetch)
-        hipLaunchKernelGGL(k_fr_mul_batch<1>, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
+        hipLaunchKernelGGL(k_fr_mul_batch<1>, dim3((unsigned)blocks), dim3(256), lds, stream, a, b, out, n);
     else
-        hipLaunchKernelGGL(k_fr_mul_batch<0>, dim3((unsigned)blocks), dim3(256), 0, stream, a, b, out, n);
+        hipLaunchKernelGGL(k_fr_mul_batch<0>, dim3((unsigned)blocks), dim3(256), lds, stream, a, b, out, n);
     return hipGetLastError();
 }
 

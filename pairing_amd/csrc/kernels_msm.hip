@@ -36,6 +36,7 @@
 // Work: n*W mixed additions + ~2*W*2^(c-1) additions + ~256 doublings.
 
 #include "curve_fl.h"
+#include "curve_fl2.h"
 #include "dec_quad.h"
 #include "launch_msm.h"
 
@@ -110,7 +111,7 @@ struct MsmPlan {
     uint32_t tpw;               // sort tiles per window
     size_t items;               // W * n
     size_t off_keys_in, off_keys_out, off_vals_in, off_vals_out, off_start, off_end;
-    size_t off_buckets, off_segs, off_tmp, off_hist, off_wtot, off_cont, off_basefl, off_hacc;
+    size_t off_buckets, off_segs, off_tmp, off_hist, off_wtot, off_cont, off_basefl, off_hacc, off_long;
     size_t total;
 };
 
@@ -143,6 +144,10 @@ static uint32_t msm_chunk() {
 }
 // window parts (msm_run): at most this many, each with a Horner accumulator slot
 constexpr uint32_t kMsmMaxParts = 8;
+// a bucket whose items span more chunks than this has its continuation pieces
+// summed by a block (k_msm_long_fix), not serially by one lane of k_msm_bucket_fix
+constexpr size_t kMsmLongSpan = 8;
+constexpr unsigned kMsmLongBlocks = 64;
 // counting sort: a tile is 16 rounds of one item per thread of a 256-thread block
 constexpr uint32_t kSortIpt = 16;
 constexpr uint32_t kSortTile = 256 * kSortIpt;
@@ -177,10 +182,11 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.off_tmp = off; off = align256(off + jw * nseg);
     p.T = msm_chunk();
     p.off_cont = off; off = align256(off + jw * ((p.items + p.T - 1) / p.T + 1));
-    p.off_basefl = off; off = align256(off + (group == 1 ? 4 * 28 * n : 0));
+    p.off_basefl = off; off = align256(off + 4 * (group == 1 ? 28 : 56) * n);
     p.off_hist = off; off = align256(off + 4 * (size_t)p.W * 256 * p.tpw);
     p.off_wtot = off; off = align256(off + 4 * (size_t)p.W);
     p.off_hacc = off; off = align256(off + jw * kMsmMaxParts);
+    p.off_long = off; off = align256(off + 4 * (nb + kMsmMaxParts));   // long-bucket lists + counts
     p.total = off;
     return hipSuccess;
 }
@@ -622,11 +628,13 @@ __global__ void __launch_bounds__(64) PA_MSM_ACC_ATTR k_msm_chunk_acc_fl(const u
 
 // One lane per bucket: empty buckets become the identity; a bucket spanning
 // several chunks adds the continuation pieces of the chunks after its first.
-template <int G>
+template <int G, bool LAZY>
 __global__ void __launch_bounds__(64) k_msm_bucket_fix(const uint32_t* __restrict__ start,
                                                        const uint32_t* __restrict__ end, size_t b0, size_t b1,
                                                        uint32_t T, const uint64_t* __restrict__ cont,
-                                                       uint64_t* __restrict__ buckets) {
+                                                       uint64_t* __restrict__ buckets,
+                                                       uint32_t* __restrict__ long_list,
+                                                       uint32_t* __restrict__ long_count) {
     using F = typename Grp<G>::F;
     constexpr int JW = Grp<G>::JW;
     const size_t b = b0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -640,11 +648,21 @@ __global__ void __launch_bounds__(64) k_msm_bucket_fix(const uint32_t* __restric
     }
     const size_t first = s / T, last = (e - 1) / T;
     if (first == last) return;
+    if (long_list && last - first > kMsmLongSpan) {   // k_msm_long_fix folds it, a block per bucket
+        long_list[atomicAdd(long_count, 1u)] = (uint32_t)b;
+        return;
+    }
     if constexpr (G == 1) {  // lazy core, same formulas and values
         FlJac acc = fl_load_jac(buckets + (size_t)JW * b);
 #pragma unroll 1
         for (size_t k = first + 1; k <= last; k++) fl_jac_add(acc, fl_load_jac(cont + (size_t)JW * k));
         fl_store_jac(buckets + (size_t)JW * b, acc);
+        return;
+    } else if constexpr (LAZY) {
+        FlJac2 acc = fl2_load_jac(buckets + (size_t)JW * b);
+#pragma unroll 1
+        for (size_t k = first + 1; k <= last; k++) fl2_jac_add(acc, fl2_load_jac(cont + (size_t)JW * k));
+        fl2_store_jac(buckets + (size_t)JW * b, acc);
         return;
     }
     Jac<F> acc;
@@ -888,6 +906,205 @@ __global__ void __launch_bounds__(64) k_msm_segments_fl(const uint64_t* __restri
     fl_store_jac(segs + (size_t)JW * t, S);
 }
 
+// ---- G2 bucket phases on the lazy core's Fq2 (curve_fl2.h; round 4) ----
+// The affine bases converted once per MSM (x.c0, x.c1, y.c0, y.c1 -> 56 u32;
+// the infinity flag in bit 31 of x.c0's top limb, below 2^18 for F<1>) ...
+__global__ void __launch_bounds__(256) k_msm_bases_fl2(const uint64_t* __restrict__ bases, size_t n,
+                                                       uint32_t* __restrict__ fl) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Aff<Fq2> a;
+    load_aff(a, bases + (size_t)Grp<2>::AW * i);
+    const F<1> v[4] = {fl_from_abi(a.x.c0), fl_from_abi(a.x.c1), fl_from_abi(a.y.c0), fl_from_abi(a.y.c1)};
+    uint32_t* d = fl + 56 * i;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int k = 0; k < 14; k++) d[14 * c + k] = v[c].w[k] | (c == 0 && k == 13 && a.inf ? 0x80000000u : 0u);
+}
+
+PA_DEV void msm_flush_fl2(uint32_t key, const FlJac2& acc, bool untouched, size_t j0, size_t k,
+                          const uint32_t* __restrict__ start, uint64_t* __restrict__ buckets,
+                          uint64_t* __restrict__ cont) {
+    constexpr int JW = Grp<2>::JW;
+    uint64_t* o = start[key] >= j0 ? buckets + (size_t)JW * key : cont + (size_t)JW * k;
+    if (untouched) {
+        Jac<Fq2> z;
+        jac_zero(z);
+        store_jac(o, z);
+    } else {
+        fl2_store_jac(o, acc);
+    }
+}
+
+// ... k_msm_chunk_acc<2> with the lazy mixed addition; the (key, value) pair
+// of the next item in flight while the current addition runs (a prefetched
+// 224-byte base would not fit beside the Fq2 temporaries)
+__global__ void __launch_bounds__(64) k_msm_chunk_acc_fl2(const uint32_t* __restrict__ basefl,
+                                                          const uint32_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ vals,
+                                                          const uint32_t* __restrict__ start,
+                                                          const uint32_t* __restrict__ wtot, uint32_t w0, uint32_t w1,
+                                                          uint32_t T, uint32_t sentinel,
+                                                          uint64_t* __restrict__ buckets, uint64_t* __restrict__ cont) {
+    size_t k, j0, j1;
+    if (!chunk_range((size_t)blockIdx.x * blockDim.x + threadIdx.x, wtot, w0, w1, T, k, j0, j1)) return;
+    uint32_t cur = keys[j0];
+    if (cur >= sentinel) return;
+    FlJac2 acc = fl2_jac_zero();
+    bool untouched = true;
+    uint32_t key = cur, v = vals[j0];
+#pragma unroll 1
+    for (size_t j = j0; j < j1; j++) {
+        if (key >= sentinel) break;
+        uint32_t nkey = sentinel, nv = 0;
+        if (j + 1 < j1) {
+            nkey = keys[j + 1];
+            nv = vals[j + 1];
+        }
+        if (key != cur) {
+            msm_flush_fl2(cur, acc, untouched, j0, k, start, buckets, cont);
+            untouched = true;
+            cur = key;
+        }
+        const uint2* src = reinterpret_cast<const uint2*>(basefl + 56 * (size_t)(v & 0x7fffffffu));
+        F<1> c[4];
+#pragma unroll
+        for (int q = 0; q < 28; q++) {
+            const uint2 t = src[q];
+            c[q / 7].w[2 * (q % 7)] = t.x;
+            c[q / 7].w[2 * (q % 7) + 1] = t.y;
+        }
+        const bool inf = (c[0].w[13] >> 31) != 0;
+        c[0].w[13] &= 0x7fffffffu;
+        if (!inf) {  // an infinity base is add_assign_mixed's no-op
+            const F2<1> y = {c[2], c[3]};
+            const F2<2> oy = (v >> 31) ? neg(y) : relax<2>(y);
+            fl2_jac_add_mixed(acc, untouched, F2<1>{c[0], c[1]}, oy);
+        }
+        key = nkey;
+        v = nv;
+    }
+    msm_flush_fl2(cur, acc, untouched, j0, k, start, buckets, cont);
+}
+
+// k_msm_segments<2> on the lazy core (same sums, same formulas)
+__global__ void __launch_bounds__(64) k_msm_segments_fl2(const uint64_t* __restrict__ buckets, uint32_t B, uint32_t L,
+                                                         size_t t0, size_t t1, uint64_t* __restrict__ segs) {
+    constexpr int JW = Grp<2>::JW;
+    const size_t t = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= t1) return;
+    const uint32_t spw = B / L;
+    const size_t w = t / spw;
+    const uint32_t j = (uint32_t)(t % spw);
+    const uint64_t* bw = buckets + (size_t)JW * (w * B);
+    FlJac2 T = fl2_jac_zero(), S = T;
+#pragma unroll 1
+    for (uint32_t m = (j + 1) * L; m > j * L; m--) {  // magnitudes (j*L, (j+1)*L], top down
+        fl2_jac_add(T, fl2_load_jac(bw + (size_t)JW * (m - 1)));
+        fl2_jac_add(S, T);
+    }
+    const uint32_t a = j * L;  // S = sum (m - a) B_m; add a * T
+    if (a && !f2_is_zero(T.z)) {
+        FlJac2 aT = T;  // top set bit of a
+        const int top = 31 - __clz(a);
+#pragma unroll 1
+        for (int bit = top - 1; bit >= 0; bit--) {
+            fl2_jac_double(aT);
+            if ((a >> bit) & 1) fl2_jac_add(aT, T);
+        }
+        fl2_jac_add(S, aT);
+    }
+    fl2_store_jac(segs + (size_t)JW * t, S);
+}
+
+// k_msm_group_sum<2> on the lazy core, one lane per output
+__global__ void __launch_bounds__(64) k_msm_group_sum_fl2(const uint64_t* __restrict__ in, uint32_t count,
+                                                          uint32_t group, uint32_t gpw, uint32_t w0, uint32_t w1,
+                                                          uint32_t stride, uint64_t* __restrict__ out) {
+    constexpr int JW = Grp<2>::JW;
+    const size_t t = (size_t)w0 * gpw + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)w1 * gpw) return;
+    const size_t w = t / gpw;
+    const uint32_t g = (uint32_t)(t % gpw);
+    FlJac2 acc = fl2_jac_zero();
+#pragma unroll 1
+    for (uint32_t k = 0; k < group; k++) {
+        const uint32_t idx = g * group + k;
+        if (idx >= count) break;
+        fl2_jac_add(acc, fl2_load_jac(in + (size_t)JW * (w * stride + idx)));
+    }
+    fl2_store_jac(out + (size_t)JW * (w * stride + g), acc);
+}
+
+// Buckets spanning more than kMsmLongSpan chunks (crowded digits: equal
+// scalars, the carry-only top window of c-bit windows above bit 255): one
+// block per bucket, each thread summing a strided share of the continuation
+// pieces, then a tree through LDS; the bucket's own piece is added last.  The
+// list comes from k_msm_bucket_fix; without long buckets the blocks exit at
+// once.  Without it one lane walked every piece (G2 at 2^18: 46 ms).
+template <int G> struct LazyJac;
+template <> struct LazyJac<1> {
+    using P = FlJac;
+    static constexpr int NT = 256;
+    static PA_DEV P zero() { return {fl_zero(), fl_one(), fl_zero()}; }
+    static PA_DEV void add(P& a, const P& b) { fl_jac_add(a, b); }
+    static PA_DEV P load(const uint64_t* p) { return fl_load_jac(p); }
+    static PA_DEV void store(uint64_t* p, const P& a) { fl_store_jac(p, a); }
+};
+template <> struct LazyJac<2> {
+    using P = FlJac2;
+    static constexpr int NT = 128;
+    static PA_DEV P zero() { return fl2_jac_zero(); }
+    static PA_DEV void add(P& a, const P& b) { fl2_jac_add(a, b); }
+    static PA_DEV P load(const uint64_t* p) { return fl2_load_jac(p); }
+    static PA_DEV void store(uint64_t* p, const P& a) { fl2_store_jac(p, a); }
+};
+template <int G>
+__global__ void __launch_bounds__(LazyJac<G>::NT) k_msm_long_fix(const uint32_t* __restrict__ start,
+                                                                 const uint32_t* __restrict__ end, uint32_t T,
+                                                                 const uint64_t* __restrict__ cont,
+                                                                 uint64_t* __restrict__ buckets,
+                                                                 const uint32_t* __restrict__ long_list,
+                                                                 const uint32_t* __restrict__ long_count) {
+    using L = LazyJac<G>;
+    using P = typename L::P;
+    constexpr int NT = L::NT, JW = Grp<G>::JW, PW = sizeof(P) / 4;
+    __shared__ uint32_t sh[(NT / 2) * PW];
+    const int t = threadIdx.x;
+    const uint32_t count = *long_count;
+#pragma unroll 1
+    for (uint32_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
+        const uint32_t b = long_list[idx];
+        const size_t first = start[b] / T, last = (end[b] - 1) / T;
+        P acc = L::zero();
+#pragma unroll 1
+        for (size_t k = first + 1 + t; k <= last; k += NT) L::add(acc, L::load(cont + (size_t)JW * k));
+#pragma unroll 1
+        for (int h = NT / 2; h >= 1; h >>= 1) {
+            if (t >= h && t < 2 * h) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(&acc);
+#pragma unroll
+                for (int q = 0; q < PW; q++) sh[(t - h) * PW + q] = src[q];
+            }
+            __syncthreads();
+            if (t < h) {
+                P o;
+                uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+                for (int q = 0; q < PW; q++) dst[q] = sh[t * PW + q];
+                L::add(acc, o);
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            P bk = L::load(buckets + (size_t)JW * b);
+            L::add(bk, acc);
+            L::store(buckets + (size_t)JW * b, bk);
+        }
+    }
+}
+
 template <int G>
 __global__ void __launch_bounds__(64) k_jac_zero_out(uint64_t* __restrict__ out) {
     using F = typename Grp<G>::F;
@@ -993,8 +1210,14 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     uint64_t* cont = reinterpret_cast<uint64_t*>(base + p.off_cont);
     uint64_t* hacc = reinterpret_cast<uint64_t*>(base + p.off_hacc);
     const uint32_t* basefl = reinterpret_cast<const uint32_t*>(base + p.off_basefl);
+    // G2 on the lazy core's Fq2 (round 4); PA_MSM_G2_LAZY=0: the 12-word kernels (A/B)
+    static const bool g2_lazy_env = !getenv("PA_MSM_G2_LAZY") || atoi(getenv("PA_MSM_G2_LAZY")) != 0;
+    const bool g2_lazy = G == 2 && g2_lazy_env;
     if constexpr (G == 1)
         hipLaunchKernelGGL(k_msm_bases_fl, dim3(msm_blocks(n, 256)), dim3(256), 0, s, bases, n,
+                           reinterpret_cast<uint32_t*>(base + p.off_basefl));
+    else if (g2_lazy)
+        hipLaunchKernelGGL(k_msm_bases_fl2, dim3(msm_blocks(n, 256)), dim3(256), 0, s, bases, n,
                            reinterpret_cast<uint32_t*>(base + p.off_basefl));
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t spw = p.B / p.L;
@@ -1018,20 +1241,39 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
         if constexpr (G == 1)
             hipLaunchKernelGGL(k_msm_chunk_acc_fl, dim3(msm_blocks(chunks, 64)), dim3(64), 0, st, bases, basefl,
                                keys_out, vals_out, start, wtot, w0, w1, p.T, p.W * p.B, buckets, cont);
+        else if (g2_lazy)
+            hipLaunchKernelGGL(k_msm_chunk_acc_fl2, dim3(msm_blocks(chunks, 64)), dim3(64), 0, st, basefl, keys_out,
+                               vals_out, start, wtot, w0, w1, p.T, p.W * p.B, buckets, cont);
         else
             hipLaunchKernelGGL(k_msm_chunk_acc<G>, dim3(msm_blocks(chunks, 64)), dim3(64), 0, st, bases, keys_out,
                                vals_out, start, wtot, w0, w1, p.T, p.W * p.B, buckets, cont);
         return hipGetLastError();
     };
     // ... and its bucket -> window-sum reduction
-    auto reduce = [&](uint32_t w0, uint32_t w1, hipStream_t st) {
+    // (part q: long-bucket list at long_list + b0, its count at long_count[q])
+    uint32_t* long_list = reinterpret_cast<uint32_t*>(base + p.off_long);
+    uint32_t* long_count = long_list + nb;
+    const bool lazy = G == 1 || g2_lazy;
+    auto reduce = [&](uint32_t w0, uint32_t w1, uint32_t q, hipStream_t st) {
         const size_t b0 = (size_t)w0 * p.B, b1 = (size_t)w1 * p.B;
-        hipLaunchKernelGGL(k_msm_bucket_fix<G>, dim3(msm_blocks(b1 - b0, 64)), dim3(64), 0, st, start, end, b0, b1,
-                           p.T, cont, buckets);
+        hipError_t r;
+        if (lazy && (r = hipMemsetAsync(long_count + q, 0, 4, st)) != hipSuccess) return r;
+        if (lazy)
+            hipLaunchKernelGGL((k_msm_bucket_fix<G, true>), dim3(msm_blocks(b1 - b0, 64)), dim3(64), 0, st, start, end,
+                               b0, b1, p.T, cont, buckets, long_list + b0, long_count + q);
+        else
+            hipLaunchKernelGGL((k_msm_bucket_fix<G, false>), dim3(msm_blocks(b1 - b0, 64)), dim3(64), 0, st, start,
+                               end, b0, b1, p.T, cont, buckets, nullptr, long_count + q);
+        if (lazy)
+            hipLaunchKernelGGL(k_msm_long_fix<G>, dim3(kMsmLongBlocks), dim3(LazyJac<G>::NT), 0, st, start, end, p.T,
+                               cont, buckets, long_list + b0, long_count + q);
         const size_t t0 = (size_t)w0 * spw, t1 = (size_t)w1 * spw;
         if constexpr (G == 1)
             hipLaunchKernelGGL(k_msm_segments_fl, dim3(msm_blocks(t1 - t0, 64)), dim3(64), 0, st, buckets, p.B, p.L,
                                t0, t1, segs);
+        else if (g2_lazy)
+            hipLaunchKernelGGL(k_msm_segments_fl2, dim3(msm_blocks(t1 - t0, 64)), dim3(64), 0, st, buckets, p.B,
+                               p.L, t0, t1, segs);
         else
             hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(t1 - t0, 64)), dim3(64), 0, st, buckets, p.B, p.L,
                                t0, t1, segs);
@@ -1041,6 +1283,9 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
             const size_t outs = (size_t)(w1 - w0) * gpw;
             if constexpr (G == 1)
                 hipLaunchKernelGGL(k_msm_group_sum_fl, dim3(msm_blocks(4 * outs, 64)), dim3(64), 0, st, src, count,
+                                   group, gpw, w0, w1, spw, dst);
+            else if (g2_lazy)
+                hipLaunchKernelGGL(k_msm_group_sum_fl2, dim3(msm_blocks(outs, 64)), dim3(64), 0, st, src, count,
                                    group, gpw, w0, w1, spw, dst);
             else
                 hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks(outs, 64)), dim3(64), 0, st, src, count, group,
@@ -1056,7 +1301,7 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     static const bool horner_wave = getenv("PA_MSM_HORNER") && atoi(getenv("PA_MSM_HORNER")) == 1;
     const uint32_t parts = horner_wave ? 1 : msm_parts(p.W);
     if (parts == 1) {
-        if ((e = accumulate(0, p.W, s)) != hipSuccess || (e = reduce(0, p.W, s)) != hipSuccess) return e;
+        if ((e = accumulate(0, p.W, s)) != hipSuccess || (e = reduce(0, p.W, 0, s)) != hipSuccess) return e;
         if (!horner_wave)
             hipLaunchKernelGGL(k_msm_horner_q<G>, dim3(1), dim3(64), 0, s, wsum, spw, (int)p.W, 0, p.c, nullptr, out);
         else if constexpr (G == 1)
@@ -1095,14 +1340,14 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
         uint64_t* leg_out = q + 1 == parts ? out : hacc + (size_t)JW * q;
         const uint64_t* leg_in = q == 0 ? nullptr : hacc + (size_t)JW * (q - 1);
         if (q + 1 == parts) {
-            if (!ck(reduce(w0, w1, s)) || !ck(hipStreamWaitEvent(s, ev[2 * parts], 0))) break;
+            if (!ck(reduce(w0, w1, q, s)) || !ck(hipStreamWaitEvent(s, ev[2 * parts], 0))) break;
             hipLaunchKernelGGL(k_msm_horner_q<G>, dim3(1), dim3(64), 0, s, wsum, spw, (int)w1, (int)w0, p.c, leg_in,
                                leg_out);
             ck(hipGetLastError());
             break;
         }
         if (!ck(hipEventRecord(ev[2 * q], s)) || !ck(hipStreamWaitEvent(red_s, ev[2 * q], 0)) ||
-            !ck(reduce(w0, w1, red_s)) || !ck(hipEventRecord(ev[2 * q + 1], red_s)) ||
+            !ck(reduce(w0, w1, q, red_s)) || !ck(hipEventRecord(ev[2 * q + 1], red_s)) ||
             !ck(hipStreamWaitEvent(hor_s, ev[2 * q + 1], 0)))
             break;
         hipLaunchKernelGGL(k_msm_horner_q<G>, dim3(1), dim3(64), 0, hor_s, wsum, spw, (int)w1, (int)w0, p.c, leg_in,

@@ -156,6 +156,24 @@ def test_g1_multiexp_deterministic(gpu, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("group,n", [(1, 9000), (2, 2000)])
+def test_multiexp_crowded_buckets(gpu, oracle, group, n):
+    """Every scalar equal: one bucket per window holds all n terms, spanning
+    n/64 chunks, so its continuation pieces go through k_msm_long_fix (a block
+    per bucket) instead of one lane; a few infinity bases and a second scalar
+    value keep the rest of the machinery busy"""
+    g = rng(95 + group)
+    gen, msm, eq = ((oracle.g1_mul_generator, gpu.g1_multiexp, oracle.g1_eq) if group == 1 else
+                    (oracle.g2_mul_generator, gpu.g2_multiexp, oracle.g2_eq))
+    p = gen(random_scalars(g, n), NT)
+    s = np.repeat(random_scalars(g, 1), n, axis=0)
+    s[n // 3:n // 3 + 50] = random_scalars(g, 1)
+    set_infinity(p, [5, n // 2])
+    ref = oracle.g1_multiexp if group == 1 else oracle.g2_multiexp
+    assert eq(msm(p, s), ref(p, s, NT)).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("parts,chunk", [("1", "32"), ("3", "8"), ("8", "16"), ("2", "512")])
 def test_multiexp_window_parts(gpu, oracle, parts, chunk):
     """The MSM's launch structure (kernels_msm.hip msm_run): the windows in
