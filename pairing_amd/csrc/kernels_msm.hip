@@ -134,13 +134,18 @@ static inline uint32_t msm_window_bits(size_t n) {
 // 170 / 159 / 171 M terms/s at 2^20 with one part, 64 with two parts 175-177
 // (profiles/r04_msm_parts.txt)
 constexpr uint32_t kMsmChunk = 64;
-static uint32_t msm_chunk() {
-    static const uint32_t t = [] {
+// Below 64 items per lane the chunk shrinks until a part's accumulation has
+// one lane for each of the chip's 256 CUs x 4 SIMDs x 64 (G2 at 2^16: 20 x 2^16
+// items, 320 waves at 64 per lane)
+constexpr size_t kMsmFillLanes = 65536;
+static uint32_t msm_chunk(size_t items, uint32_t parts) {
+    static const int env = [] {
         const char* v = getenv("PA_MSM_CHUNK");
-        const int k = v ? atoi(v) : (int)kMsmChunk;
-        return (uint32_t)(k < 8 ? 8 : (k > 512 ? 512 : k));
+        return v ? atoi(v) : 0;
     }();
-    return t;
+    if (env) return (uint32_t)(env < 8 ? 8 : (env > 512 ? 512 : env));
+    const size_t t = (items + kMsmFillLanes * parts - 1) / (kMsmFillLanes * parts);
+    return (uint32_t)(t < 8 ? 8 : (t > kMsmChunk ? kMsmChunk : t));
 }
 // window parts (msm_run): at most this many, each with a Horner accumulator slot
 constexpr uint32_t kMsmMaxParts = 8;
@@ -153,6 +158,18 @@ constexpr uint32_t kSortIpt = 16;
 constexpr uint32_t kSortTile = 256 * kSortIpt;
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// window parts of one MSM (PA_MSM_PARTS, default 2; 1 = every kernel on the
+// caller's stream in order; 3 and 4 measured slower: the tails compete with the
+// next part's accumulation for SIMDs, profiles/r04_msm_parts.txt)
+static uint32_t msm_parts(uint32_t W) {
+    static const uint32_t parts = [] {
+        const char* v = getenv("PA_MSM_PARTS");
+        const int k = v ? atoi(v) : 2;
+        return (uint32_t)(k < 1 ? 1 : (k > (int)kMsmMaxParts ? (int)kMsmMaxParts : k));
+    }();
+    return parts < W ? parts : W;
+}
 
 static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.c = msm_window_bits(n);
@@ -180,7 +197,7 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.off_buckets = off; off = align256(off + jw * nb);
     p.off_segs = off; off = align256(off + jw * nseg);
     p.off_tmp = off; off = align256(off + jw * nseg);
-    p.T = msm_chunk();
+    p.T = msm_chunk(p.items, msm_parts(p.W));
     p.off_cont = off; off = align256(off + jw * ((p.items + p.T - 1) / p.T + 1));
     p.off_basefl = off; off = align256(off + 4 * (group == 1 ? 28 : 56) * n);
     p.off_hist = off; off = align256(off + 4 * (size_t)p.W * 256 * p.tpw);
@@ -1121,18 +1138,6 @@ size_t msm_workspace_bytes(int group, size_t n) {
     MsmPlan p;
     if (msm_plan(p, group, n) != hipSuccess) return 0;
     return p.total;
-}
-
-// window parts of one MSM (PA_MSM_PARTS, default 2; 1 = every kernel on the
-// caller's stream in order; 3 and 4 measured slower: the tails compete with the
-// next part's accumulation for SIMDs, profiles/r04_msm_parts.txt)
-static uint32_t msm_parts(uint32_t W) {
-    static const uint32_t parts = [] {
-        const char* v = getenv("PA_MSM_PARTS");
-        const int k = v ? atoi(v) : 2;
-        return (uint32_t)(k < 1 ? 1 : (k > (int)kMsmMaxParts ? (int)kMsmMaxParts : k));
-    }();
-    return parts < W ? parts : W;
 }
 
 // two non-blocking side streams per device (bucket reduction, Horner legs)
