@@ -279,7 +279,8 @@ hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* o
     // Default: the lazy 28-bit core (k_fq_mul_batch_fl, 29.4 us at 2^20
     // against 32.5 us for the 12 x u32 kernel, profiles/r02_fq_variants.txt;
     // wave-coalesced LDS-DMA transfers measured 3 us slower in round 4,
-    // profiles/r04_fq_glds_icache.txt).
+    // profiles/r04_fq_glds_icache.txt; nontemporal loads / stores 10 us slower,
+    // a grid-stride prefetching form 3-4 us slower, profiles/r04_fr_fq_ab.txt).
     // PA_FQ_VARIANT=0 selects the 12 x u32 streaming kernel for A/B runs.
     static const int variant = [] {
         const char* e = getenv("PA_FQ_VARIANT");

@@ -96,7 +96,8 @@ hipError_t launch_fr_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* o
     if (blocks > c.max_blocks) blocks = c.max_blocks;
     // 27000 B of (unused) dynamic LDS per 256-thread block caps residency at 5
     // waves per SIMD, as for config 2 (k_fq_mul_batch_fl): 21.2 vs 22.2-22.3 us
-    // at 2^20 uncapped (profiles/r04_fr_fq_ab.txt); PA_FR_LDS overrides it
+    // at 2^20 uncapped; nontemporal loads / stores were 1.5 us slower
+    // (profiles/r04_fr_fq_ab.txt); PA_FR_LDS overrides it
     static const unsigned lds = [] {
         const char* e = getenv("PA_FR_LDS");
         return e ? (unsigned)atoi(e) : 27000u;

@@ -10,13 +10,18 @@
 //                       Montgomery's trick over chunks of points per lane
 //   k_comb_*            fixed-base Wnaf::base(g, n).scalar(s_i) for G2
 //                       (wnaf.rs:93-107, 169-178): the signed base-256 comb of
-//                       kernels_curve.hip on the 12-word core, G2 affine table
-//                       (33 x 128 entries, 845 KB) -- equal as points to the
-//                       reference's wNAF (representation-independent
-//                       PartialEq, ec.rs:45-85).
+//                       kernels_curve.hip, G2 affine table (33 x 128 entries)
+//                       -- equal as points to the reference's wNAF
+//                       (representation-independent PartialEq, ec.rs:45-85).
+//                       Round 4: the base chain on lane-quad groups, the
+//                       entries and the multiply on the lazy Fq2 (curve_fl2.h),
+//                       the table in the lazy core's limbs (224 B per entry);
+//                       the batch normalization stays on the 12-word core.
 #include <mutex>
 
 #include "curve.h"
+#include "curve_fl2.h"
+#include "dec_quad.h"
 #include "launch.h"
 
 namespace pa {
@@ -180,73 +185,98 @@ constexpr int kG2NormChunk = 4;
 constexpr int kCombWindows = 33;   // 8-bit digits of a 256-bit scalar + the final carry
 constexpr int kCombEntries = 128;  // |d| in 1..128
 
-// B_i = 2^(8i) g, i in [0, 33): one wave, eight doublings per base, the seven
-// products of each doubling over three lanes (jac_double_3lane).
-template <int G>
-__global__ void __launch_bounds__(64) k_comb_bases(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases) {
-    using F = typename Grp<G>::F;
-    constexpr int JW = Grp<G>::JW;
+// B_i = 2^(8i) g, i in [0, 33), on a group of eight lane quads (dec_quad.h, as
+// k_g1_comb_bases: each doubling three levels of side-by-side products, one Fq2
+// coordinate per quad; round 4, was three lanes on the 12-word core) -- the
+// 256-doubling chain is the G2 table's latency; canonical at the store
+__global__ void __launch_bounds__(64) k_comb_bases_g2q(const uint64_t* __restrict__ base, uint64_t* __restrict__ bases) {
+    constexpr int JW = Grp<2>::JW;
+    if (blockIdx.x != 0) return;
     const int lane = threadIdx.x;
-    Jac<F> p;
-    load_jac(p, base);
+    Jac<Fq2> p0;
+    load_jac(p0, base);
+    if (jac_is_zero(p0)) {
+        if (lane == 0)
+            for (int i = 0; i < kCombWindows; i++) store_jac(bases + JW * i, p0);
+        return;
+    }
+    if (lane >= 32) return;
+    const dq::Lc l = dq::lctx(lane, 8);
+    dq::Jq<dq::Q2> p;
+    p.x = {dq::from_abi(p0.x.c0, l), dq::from_abi(p0.x.c1, l)};
+    p.y = {dq::from_abi(p0.y.c0, l), dq::from_abi(p0.y.c1, l)};
+    p.z = {dq::from_abi(p0.z.c0, l), dq::from_abi(p0.z.c1, l)};
 #pragma unroll 1
     for (int i = 0; i < kCombWindows; i++) {
         if (i > 0) {
 #pragma unroll 1
-            for (int k = 0; k < 8; k++) jac_double_3lane(p, lane);
+            for (int k = 0; k < 8; k++) dq::jdbl<8>(p, l);
         }
-        if (lane == 0) store_jac(bases + JW * i, p);
+        const Fq v[6] = {dq::to_abi(p.x.c0), dq::to_abi(p.x.c1), dq::to_abi(p.y.c0),
+                         dq::to_abi(p.y.c1), dq::to_abi(p.z.c0), dq::to_abi(p.z.c1)};
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < 6; k++) fq_store(bases + JW * i + 6 * k, v[k]);
     }
 }
 
-// T[i][d-1] = d B_i (Jacobian), one lane per entry: double-and-add over d's 8 bits
-template <int G>
-__global__ void __launch_bounds__(64) k_comb_fill(const uint64_t* __restrict__ bases, uint64_t* __restrict__ table_jac) {
-    using F = typename Grp<G>::F;
-    constexpr int JW = Grp<G>::JW;
+// T[i][d-1] = d B_i (Jacobian), one lane per entry: double-and-add over d's 8
+// bits on the lazy core's Fq2 (dbl-2009-l / add-2007-bl, curve_fl2.h; round 4),
+// canonical at the store
+__global__ void __launch_bounds__(64) k_comb_fill_fl2(const uint64_t* __restrict__ bases,
+                                                      uint64_t* __restrict__ table_jac) {
+    constexpr int JW = Grp<2>::JW;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= kCombWindows * kCombEntries) return;
     const int i = e / kCombEntries, d = e % kCombEntries + 1;
-    Jac<F> b, acc;
-    load_jac(b, bases + JW * i);
-    jac_zero(acc);
+    const FlJac2 b = fl2_load_jac(bases + JW * i);
+    FlJac2 acc = fl2_jac_zero();
 #pragma unroll 1
     for (int bit = 7; bit >= 0; bit--) {
-        jac_double(acc);
-        if ((d >> bit) & 1) jac_add(acc, b);
+        if (!f2_is_zero(acc.z)) fl2_jac_double(acc);
+        if ((d >> bit) & 1) fl2_jac_add(acc, b);
     }
-    store_jac(table_jac + (size_t)JW * e, acc);
+    if (f2_is_zero(acc.z)) {
+        Jac<Fq2> z;
+        jac_zero(z);
+        store_jac(table_jac + (size_t)JW * e, z);
+    } else {
+        fl2_store_jac(table_jac + (size_t)JW * e, acc);
+    }
 }
 
-// normalized Jacobian entries -> affine records (zero -> infinity flag)
-template <int G>
-__global__ void __launch_bounds__(64) k_comb_pack(const uint64_t* __restrict__ table_jac, uint64_t* __restrict__ table) {
-    using F = typename Grp<G>::F;
+// G2 table entries in the lazy core's limbs: x.c0, x.c1, y.c0, y.c1 as 14 u32
+// each, the infinity flag in bit 31 of x.c0's top limb (below 2^18 for F<1>)
+constexpr int kFl2Words = 28;   // u64 per entry
+__global__ void __launch_bounds__(64) k_comb_pack_fl2(const uint64_t* __restrict__ table_jac,
+                                                      uint64_t* __restrict__ table) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= kCombWindows * kCombEntries) return;
-    Jac<F> p;
-    load_jac(p, table_jac + (size_t)Grp<G>::JW * e);
-    Aff<F> a;
-    a.inf = jac_is_zero(p);
-    a.x = p.x;
-    a.y = p.y;
-    store_aff(table + (size_t)Grp<G>::AW * e, a);
+    Jac<Fq2> p;
+    load_jac(p, table_jac + (size_t)Grp<2>::JW * e);
+    const bool inf = jac_is_zero(p);
+    const F<1> v[4] = {fl_from_abi(p.x.c0), fl_from_abi(p.x.c1), fl_from_abi(p.y.c0), fl_from_abi(p.y.c1)};
+    uint32_t* d = reinterpret_cast<uint32_t*>(table + (size_t)kFl2Words * e);
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int k = 0; k < 14; k++) d[14 * c + k] = v[c].w[k] | (c == 0 && k == 13 && inf ? 0x80000000u : 0u);
 }
 
 // s g = sum_i sign(d_i) T[i][|d_i|], digits d_i in [-127, 128] (carry into the
-// next window), mixed additions from zero (madd-2007-bl, ec.rs:446-526)
-template <int G>
-__global__ void __launch_bounds__(64) k_comb_mul(const uint64_t* __restrict__ table, const uint64_t* __restrict__ scalars,
-                                                 uint64_t* __restrict__ out, size_t n, int window) {
-    using F = typename Grp<G>::F;
+// next window), mixed additions from zero (madd-2007-bl, ec.rs:446-526) on the
+// lazy core's Fq2 (curve_fl2.h), canonical at the store
+__global__ void __launch_bounds__(64) k_comb_mul_fl2(const uint64_t* __restrict__ table,
+                                                     const uint64_t* __restrict__ scalars, uint64_t* __restrict__ out,
+                                                     size_t n, int window) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t s[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) s[w] = scalars[4 * i + w];
     const bool flip = wnaf_wrap(s, window);   // the reference's digits spell -(2^256 - s)
-    Jac<F> acc;
-    jac_zero(acc);
+    FlJac2 acc = fl2_jac_zero();
+    bool untouched = true;
     int carry = 0;
 #pragma unroll 1
     for (int win = 0; win < kCombWindows; win++) {
@@ -255,12 +285,28 @@ __global__ void __launch_bounds__(64) k_comb_mul(const uint64_t* __restrict__ ta
         carry = d > 128 ? 1 : 0;
         if (d > 128) d -= 256;
         if (d == 0) continue;
-        Aff<F> t;
-        load_aff(t, table + (size_t)Grp<G>::AW * (win * kCombEntries + (d < 0 ? -d : d) - 1));
-        if ((d < 0) != flip && !t.inf) neg(t.y, t.y);
-        jac_add_mixed(acc, t);
+        const uint2* src = reinterpret_cast<const uint2*>(table + (size_t)kFl2Words *
+                                                                     (win * kCombEntries + (d < 0 ? -d : d) - 1));
+        F<1> c[4];
+#pragma unroll
+        for (int q = 0; q < 28; q++) {
+            const uint2 t = src[q];
+            c[q / 7].w[2 * (q % 7)] = t.x;
+            c[q / 7].w[2 * (q % 7) + 1] = t.y;
+        }
+        if ((c[0].w[13] >> 31) != 0) continue;   // an infinity entry: add_assign_mixed's no-op
+        const F2<1> y = {c[2], c[3]};
+        const F2<2> oy = ((d < 0) != flip) ? neg(y) : relax<2>(y);
+        fl2_jac_add_mixed(acc, untouched, F2<1>{c[0], c[1]}, oy);
     }
-    store_jac(out + (size_t)Grp<G>::JW * i, acc);
+    uint64_t* o = out + (size_t)Grp<2>::JW * i;
+    if (untouched) {
+        Jac<Fq2> z;
+        jac_zero(z);
+        store_jac(o, z);
+    } else {
+        fl2_store_jac(o, acc);
+    }
 }
 
 }  // namespace
@@ -278,25 +324,25 @@ hipError_t launch_g2_batch_normalize(uint64_t* v, size_t n, hipStream_t stream) 
     return hipGetLastError();
 }
 
-size_t g2_comb_table_words() { return (size_t)Grp<2>::AW * kCombWindows * kCombEntries; }
+size_t g2_comb_table_words() { return (size_t)kFl2Words * kCombWindows * kCombEntries; }
 size_t g2_comb_workspace_words() { return (size_t)Grp<2>::JW * kCombWindows * (1 + kCombEntries); }
 
 hipError_t launch_g2_comb_table(const uint64_t* base, uint64_t* table, uint64_t* workspace, hipStream_t stream) {
     uint64_t* bases = workspace;
     uint64_t* table_jac = workspace + (size_t)Grp<2>::JW * kCombWindows;
     const unsigned entries = kCombWindows * kCombEntries;
-    hipLaunchKernelGGL(k_comb_bases<2>, dim3(1), dim3(64), 0, stream, base, bases);
-    hipLaunchKernelGGL(k_comb_fill<2>, dim3(blocks_for(entries, 64)), dim3(64), 0, stream, bases, table_jac);
+    hipLaunchKernelGGL(k_comb_bases_g2q, dim3(1), dim3(64), 0, stream, base, bases);
+    hipLaunchKernelGGL(k_comb_fill_fl2, dim3(blocks_for(entries, 64)), dim3(64), 0, stream, bases, table_jac);
     hipError_t e = launch_g2_batch_normalize(table_jac, entries, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_comb_pack<2>, dim3(blocks_for(entries, 64)), dim3(64), 0, stream, table_jac, table);
+    hipLaunchKernelGGL(k_comb_pack_fl2, dim3(blocks_for(entries, 64)), dim3(64), 0, stream, table_jac, table);
     return hipGetLastError();
 }
 
 hipError_t launch_g2_comb_mul(const uint64_t* table, const uint64_t* scalars, uint64_t* out, size_t n,
                               int window, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_comb_mul<2>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table, scalars, out, n, window);
+    hipLaunchKernelGGL(k_comb_mul_fl2, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table, scalars, out, n, window);
     return hipGetLastError();
 }
 
