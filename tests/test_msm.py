@@ -208,3 +208,47 @@ def test_multiexp_window_parts(gpu, oracle, parts, chunk):
         o1, o2 = np.load(os.path.join(d, "o1.npy")), np.load(os.path.join(d, "o2.npy"))
     assert oracle.g1_eq(o1, oracle.g1_multiexp(p1, s1, NT)).all()
     assert oracle.g2_eq(o2, oracle.g2_multiexp(p2, s2, NT)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group,n", [(1, 1 << 20), (2, 1 << 18)])
+def test_multiexp_bench_size_identity(gpu, oracle, group, n):
+    """bench.py --workload msm's size (2^20 G1 terms: c = 16, two window parts
+    on side streams, 64-item chunks) and 2^18 G2 terms (c = 15, whose
+    carry-only top window crowds ~45 % of the terms into one bucket, folded by
+    k_msm_long_fix): bases a_i g made on the device (fixed-base comb + batch
+    normalization, both checked elsewhere), the size-independent identity
+    sum s_i (a_i g) = (sum s_i a_i mod r) g; a run of equal scalars and a few
+    zeros ride along"""
+    import torch
+    import pairing_amd.device as pdev
+    from helpers import from_limbs
+    g = rng(120 + group)
+    a = random_scalars(g, n)
+    s = random_scalars(g, n)
+    s[1000:3000] = s[5]
+    s[7:12] = 0
+    w, aw = (18, 13) if group == 1 else (36, 25)
+    gen_aff = (oracle.g1_mul_generator if group == 1 else oracle.g2_mul_generator)(small_scalars([1]))
+    base = torch.from_numpy((oracle.g1_from_affine if group == 1 else oracle.g2_from_affine)(gen_aff)
+                            .view(np.int64)).cuda()
+    ka = torch.from_numpy(a.view(np.int64)).cuda()
+    jac = pdev.empty_records(n, w, "cuda")
+    if group == 1:
+        table, _ = pdev.g1_fixed_base_table(base)
+        pdev.g1_fixed_base_mul(table, ka, jac)
+        pdev.g1_batch_normalization(jac)
+    else:
+        table, ws = pdev.g2_fixed_base_buffers("cuda")
+        pdev.g2_wnaf_fixed_base(base, ka, jac, table, ws)
+        pdev.g2_batch_normalization(jac)
+    bases = torch.zeros((n, aw), dtype=torch.int64, device="cuda")
+    bases[:, :aw - 1] = jac[:, :aw - 1]
+    del jac, table
+    out = pdev.empty_records(1, w, "cuda")
+    pdev.multiexp(group, bases, torch.from_numpy(s.view(np.int64)).cuda(), out, pdev.multiexp_workspace(group, n, "cuda"))
+    torch.cuda.synchronize()
+    tot = sum(from_limbs(x) * from_limbs(y) for x, y in zip(a, s)) % R_ORDER
+    into = oracle.g1_into_affine if group == 1 else oracle.g2_into_affine
+    gen = oracle.g1_mul_generator if group == 1 else oracle.g2_mul_generator
+    np.testing.assert_array_equal(into(out.cpu().numpy().view(np.uint64)), gen(small_scalars([tot])))
