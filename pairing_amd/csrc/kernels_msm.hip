@@ -175,11 +175,15 @@ static hipError_t msm_plan(MsmPlan& p, int group, size_t n) {
     p.c = msm_window_bits(n);
     p.W = (257 + p.c - 1) / p.c;
     p.B = 1u << (p.c - 1);
-    static const uint32_t seg = [] {   // A/B knob: PA_MSM_SEG (default 8)
+    // A/B knob: PA_MSM_SEG; default 8 buckets per segment for G1, 4 for G2 (G2
+    // at 2^16 / 2^18: 5.91 / 9.13 ms with 8, 5.73 / 8.90 with 4; G1 at 2^20: 173
+    // vs 163 M terms/s; profiles/r04_msm_g2_lazy.txt)
+    static const int seg_env = [] {
         const char* v = getenv("PA_MSM_SEG");
-        const int k = v ? atoi(v) : 8;
-        return (uint32_t)(k == 2 || k == 4 || k == 16 || k == 32 ? k : 8);
+        const int k = v ? atoi(v) : 0;
+        return k == 2 || k == 4 || k == 8 || k == 16 || k == 32 ? k : 0;
     }();
+    const uint32_t seg = seg_env ? (uint32_t)seg_env : (group == 1 ? 8u : 4u);
     p.L = p.B < seg ? p.B : seg;  // short segments: the running sums are a latency chain per lane
     p.items = (size_t)p.W * n;
     p.passes = (p.c - 1 + 7) / 8;
