@@ -647,6 +647,7 @@ __global__ void __launch_bounds__(64) PA_MSM_ACC_ATTR k_msm_chunk_acc_fl(const u
     msm_flush_fl(cur, acc, untouched, j0, k, start, buckets, cont);
 }
 
+
 // One lane per bucket: empty buckets become the identity; a bucket spanning
 // several chunks adds the continuation pieces of the chunks after its first.
 template <int G, bool LAZY>
