@@ -1365,6 +1365,12 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
         if (!ck(hipGetLastError())) break;
         if (q + 2 == parts) ck(hipEventRecord(ev[2 * parts], hor_s));
     }
+    if (err != hipSuccess) {
+        // a failed launch sequence: let work already queued on the side streams
+        // drain before the caller may release the workspace
+        (void)hipStreamSynchronize(red_s);
+        (void)hipStreamSynchronize(hor_s);
+    }
     for (int k = 0; k < made; k++) (void)hipEventDestroy(ev[k]);
     (void)JW;
     return err;
