@@ -43,7 +43,7 @@ def value(limbs):
     return sum(int(x) << (28 * i) for i, x in enumerate(limbs))
 
 
-def run(op, cases):
+def run(op, cases, kernel="coop_quad_unit", per_block=64):
     import torch
     import hipmod
     n = len(cases)
@@ -53,9 +53,9 @@ def run(op, cases):
             buf[i, k, :14] = limbs
     src = torch.from_numpy(buf.view(np.int32)).cuda()
     out = torch.zeros((n, 2, 16), dtype=torch.int32, device="cuda")
-    hipmod.launch_kernel(CO, "coop_quad_unit",
+    hipmod.launch_kernel(CO, kernel,
                          [(ctypes.c_uint64, src.data_ptr()), (ctypes.c_uint64, out.data_ptr()),
-                          (ctypes.c_uint32, n), (ctypes.c_uint32, op)], (n + 63) // 64, 256)
+                          (ctypes.c_uint32, n), (ctypes.c_uint32, op)], (n + per_block - 1) // per_block, 256)
     return out.cpu().numpy().view(np.uint32)
 
 
@@ -97,3 +97,26 @@ def test_quad_ops_bit_identical_to_one_lane(op):
             want = va
         assert r % Q == want % Q and r < 2 * Q, (op, i)
         assert all(int(x) <= M for x in got[i, 0, :13]) and got[i, 0, 14] == 0 and got[i, 0, 15] == 0
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 4], ids=["mul", "sop2", "sqr", "gather_mul"])
+def test_hex_ops_bit_identical_to_one_lane(op):
+    """coop_hex.h (experiment): one value per 16-lane DPP row, the digit
+    broadcast by row_newbcast and the accumulator shift by row_shl -- the same
+    limbs as the one-lane leaves at the bounds the quad test uses"""
+    g = random.Random(200 + op)
+    cases = []
+    for bnd in BOUNDS[op]:
+        for t in range(160):
+            edge = "max" if t % 40 == 0 else "zero" if t % 40 == 1 else None
+            if op == 1:
+                (ua, ub), (uc, ud) = bnd
+                cases.append([lazy(g, ua, edge), lazy(g, ub, edge), lazy(g, uc), lazy(g, ud, edge)])
+            elif op == 2:
+                cases.append([lazy(g, bnd[0], edge), [0] * 14, [0] * 14, [0] * 14])
+            else:
+                ua, ub = bnd
+                cases.append([lazy(g, ua, edge), lazy(g, ub), [0] * 14, [0] * 14])
+    got = run(op, cases, kernel="coop_hex_unit", per_block=16)
+    assert (got[:, 0, :] == got[:, 1, :]).all(), \
+        "hex != one-lane at cases %s" % np.nonzero((got[:, 0, :] != got[:, 1, :]).any(axis=1))[0][:10]

@@ -70,6 +70,8 @@ for step in "$@"; do
         cooptests) run pytest_coop 600 python -u -m pytest tests/test_gpu_parity.py tests/test_bench_sizes.py -m gpu -k "coop or multi_pairing" -x -v --timeout 200 --timeout-method thread ;;
         coopprof) run coop_prof 120 ./tools/coop_prof ;;
         quadtests) run pytest_quad 300 python -u -m pytest tests/test_coop_quad.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+        hextests) run pytest_hex 300 python -u -m pytest tests/test_coop_quad.py -m gpu -v --timeout 120 --timeout-method thread ;;
+        hexlat) run hex_latency 120 python tools/hex_latency.py 2000 ;;
         cooplat_small) run coop_latency 300 python tools/coop_latency.py 1 2 16 64 256 1024 2048 ;;
         cooplat) run coop_latency 300 python tools/coop_latency.py ;;
         distwl) for w in fq_mul fr_mul wnaf decode msm; do
