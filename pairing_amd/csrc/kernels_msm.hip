@@ -928,6 +928,7 @@ __global__ void __launch_bounds__(64) k_msm_segments_fl(const uint64_t* __restri
     fl_store_jac(segs + (size_t)JW * t, S);
 }
 
+
 // ---- G2 bucket phases on the lazy core's Fq2 (curve_fl2.h; round 4) ----
 // The affine bases converted once per MSM (x.c0, x.c1, y.c0, y.c1 -> 56 u32;
 // the infinity flag in bit 31 of x.c0's top limb, below 2^18 for F<1>) ...
@@ -1264,6 +1265,26 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     uint32_t* long_list = reinterpret_cast<uint32_t*>(base + p.off_long);
     uint32_t* long_count = long_list + nb;
     const bool lazy = G == 1 || g2_lazy;
+    // segment sums -> one per window, `group` at a time, windows [w0, w1)
+    auto group_levels = [&](uint32_t w0, uint32_t w1, hipStream_t st) {
+        uint64_t *src = segs, *dst = tmp;
+        for (uint32_t count = spw; count > 1;) {
+            const uint32_t gpw = (count + group - 1) / group;
+            const size_t outs = (size_t)(w1 - w0) * gpw;
+            if constexpr (G == 1)
+                hipLaunchKernelGGL(k_msm_group_sum_fl, dim3(msm_blocks(4 * outs, 64)), dim3(64), 0, st, src, count,
+                                   group, gpw, w0, w1, spw, dst);
+            else if (g2_lazy)
+                hipLaunchKernelGGL(k_msm_group_sum_fl2, dim3(msm_blocks(outs, 64)), dim3(64), 0, st, src, count,
+                                   group, gpw, w0, w1, spw, dst);
+            else
+                hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks(outs, 64)), dim3(64), 0, st, src, count, group,
+                                   gpw, w0, w1, spw, dst);
+            count = gpw;
+            std::swap(src, dst);
+        }
+        return hipGetLastError();
+    };
     auto reduce = [&](uint32_t w0, uint32_t w1, uint32_t q, hipStream_t st) {
         const size_t b0 = (size_t)w0 * p.B, b1 = (size_t)w1 * p.B;
         hipError_t r;
@@ -1287,23 +1308,7 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
         else
             hipLaunchKernelGGL(k_msm_segments<G>, dim3(msm_blocks(t1 - t0, 64)), dim3(64), 0, st, buckets, p.B, p.L,
                                t0, t1, segs);
-        uint64_t *src = segs, *dst = tmp;
-        for (uint32_t count = spw; count > 1;) {
-            const uint32_t gpw = (count + group - 1) / group;
-            const size_t outs = (size_t)(w1 - w0) * gpw;
-            if constexpr (G == 1)
-                hipLaunchKernelGGL(k_msm_group_sum_fl, dim3(msm_blocks(4 * outs, 64)), dim3(64), 0, st, src, count,
-                                   group, gpw, w0, w1, spw, dst);
-            else if (g2_lazy)
-                hipLaunchKernelGGL(k_msm_group_sum_fl2, dim3(msm_blocks(outs, 64)), dim3(64), 0, st, src, count,
-                                   group, gpw, w0, w1, spw, dst);
-            else
-                hipLaunchKernelGGL(k_msm_group_sum<G>, dim3(msm_blocks(outs, 64)), dim3(64), 0, st, src, count, group,
-                                   gpw, w0, w1, spw, dst);
-            count = gpw;
-            std::swap(src, dst);
-        }
-        return hipGetLastError();
+        return group_levels(w0, w1, st);
     };
 
     // the round-3 one-wave Horner kernels (PA_MSM_HORNER=1: three-lane
