@@ -150,9 +150,14 @@ static uint32_t msm_chunk(size_t items, uint32_t parts) {
 // window parts (msm_run): at most this many, each with a Horner accumulator slot
 constexpr uint32_t kMsmMaxParts = 8;
 // a bucket whose items span more chunks than this has its continuation pieces
-// summed by a block (k_msm_long_fix), not serially by one lane of k_msm_bucket_fix
-constexpr size_t kMsmLongSpan = 8;
-constexpr unsigned kMsmLongBlocks = 64;
+// summed by a block (k_msm_long_fix), not serially by one lane of
+// k_msm_bucket_fix.  A block costs ~span/256 + 8 additions per bucket with at
+// most kMsmLongBlocks buckets at a time, a lane `span` additions with every
+// bucket at once: above 128 chunks the block is never the slower choice, even
+// when every bucket of every window is that long (at most ~2 100 of them at
+// 2^20 terms)
+constexpr size_t kMsmLongSpan = 128;
+constexpr unsigned kMsmLongBlocks = 256;
 // counting sort: a tile is 16 rounds of one item per thread of a 256-thread block
 constexpr uint32_t kSortIpt = 16;
 constexpr uint32_t kSortTile = 256 * kSortIpt;
