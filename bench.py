@@ -254,6 +254,23 @@ def cpu_baseline_wnaf(base, scalars, seconds):
                       "restatement, OpenMP over scalars, %.1f s wall" % (n, wall)}
 
 
+def _check_work_json(work_path):
+    """The VALU roofline's MAC count comes from pa_gen_work.json, written by
+    tools/pgen/build_gen.py next to the code objects it counts.  A missing file
+    or one older than those code objects would price the kernels with stale
+    counts, so fail loudly instead of reporting a roofline."""
+    if not os.path.exists(work_path):
+        raise SystemExit("bench.py: %s is missing (run `make -C pairing_amd`)" % work_path)
+    lib = os.path.dirname(work_path)
+    t = os.path.getmtime(work_path)
+    for co in ("pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco"):
+        cp = os.path.join(lib, co)
+        # code objects are written first, the work file right after them
+        if os.path.exists(cp) and os.path.getmtime(cp) > t + 60:
+            raise SystemExit("bench.py: %s is older than %s (rebuild with `make -C pairing_amd`)"
+                             % (work_path, cp))
+
+
 def measure_copy_gbs(nbytes, dev, stream, reps=20):
     """Device-to-device copy of nbytes/2 (nbytes moved: half read, half
     written) timed with HIP events: the achievable streaming rate on this box."""
@@ -812,8 +829,8 @@ def main():
             roof["copy_GBs"] = round(copy_gbs, 1)
             roof["frac_of_copy"] = achieved / copy_gbs
         work_path = os.path.join(ROOT, "pairing_amd", "lib", "pa_gen_work.json")
-        if (args.workload == "pairing" or (args.workload == "prepared" and dom_name == "final_exponentiation")) \
-                and os.path.exists(work_path):
+        if args.workload == "pairing" or (args.workload == "prepared" and dom_name == "final_exponentiation"):
+            _check_work_json(work_path)
             # the pairing kernels are VALU-issue bound (multiply-accumulate
             # chains), not HBM bound: report that roofline, with the HBM view
             # kept alongside

@@ -16,7 +16,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# PA_ORACLE_LIB selects another build of the same sources (the sanitizer
+# build `make -C oracle asan` -> liboracle_asan.so, tests/test_sanitizer.py)
+LIB_PATH = os.environ.get("PA_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 
 W_FQ, W_FQ2, W_FQ6, W_FQ12 = 6, 12, 36, 72
 W_G1A, W_G1, W_G2A, W_G2 = 13, 18, 25, 36

@@ -2,6 +2,7 @@
 // buffers for the host-pointer entry points, error reporting.  No compute
 // happens here; every entry point ends in a HIP kernel from
 // kernels_field.hip / kernels_pairing.hip.
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -32,7 +33,9 @@ thread_local std::string g_last_error;
 // 1 -> lane pairs for every batch size; 2 -> cooperative for every batch
 // size; 3 -> one lane per pairing for every batch size; 4 -> cooperative for
 // every batch size on the round-2 one-wave VM (A/B against the quad VM).
-int g_pairing_variant = 0;
+// written by pa_set_pairing_kernel and read by launches from any host thread
+std::atomic<int> g_pairing_variant{0};
+int pairing_variant() { return g_pairing_variant.load(std::memory_order_relaxed); }
 
 size_t env_size(const char* name, size_t dflt) {
     const char* e = getenv(name);   // A/B measurements
@@ -47,13 +50,15 @@ size_t pair_max() {
     return v;
 }
 bool use_coop(size_t n) {
-    return g_pairing_variant == 2 || g_pairing_variant == 4 || (g_pairing_variant == 0 && n <= coop_max());
+    const int v = pairing_variant();
+    return v == 2 || v == 4 || (v == 0 && n <= coop_max());
 }
-int coop_vm() { return g_pairing_variant == 4 ? 1 : 0; }
+int coop_vm() { return pairing_variant() == 4 ? 1 : 0; }
 // lanes per pairing of the generated kernels
 int gen_lanes(size_t n) {
-    if (g_pairing_variant == 1) return 2;
-    if (g_pairing_variant == 3) return 1;
+    const int v = pairing_variant();
+    if (v == 1) return 2;
+    if (v == 3) return 1;
     return n <= pair_max() ? 2 : 1;
 }
 // multi-pairings of at most this many pairs multiply their Miller values inside
@@ -302,7 +307,7 @@ int pa_set_device(int device) {
 }
 int pa_set_pairing_kernel(int variant) {
     if (variant < 0 || variant > 4) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..4");
-    g_pairing_variant = variant;
+    g_pairing_variant.store(variant, std::memory_order_relaxed);
     return PA_OK;
 }
 int pa_set_decode_kernel(int variant) {

@@ -13,6 +13,7 @@
 // identities phi(P) == -[x^2]P (G1) and psi(P) == [x]P (G2), see
 // in_subgroup below.  Records are
 // read as 32-bit words and byte-swapped (the wire format is big-endian).
+#include <atomic>
 #include <type_traits>
 
 #include "curve.h"
@@ -847,7 +848,7 @@ unsigned blocks_for(size_t n) { return (unsigned)((n + 63) / 64); }
 }  // namespace
 
 namespace {
-int g_decode_variant = 0;   // pa_set_decode_kernel: 0 by batch size, 1 one lane per record, 2 quad groups
+std::atomic<int> g_decode_variant{0};   // pa_set_decode_kernel (any host thread): 0 by batch size, 1 one lane per record, 2 quad groups
 size_t decode_quad_max() {
     static const size_t v = [] {
         const char* e = getenv("PA_DECODE_QUAD_MAX");
@@ -856,15 +857,15 @@ size_t decode_quad_max() {
     return v;
 }
 }  // namespace
-void set_decode_variant(int v) { g_decode_variant = v; }
+void set_decode_variant(int v) { g_decode_variant.store(v, std::memory_order_relaxed); }
 
 hipError_t launch_decode(int group, int compressed, int checked, const uint8_t* enc, size_t n, uint64_t* out,
                          uint8_t* status, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     // the latency form for small batches with field work (an uncompressed
     // unchecked decode is byte handling only: one lane per record)
-    const bool quad = (compressed || checked) &&
-                      (g_decode_variant == 2 || (g_decode_variant == 0 && n <= decode_quad_max()));
+    const int dv = g_decode_variant.load(std::memory_order_relaxed);
+    const bool quad = (compressed || checked) && (dv == 2 || (dv == 0 && n <= decode_quad_max()));
     if (quad) {
         const unsigned per = group == 1 ? 4 : 2;   // records per 64-lane block
         const unsigned bq = (unsigned)((n + per - 1) / per);

@@ -1151,10 +1151,14 @@ size_t msm_workspace_bytes(int group, size_t n) {
     return p.total;
 }
 
-// two non-blocking side streams per device (bucket reduction, Horner legs)
-static hipError_t msm_side_streams(hipStream_t out[2]) {
+// two non-blocking side streams per device (bucket reduction, Horner legs),
+// created on the device of the caller's stream.  They are shared by every
+// caller on that device, so MSMs issued concurrently from several host threads
+// serialize their window-part tails through them (results are unaffected: each
+// call orders its own work with events).
+static hipError_t msm_side_streams(hipStream_t caller, hipStream_t out[2]) {
     int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
+    hipError_t e = hipStreamGetDevice(caller, &dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     static std::mutex mu;
@@ -1165,12 +1169,18 @@ static hipError_t msm_side_streams(hipStream_t out[2]) {
     static const bool prio = !getenv("PA_MSM_PRIO") || atoi(getenv("PA_MSM_PRIO")) != 0;
     int lo = 0, hi = 0;
     if (prio && (e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return e;
-    for (int k = 0; k < 2; k++) {
-        if (!side[dev][k] &&
-            (e = hipStreamCreateWithPriority(&side[dev][k], hipStreamNonBlocking, prio ? hi : lo)) != hipSuccess)
-            return e;
-        out[k] = side[dev][k];
+    if (!side[dev][0] || !side[dev][1]) {
+        // streams belong to the current device: create them on the caller's
+        int cur = 0;
+        if ((e = hipGetDevice(&cur)) != hipSuccess) return e;
+        if (cur != dev && (e = hipSetDevice(dev)) != hipSuccess) return e;
+        for (int k = 0; k < 2 && e == hipSuccess; k++)
+            if (!side[dev][k]) e = hipStreamCreateWithPriority(&side[dev][k], hipStreamNonBlocking, prio ? hi : lo);
+        if (cur != dev) (void)hipSetDevice(cur);
+        if (e != hipSuccess) return e;
     }
+    out[0] = side[dev][0];
+    out[1] = side[dev][1];
     return hipSuccess;
 }
 
@@ -1338,7 +1348,7 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     // hide under the next parts' accumulation.  Only the last part's reduction
     // and Horner leg are exposed.  Same window sums, same Horner: same point.
     hipStream_t side[2];
-    if ((e = msm_side_streams(side)) != hipSuccess) return e;
+    if ((e = msm_side_streams(s, side)) != hipSuccess) return e;
     hipStream_t red_s = side[0], hor_s = side[1];
     static const bool serial = getenv("PA_MSM_SERIAL") && atoi(getenv("PA_MSM_SERIAL")) != 0;
     if (serial) red_s = hor_s = s;   // measurement / debugging: the parts in order on the caller's stream
@@ -1376,10 +1386,19 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
         if (q + 2 == parts) ck(hipEventRecord(ev[2 * parts], hor_s));
     }
     if (err != hipSuccess) {
-        // a failed launch sequence: let work already queued on the side streams
-        // drain before the caller may release the workspace
-        (void)hipStreamSynchronize(red_s);
-        (void)hipStreamSynchronize(hor_s);
+        // a failed launch sequence: let this call's work already queued on the
+        // side streams drain before the caller may release the workspace (an
+        // event recorded now waits for that work only, not for what other
+        // callers queue on the shared side streams later)
+        for (hipStream_t x : {red_s, hor_s}) {
+            hipEvent_t done = nullptr;
+            if (hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess &&
+                hipEventRecord(done, x) == hipSuccess)
+                (void)hipEventSynchronize(done);
+            else
+                (void)hipStreamSynchronize(x);
+            if (done) (void)hipEventDestroy(done);
+        }
     }
     for (int k = 0; k < made; k++) (void)hipEventDestroy(ev[k]);
     (void)JW;
