@@ -52,6 +52,9 @@ ML_BYTES = 96 + 192 + 2 + FQ12_BYTES   # P, Q coordinates + flags in, f out
 FE_BYTES = FQ12_BYTES + FQ12_BYTES     # f in, e(P,Q) out
 G2P_BYTES = 68 * 3 * 96 + 8            # G2Prepared record: 68 (Fq2, Fq2, Fq2) lines + infinity word
 ML_PREP_BYTES = G1A_BYTES + G2P_BYTES + FQ12_BYTES
+# one prepared Q for the batch: per pairing only P in and the Fq12 out (the
+# 22.9 KB line table is read from L2 by every wave, once per call from HBM)
+ML_SHARED_BYTES = G1A_BYTES + FQ12_BYTES
 
 
 def parse():
@@ -68,7 +71,7 @@ def parse():
     ap.add_argument("--stub-echo", action="store_true",
                     help="with --cpu-stub: each rank echoes its shard instead of computing pairings "
                          "(plumbing test of large shapes)")
-    ap.add_argument("--workload", choices=["pairing", "prepared", "fq_mul", "fr_mul", "wnaf", "decode", "msm", "verify"],
+    ap.add_argument("--workload", choices=["pairing", "prepared", "prepared_shared", "fq_mul", "fr_mul", "wnaf", "decode", "msm", "verify"],
                     default="pairing")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-work seconds for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -219,6 +222,36 @@ def cpu_baseline_prepared(p, q, seconds):
     return {"value": vt, "unit": "pairings/s", "cores": th, "kind": "port", "host_cores": host, "value_1core": v1,
             "sample": "C restatement of the reference (oracle/): miller_loop_batch over prepared records + "
                       "final_exponentiation, %d pairs on 1 core in %.1f s; %d pairs on %d threads in %.1f s"
+                      % (res[0][2], res[0][3], mt, th, wt)}
+
+
+def cpu_baseline_prepared_shared(p, prep1, seconds):
+    """The oracle's miller_loop of every P_i against ONE prepared Q (the record
+    repeated per pair, as the reference's &G2Prepared in each pair) + final
+    exponentiation, one core then every thread, over a prefix of the batch"""
+    from oracle import binding as oracle
+    host, threads = host_threads()
+
+    def run(m, th):
+        for k in range(0, m, 4096):
+            pc = p[k:min(m, k + 4096)]
+            oracle.final_exponentiation(oracle.miller_loop_batch(pc, np.repeat(prep1, len(pc), axis=0), th), th)
+    res = []
+    for th in sorted({1, threads}):
+        k = 2 * th
+        t0 = time.perf_counter()
+        run(k, th)
+        per = max(time.perf_counter() - t0, 1e-4) / k
+        m = int(max(k, min(len(p), max(5.0, seconds / 2) / per)))
+        t0 = time.perf_counter()
+        run(m, th)
+        wall = time.perf_counter() - t0
+        res.append((th, m / wall, m, wall))
+    v1 = res[0][1]
+    th, vt, mt, wt = res[-1]
+    return {"value": vt, "unit": "pairings/s", "cores": th, "kind": "port", "host_cores": host, "value_1core": v1,
+            "sample": "C restatement of the reference (oracle/): miller_loop_batch of P_i against one prepared Q "
+                      "+ final_exponentiation, %d pairs on 1 core in %.1f s; %d pairs on %d threads in %.1f s"
                       % (res[0][2], res[0][3], mt, th, wt)}
 
 
@@ -493,6 +526,35 @@ def main():
                 ev[2].record(stream)
             if dist_on:
                 gather_rows_to_root(out, n_global)
+    elif args.workload == "prepared_shared":
+        # the verifier's fixed-key shape: every P_i against ONE prepared Q
+        # (Engine::miller_loop with the same &G2Prepared in each pair,
+        # lib.rs:88-96); the record is prepared once before the timed region
+        from pairing_amd._native import W_G2P
+        span = shard_range(args.global_batch, ws, rank) if args.global_batch else None
+        if span:
+            n, n_global = span[1] - span[0], args.global_batch
+        p_np, q_np = make_pairs(n, rank, span=span)
+        q1_np = q_np[[i for i in range(len(q_np)) if not q_np[i, 24] & 0xff][:1]]
+        p = torch.from_numpy(p_np.view(np.int64)).to(dev)
+        qp = pdev.empty_records(1, W_G2P, dev)
+        pdev.g2_prepare(torch.from_numpy(q1_np.view(np.int64)).to(dev), qp, stream)
+        torch.cuda.synchronize()
+        prep1_np = qp.cpu().numpy().view(np.uint64)
+        out = pdev.empty_records(n, 72, dev)
+        scratch = pdev.empty_records(n, 72, dev)
+
+        def step(timed):
+            if timed:
+                ev[0].record(stream)
+            pdev.miller_loop_shared_prepared(p, qp, scratch, stream)
+            if timed:
+                ev[1].record(stream)
+            pdev.final_exponentiation(scratch, out, None, stream)
+            if timed:
+                ev[2].record(stream)
+            if dist_on:
+                gather_rows_to_root(out, n_global)
     elif args.workload == "wnaf":
         # config 3: Wnaf::new().base(g, 2^18).scalar(s_i) + G1::batch_normalization
         n, n_global, idx = shard(args.batch if args.batch != (1 << 16) else (1 << 18))
@@ -712,7 +774,7 @@ def main():
     elapsed = time.perf_counter() - t0
     for e in step_ev:
         k_ms["a"].append(e[0].elapsed_time(e[1]))
-        if args.workload in ("pairing", "prepared", "wnaf", "decode"):
+        if args.workload in ("pairing", "prepared", "prepared_shared", "wnaf", "decode"):
             k_ms["b"].append(e[1].elapsed_time(e[2]))
         if args.workload == "verify" and args.decode:
             k_ms["b"].append(e[0].elapsed_time(e[2]))   # the decodes
@@ -754,6 +816,19 @@ def main():
                       "parallelism": "shard%d+rccl_gather" % ws if dist_on else "single",
                       "kernel_ms": {"miller_loop_prepared": round(ml, 3), "final_exponentiation": round(fe, 3),
                                     "untimed: g2_prepare": round(float(np.median(prep_ms)), 3)}}
+        elif args.workload == "prepared_shared":
+            ml = float(np.mean(k_ms["a"]))
+            fe = float(np.mean(k_ms["b"]))
+            dom_name, dom_ms, dom_bytes = ("final_exponentiation", fe, FE_BYTES) if fe >= ml else \
+                ("miller_loop_shared", ml, ML_SHARED_BYTES)
+            value = n_global * args.steps / elapsed
+            metric, unit = "BLS12-381 miller_loop(G1Affine_i, one G2Prepared) + final_exponentiation per second " \
+                           "at batch 2^16", "pairings/s"
+            config = {"workload": "bls12_381 final_exponentiation(miller_loop([(P_i, Q)])) batch against ONE "
+                                  "prepared Q (lines staged once per call, no G2 arithmetic per pair)",
+                      "batch_per_gpu": n, "global_batch": n_global,
+                      "parallelism": "shard%d+rccl_gather" % ws if dist_on else "single",
+                      "kernel_ms": {"miller_loop_shared": round(ml, 3), "final_exponentiation": round(fe, 3)}}
         elif args.workload == "wnaf":
             tot_ms, norm_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
             table_ms, mul_ms = comb_parts_ms()
@@ -809,7 +884,7 @@ def main():
             metric, unit = "Fq::mul_assign per second at batch 2^20", "muls/s"
             config = {"workload": "2^20 Fq Montgomery multiplications (%s 6x u64)" % args.layout.upper(), "batch_per_gpu": n,
                       "global_batch": n_global}
-        if dist_on and args.workload not in ("pairing", "prepared"):
+        if dist_on and args.workload not in ("pairing", "prepared", "prepared_shared"):
             config["parallelism"] = ("shard%d+partial_sums_to_root" if args.workload == "msm" else
                                      "replicas%d" if args.workload == "verify" else "shard%d+rccl_gather") % ws
         achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9
@@ -829,7 +904,8 @@ def main():
             roof["copy_GBs"] = round(copy_gbs, 1)
             roof["frac_of_copy"] = achieved / copy_gbs
         work_path = os.path.join(ROOT, "pairing_amd", "lib", "pa_gen_work.json")
-        if args.workload == "pairing" or (args.workload == "prepared" and dom_name == "final_exponentiation"):
+        if args.workload == "pairing" or (args.workload in ("prepared", "prepared_shared") and
+                                          dom_name in ("final_exponentiation", "miller_loop_shared")):
             _check_work_json(work_path)
             # the pairing kernels are VALU-issue bound (multiply-accumulate
             # chains), not HBM bound: report that roofline, with the HBM view
@@ -840,7 +916,8 @@ def main():
             # in-kernel binary-GCD inversions, compressed squarings).  The
             # binary GCD's instructions are counted, its 64-bit approximation
             # steps are not limb MACs.
-            wk = work["miller_loop"] if dom_name != "final_exponentiation" else work["final_exp"]
+            wk = work["final_exp"] if dom_name == "final_exponentiation" else \
+                work["miller_loop_shared"] if dom_name == "miller_loop_shared" else work["miller_loop"]
             macs = wk["limb_macs"]
             mac_rate = macs * n / (dom_ms * 1e-3) / 1e12
             roof = {"kernel": dom_name, "bound": "valu", "achieved": round(mac_rate, 3),
@@ -911,6 +988,8 @@ def main():
                 cpu = cpu_baseline_pairing(p_np, q_np, args.cpu_seconds)
             elif args.workload == "prepared":
                 cpu = cpu_baseline_prepared(p_np, q_np, args.cpu_seconds)
+            elif args.workload == "prepared_shared":
+                cpu = cpu_baseline_prepared_shared(p_np, prep1_np, args.cpu_seconds)
             elif args.workload == "wnaf":
                 cpu = cpu_baseline_wnaf(base_np, s_np, args.cpu_seconds)
             elif args.workload == "decode":
@@ -939,7 +1018,7 @@ def main():
                 "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": args.workload != "verify",
                 "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None,
                 "dtype": "u32 (14 x 28-bit lazy Montgomery limbs)"
-                if args.workload in ("pairing", "prepared", "verify", "fq_mul")
+                if args.workload in ("pairing", "prepared", "prepared_shared", "verify", "fq_mul")
                 else "u32 (256-bit Montgomery, 8 x u32 limbs)" if args.workload == "fr_mul"
                 else "u32 (14 x 28-bit lazy Montgomery limbs; 12 x u32 normalize)" if args.workload == "wnaf"
                 else "u32 (384-bit Montgomery, 12 x u32 limbs)",

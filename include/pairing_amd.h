@@ -145,6 +145,13 @@ int pa_g2_prepare_batch(const pa_g2_affine *q, pa_g2_prepared *out, size_t n);
 /* ---- Engine (src/lib.rs:34-110, src/bls12_381/mod.rs:30-161) ---- */
 /* n independent single-pair loops: out[i] = Bls12::miller_loop([(p[i], q[i])]) (mod.rs:40-102) */
 int pa_miller_loop_batch(const pa_g1_affine *p, const pa_g2_prepared *q, pa_fq12 *out, size_t n);
+/* One G2Prepared shared by every pair -- Engine::miller_loop takes &G2Prepared
+ * references (lib.rs:88-96, Prepared: Clone lib.rs:192), so a caller may pass the
+ * same prepared Q for each P (a verifying key's prepared gamma / delta):
+ * out[i] = Bls12::miller_loop([(p[i], q)]) (mod.rs:40-102) for i < n, where `q`
+ * is ONE record.  Its lines are staged once per call; no G2 arithmetic per pair.
+ * Same bits as pa_miller_loop_batch with q repeated n times. */
+int pa_miller_loop_shared_prepared(const pa_g1_affine *p, size_t n, const pa_g2_prepared *q, pa_fq12 *out);
 /* Engine::miller_loop over n pairs: the product semantics of mod.rs:40-102 */
 int pa_multi_miller_loop(const pa_g1_affine *p, const pa_g2_prepared *q, size_t n, pa_fq12 *out);
 /* Engine::final_exponentiation, mod.rs:104-160; ok[i] = 0 iff in[i] == 0 */
@@ -381,6 +388,9 @@ int pa_multi_pairing_device(const pa_g1_affine *p, const pa_g2_affine *q, size_t
 int pa_g2_prepare_batch_device(const pa_g2_affine *q, pa_g2_prepared *out, size_t n, void *stream);
 int pa_miller_loop_batch_device(const pa_g1_affine *p, const pa_g2_prepared *q, pa_fq12 *out, size_t n,
                                 void *stream);
+/* pa_miller_loop_shared_prepared on device records (p: n records, q: one) */
+int pa_miller_loop_shared_prepared_device(const pa_g1_affine *p, size_t n, const pa_g2_prepared *q,
+                                          pa_fq12 *out, void *stream);
 /* e(p[i], q[i]); `scratch` must hold n pa_fq12 (the Miller-loop values) */
 int pa_pairing_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, pa_fq12 *scratch,
                             size_t n, void *stream);

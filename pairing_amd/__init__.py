@@ -26,7 +26,7 @@ __all__ = [
     "fq12_frobenius_map", "fq12_cyclotomic_square", "fq12_mul_by_014",
     "fq2_inverse", "fq2_frobenius_map", "fq6_square", "fq6_inverse", "fq6_frobenius_map", "fq_pow", "fq12_pow",
     "g1_batch_normalization", "g1_wnaf_fixed_base",
-    "g2_prepare", "miller_loop_batch", "multi_miller_loop", "final_exponentiation", "pairing",
+    "g2_prepare", "miller_loop_batch", "miller_loop_shared_prepared", "multi_miller_loop", "final_exponentiation", "pairing",
     "multi_miller_loop_affine", "multi_pairing", "pairing_multi_gpu",
     "fq_sqrt", "fq2_sqrt", "g1_decode", "g2_decode", "g1_encode", "g2_encode", "DECODE_STATUS",
     "fr_mul", "fr_square", "fr_add", "fr_sub", "fr_double", "fr_negate", "fr_inverse",
@@ -202,6 +202,19 @@ def miller_loop_batch(p, q_prepared):
         raise ValueError("p and q_prepared lengths differ")
     out = np.empty((p.shape[0], W_FQ12), np.uint64)
     call("pa_miller_loop_batch", ptr(p), ptr(q), ptr(out), p.shape[0])
+    return out
+
+
+def miller_loop_shared_prepared(p, q_prepared):
+    """out[i] = Bls12::miller_loop([(p[i], q)]) for ONE prepared q shared by every
+    p[i] (lib.rs:88-96 called with the same &G2Prepared; mod.rs:40-102): the
+    verifier's fixed-key shape.  q_prepared: one record, shape (W_G2P,) or (1, W_G2P)."""
+    p = as_rows(p, W_G1A, "p")
+    q = as_rows(q_prepared, W_G2P, "q_prepared")
+    if q.shape[0] != 1:
+        raise ValueError("q_prepared must be ONE G2Prepared record")
+    out = np.empty((p.shape[0], W_FQ12), np.uint64)
+    call("pa_miller_loop_shared_prepared", ptr(p), p.shape[0], ptr(q), ptr(out))
     return out
 
 

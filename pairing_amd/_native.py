@@ -91,6 +91,7 @@ _SIGS = {
     "pa_fq12_mul_by_014_batch": [_P, _P, _P, _P, _P, _N],
     "pa_g2_prepare_batch": [_P, _P, _N],
     "pa_miller_loop_batch": [_P, _P, _P, _N],
+    "pa_miller_loop_shared_prepared": [_P, _N, _P, _P],
     "pa_multi_miller_loop": [_P, _P, _N, _P],
     "pa_final_exponentiation_batch": [_P, _P, _P, _N],
     "pa_pairing_batch": [_P, _P, _P, _N],
@@ -109,6 +110,7 @@ _SIGS = {
     "pa_miller_loop_fused_batch_device": [_P, _P, _P, _N, _P],
     "pa_g2_prepare_batch_device": [_P, _P, _N, _P],
     "pa_miller_loop_batch_device": [_P, _P, _P, _N, _P],
+    "pa_miller_loop_shared_prepared_device": [_P, _N, _P, _P, _P],
     "pa_final_exponentiation_batch_device": [_P, _P, _P, _N, _P],
     "pa_pairing_batch_device": [_P, _P, _P, _P, _N, _P],
     "pa_g1_decode_batch": [_P, _N, ctypes.c_int, ctypes.c_int, _P, _P],

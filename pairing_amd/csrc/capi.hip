@@ -446,6 +446,21 @@ int pa_miller_loop_batch(const pa_g1_affine* p, const pa_g2_prepared* q, pa_fq12
     return download(out, dout, 576 * n);
 }
 
+int pa_miller_loop_shared_prepared(const pa_g1_affine* p, size_t n, const pa_g2_prepared* q, pa_fq12* out) {
+    if (n == 0) return PA_OK;
+    if (!p || !q || !out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    DevBuf dp, dq, dout;
+    int rc;
+    if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_prepared))))
+        return rc;
+    PA_TRY(dout.alloc(576 * n), "device scratch");
+    PA_TRY(pa::launch_miller_loop_shared_gen(dp.as<uint64_t>(), dq.as<uint64_t>(), dout.as<uint64_t>(), n,
+                                             call_stream()),
+           "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
+    return download(out, dout, 576 * n);
+}
+
 int pa_multi_miller_loop(const pa_g1_affine* p, const pa_g2_prepared* q, size_t n, pa_fq12* out) {
     if (!out) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     if (n == 0) {
@@ -957,6 +972,14 @@ int pa_miller_loop_batch_device(const pa_g1_affine* p, const pa_g2_prepared* q, 
     if (n && (!p || !q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     PA_TRY(pa::launch_miller_loop_prepared((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n,
                                            (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
+int pa_miller_loop_shared_prepared_device(const pa_g1_affine* p, size_t n, const pa_g2_prepared* q, pa_fq12* out,
+                                          void* stream) {
+    if (n && (!p || !q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_miller_loop_shared_gen((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n,
+                                             (hipStream_t)stream),
            "kernel launch");
     return PA_OK;
 }

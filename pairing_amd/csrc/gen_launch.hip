@@ -28,7 +28,7 @@
 namespace pa {
 namespace {
 
-constexpr int kKernels = 4;
+constexpr int kKernels = 5;
 constexpr size_t kSlotBytes = 3584;  // one 14-limb spill slot for a 64-lane wave
 
 struct Workspace {
@@ -49,15 +49,18 @@ std::mutex g_mu;
 GenDevice g_dev[64];
 thread_local std::string g_detail;   // the code object that failed to load, for pa_last_error
 
-// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing
+// 0, 1: one lane per pairing; 2, 3: a lane pair per pairing; 4: the Miller
+// loop of a batch against one shared G2Prepared (a line table in place of a1)
 const char* const kFile[kKernels] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco",
-                                     "pa_gen_miller_loop2.hsaco", "pa_gen_final_exp2.hsaco"};
+                                     "pa_gen_miller_loop2.hsaco", "pa_gen_final_exp2.hsaco",
+                                     "pa_gen_miller_loop_shared.hsaco"};
 const char* const kName[kKernels] = {"pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2",
-                                     "pa_gen_final_exp2"};
+                                     "pa_gen_final_exp2", "pa_gen_miller_loop_shared"};
 const size_t kWaveBytes[kKernels] = {PA_GEN_MILLER_LOOP_MEM_SLOTS * kSlotBytes, PA_GEN_FINAL_EXP_MEM_SLOTS * kSlotBytes,
                                      PA_GEN_MILLER_LOOP2_MEM_SLOTS * kSlotBytes,
-                                     PA_GEN_FINAL_EXP2_MEM_SLOTS * kSlotBytes};
-const int kLanes[kKernels] = {1, 1, 2, 2};
+                                     PA_GEN_FINAL_EXP2_MEM_SLOTS * kSlotBytes,
+                                     PA_GEN_MILLER_LOOP_SHARED_MEM_SLOTS * kSlotBytes};
+const int kLanes[kKernels] = {1, 1, 2, 2, 1};
 
 // PA_GEN_DIR (A/B experiments with alternative generated code objects) overrides
 // the directory of libpairing_amd.so; PA_GEN_WS_SLOTS raises the workspace size
@@ -190,6 +193,8 @@ hipError_t acquire(GenDevice& d, size_t need, hipStream_t stream, Workspace** ou
     return hipSuccess;
 }
 
+// which == 4 (shared G2Prepared): a1 is the prepared record; its line table
+// is built in the workspace behind the waves' spill slices first
 hipError_t launch(int which, const void* a0, const void* a1, const void* a2, size_t n, hipStream_t stream) {
     g_detail.clear();
     if (n == 0) return hipSuccess;
@@ -205,8 +210,16 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
     }
     const size_t blocks = (n * kLanes[which] + 63) / 64;
     if (blocks > 0xffffffffull) return hipErrorInvalidValue;
+    const size_t table_at = (blocks * wave_bytes() + 255) & ~(size_t)255;
     Workspace* ws = nullptr;
-    if ((e = acquire(d, blocks * wave_bytes(), stream, &ws)) != hipSuccess) return e;
+    if ((e = acquire(d, which == 4 ? table_at + kSharedTableBytes : blocks * wave_bytes(), stream, &ws)) !=
+        hipSuccess)
+        return e;
+    if (which == 4) {
+        uint32_t* table = reinterpret_cast<uint32_t*>(static_cast<char*>(ws->p) + table_at);
+        if ((e = launch_shared_line_table(static_cast<const uint64_t*>(a1), table, stream)) != hipSuccess) return e;
+        a1 = table;
+    }
     struct {
         const void* a0;
         const void* a1;
@@ -239,6 +252,10 @@ hipError_t launch_miller_loop_gen(int lanes, const uint64_t* p_aff, const uint64
 hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n,
                                 hipStream_t stream) {
     return launch(lanes == 2 ? 3 : 1, in, out, ok, n, stream);
+}
+hipError_t launch_miller_loop_shared_gen(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out, size_t n,
+                                         hipStream_t stream) {
+    return launch(4, p_aff, prepared, out, n, stream);
 }
 
 }  // namespace pa

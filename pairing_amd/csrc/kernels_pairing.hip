@@ -67,6 +67,34 @@ __global__ void __launch_bounds__(64) k_miller_loop_prepared(const uint64_t* __r
     store12(out + 72 * i, f);
 }
 
+// ---- one G2Prepared shared by a batch of G1 points (lib.rs:88-96: the
+// caller passes the same &G2Prepared for every pair -- a verifying key's
+// prepared gamma / delta) ----
+//
+// k_shared_line_table converts the record's 68 lines ONCE per call into the
+// line table of the generated kernel pa_gen_miller_loop_shared
+// (tools/pgen/kernels.py miller_loop_shared_prog, kcfg.MillerLoopSharedCfg):
+// u32 word 0 = the prepared infinity flag, then from byte kSharedTableLines
+// per line six 14-limb values
+//   c0.c0, c0.c1, c1.c0, c1.c1 as fl_split (raw 28-bit limbs of the ABI
+//   integer: the ABI -> lazy conversion rides on the products by P's
+//   coordinates, as in ell_fl), c2.c0, c2.c1 as fl_from_abi.
+// Every lane of the Miller loop then reads the same table words, so per
+// pairing only P (104 B) crosses HBM and no G2 arithmetic runs.
+__global__ void __launch_bounds__(64) k_shared_line_table(const uint64_t* __restrict__ prepared,
+                                                          uint32_t* __restrict__ table) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) table[0] = (prepared[kNumCoeffs * 36] & 0xff) != 0 ? 1u : 0u;
+    if (t >= kNumCoeffs * 6) return;
+    const int line = t / 6, j = t % 6;
+    Fq w;
+    fq_load(w, prepared + 36 * line + 6 * j);
+    const F<1> v = j < 4 ? fl_split(w) : fl_from_abi(w);
+    uint32_t* dst = table + kSharedTableLines / 4 + kSharedLineWords * line + 14 * j;
+#pragma unroll
+    for (int l = 0; l < 14; l++) dst[l] = v.w[l];
+}
+
 // one tree level: work[i] *= work[i + half] for i < cnt - half
 __global__ void __launch_bounds__(64) k_fq12_product_level(uint64_t* __restrict__ work, size_t cnt, size_t half) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -86,6 +114,11 @@ hipError_t launch_miller_loop_prepared(const uint64_t* p_aff, const uint64_t* pr
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_miller_loop_prepared, dim3(blocks_for(n, 64)), dim3(64), 0, stream, p_aff, prepared,
                        out, n);
+    return hipGetLastError();
+}
+hipError_t launch_shared_line_table(const uint64_t* prepared, uint32_t* table, hipStream_t stream) {
+    hipLaunchKernelGGL(k_shared_line_table, dim3(blocks_for(kNumCoeffs * 6, 64)), dim3(64), 0, stream, prepared,
+                       table);
     return hipGetLastError();
 }
 hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStream_t stream) {

@@ -67,6 +67,14 @@ hipError_t launch_fq_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* o
 hipError_t launch_g2_prepare(const uint64_t* q_aff, uint64_t* prepared, size_t n, hipStream_t stream);
 hipError_t launch_miller_loop_prepared(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out,
                                        size_t n, hipStream_t stream);
+// one G2Prepared (`prepared`, one record) for every G1 point of the batch:
+// the line table (kernels_pairing.hip) and the generated Miller loop over it
+constexpr int kSharedLineWords = 6 * 14;
+constexpr int kSharedTableLines = 64;   // byte offset of line 0 (word 0: infinity flag)
+constexpr size_t kSharedTableBytes = kSharedTableLines + 68 * kSharedLineWords * 4;
+hipError_t launch_shared_line_table(const uint64_t* prepared, uint32_t* table, hipStream_t stream);
+hipError_t launch_miller_loop_shared_gen(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out, size_t n,
+                                         hipStream_t stream);
 // non-empty after a generated code object failed to load (names the file)
 const char* gen_error_detail();
 // The generated Miller-loop / final-exponentiation kernels (tools/pgen,

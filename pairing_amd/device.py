@@ -104,6 +104,16 @@ def miller_loop_prepared(p, qp, out, stream=None):
     call("pa_miller_loop_batch_device", *args, n, _stream_ptr(stream))
 
 
+def miller_loop_shared_prepared(p, qp, out, stream=None):
+    """out[i] = miller_loop([(p[i], qp[0])]): one G2Prepared record shared by the
+    batch, its lines staged once (lib.rs:88-96, mod.rs:40-102)."""
+    n = p.shape[0]
+    args = (_dptr(p, W_G1A, "p"), _dptr(qp, W_G2P, "qp"), _dptr(out, W_FQ12, "out"))
+    _rows(qp, 1, "qp")
+    _rows(out, n, "out")
+    call("pa_miller_loop_shared_prepared_device", args[0], n, args[1], args[2], _stream_ptr(stream))
+
+
 def final_exponentiation(f, out, ok=None, stream=None):
     n = f.shape[0]
     args = (_dptr(f, W_FQ12, "f"), _dptr(out, W_FQ12, "out"), _flags(ok, n))

@@ -90,6 +90,27 @@ for step in "$@"; do
                   run bench_wnaf 300 python bench.py --workload wnaf --steps 5 --warmup 1 &&
                   run bench_fq 300 python bench.py --workload fq_mul --steps 20 --warmup 3 &&
                   run bench_fr 300 python bench.py --workload fr_mul --steps 20 --warmup 3 ;;
+        sharedtests) run pytest_shared 600 python -u -m pytest tests/test_shared_prepared.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+        sharedbench) run bench_shared 300 python bench.py --workload prepared_shared --steps 10 --warmup 2 --no-cpu-baseline ;;
+        sharedbenchcpu) run bench_shared_cpu 400 python bench.py --workload prepared_shared --steps 10 --warmup 2 ;;
+        profshared) run prof_shared 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_shared -o run -- python bench.py --workload prepared_shared --steps 5 --warmup 1 --no-cpu-baseline ;;
+        pmcpair)  # r05: counters of lane-pair vs one-lane kernels and the leaf probe
+            P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+            P2="SQ_ACTIVE_INST_VALU2 SQ_INST_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC"
+            P3="MeanOccupancyPerCU SQ_IFETCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32"
+            P4="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE InstrFetchLatency"
+            for cfg in "1 65536" "1 32768" "3 65536" "3 32768"; do
+                set -- $cfg
+                run pair_time_v$1_n$2 120 python tools/pair_pmc.py $2 $1 2 || exit 1
+                for k in 1 2 3 4; do
+                    eval "ctrs=\$P$k"
+                    run pmcpair_v$1_n$2_p$k 120 rocprofv3 --pmc $ctrs --output-format csv -d gpurun_out/pmcpair/v$1_n$2_p$k -o run -- python tools/pair_pmc.py $2 $1 1 || exit 1
+                done
+            done
+            for k in 1 2 3 4; do
+                eval "ctrs=\$P$k"
+                run pmcprobe_p$k 120 rocprofv3 --pmc $ctrs --output-format csv -d gpurun_out/pmcpair/probe_p$k -o run -- ./tools/icache_probe || exit 1
+            done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

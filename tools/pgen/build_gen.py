@@ -92,6 +92,8 @@ PROGRAMS = {
     "fen": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="norm"), kcfg.FinalExpCfg, "pa_gen_fe_norm"),
     "fei": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="inv"), kcfg.FinalExpCfg, "pa_gen_fe_inv"),
     "ml2": _mk(lambda: kernels.miller_loop_prog(lanes=2), kcfg.MillerLoopCfg2, "pa_gen_miller_loop2"),
+    # one G2Prepared shared by the whole batch: the line table in place of G2 arithmetic
+    "mls": _mk(kernels.miller_loop_shared_prog, kcfg.MillerLoopSharedCfg, "pa_gen_miller_loop_shared"),
     # test-only kernels (tools/pgen/unit_progs.py, tests/test_gen_units.py)
     "tdec": _mk(lambda: __import__("unit_progs").dec_prog(), kcfg.FinalExpCfg, "pa_gen_tdec"),
     "tunit": _mk(lambda: __import__("unit_progs").unit_prog(), kcfg.FinalExpCfg, "pa_gen_tunit"),
@@ -102,6 +104,7 @@ PROGRAMS = {
     "fez": _mk(lambda: kernels.final_exp_prog(lazy=True), kcfg.FinalExpCfg, "pa_gen_final_exp_lazy"),
 }
 FILES = {"small": "pa_gen_small.hsaco", "cyc": "pa_gen_cyc.hsaco", "ml": "pa_gen_miller_loop.hsaco", "fe": "pa_gen_final_exp.hsaco",
+         "mls": "pa_gen_miller_loop_shared.hsaco",
          "fen": "pa_gen_fe_norm.hsaco", "fei": "pa_gen_fe_inv.hsaco",
          "ml2": "pa_gen_miller_loop2.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
          "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco",
@@ -116,7 +119,7 @@ def build(which, outdir):
     import emit
     asm = render.kernel_asm(kname, code, em.lds_bytes, lanes=prog.lanes,
                             nvgpr=256 if prog.lanes == 1 else min(256, -(-(emit.VSLOT0 + 14 * em.NV) // 4) * 4),
-                            mem_slots=nmem)
+                            mem_slots=nmem, nsgpr=getattr(cfg, "nsgpr", 96))
     out = os.path.join(outdir, FILES[which])
     os.makedirs(os.path.dirname(out), exist_ok=True)
     render.assemble(asm, out, os.path.join(ROOT, "build", "pgen"))
@@ -149,12 +152,15 @@ def write_work_json(outdir):
     rng = random.Random(1)
     out = {}
     for key, name, nin in (("ml", "miller_loop", 6), ("fe", "final_exp", 12), ("fen", "fe_norm", 12),
-                           ("fei", "fe_inv", 13)):
-        if key in ("fen", "fei") and not PROGRAMS[key].cache:
+                           ("fei", "fe_inv", 13), ("mls", "miller_loop_shared", 2)):
+        if key in ("fen", "fei", "mls") and not PROGRAMS[key].cache:
             continue
         prog = PROGRAMS[key]()[0]
         st = dsl.Stats()
-        dsl.evaluate(prog, {k: rng.randrange(dsl.Q) for k in range(nin)}, st)
+        ins = {k: rng.randrange(dsl.Q) for k in range(nin)}
+        if key == "mls":
+            ins["lines"] = kernels.shared_table_lines([[rng.randrange(dsl.Q) for _ in range(6)] for _ in range(68)])
+        dsl.evaluate(prog, ins, st)
         em = PROGRAMS[key].cache["r"][5]
         # instructions one lane executes (exact: the loop trip counts and branch
         # masks are static, the emitter weights every instruction by them)
@@ -172,16 +178,17 @@ def main():
         del args[i:i + 2]
     os.makedirs(outdir, exist_ok=True)
     meta = {}
-    for w in args or ["ml", "fe", "ml2", "fe2"]:
+    for w in args or ["ml", "fe", "ml2", "fe2", "mls"]:
         build(w, outdir)
         meta[w] = PROGRAMS[w].cache["r"][3]
     if "ml" in meta and "fe" in meta:
         write_work_json(outdir)
-    if all(k in meta for k in ("ml", "fe", "ml2", "fe2")):
+    if all(k in meta for k in ("ml", "fe", "ml2", "fe2", "mls")):
         hdr = os.path.join(ROOT, "pairing_amd", "csrc", "pa_gen_meta.h")
         with open(hdr, "w") as f:
             f.write("// GENERATED by tools/pgen/build_gen.py -- spill workspace per wave (M slots)\n#pragma once\n")
-            for k, name in (("ml", "MILLER_LOOP"), ("fe", "FINAL_EXP"), ("ml2", "MILLER_LOOP2"), ("fe2", "FINAL_EXP2")):
+            for k, name in (("ml", "MILLER_LOOP"), ("fe", "FINAL_EXP"), ("ml2", "MILLER_LOOP2"), ("fe2", "FINAL_EXP2"),
+                            ("mls", "MILLER_LOOP_SHARED")):
                 f.write("#define PA_GEN_%s_MEM_SLOTS %d\n" % (name, meta[k]))
 
 

@@ -360,6 +360,23 @@ class Prog:
         raw = self._op("load_raw", [], 1, imm=imm)
         return self.mul(raw, self.const_limbs(gen_fl.limbs(pow(2, 400, Q))))
 
+    def load_scaled(self, slot, c):
+        """input Fq `slot` (raw ABI limbs, value x R) times the constant integer c
+        in one product: x R c / R' (load() is c = 2^400, i.e. x R')"""
+        raw = self._op("load_raw", [], 1, imm=slot)
+        return self.mul(raw, self.const_limbs(gen_fl.limbs(c % Q)))
+
+    # ---- a line table shared by every lane (one G2Prepared for the batch) ----
+    def tload(self, j):
+        """value j (0..5) of the current line of the kernel's line table: 14
+        limbs read from a wave-uniform address (kcfg.MillerLoopSharedCfg), given
+        as exact limbs (u = vb = 1, see kernels.miller_loop_shared_prog)"""
+        return self._op("tload", [], 1, imm=j)
+
+    def tnext(self):
+        """advance the line table to the next line"""
+        self.cur.items.append(Op("tnext", None, [], imm=None))
+
     def store(self, slot, v, slot1=None):
         """canonical output Fq `slot` (R = 2^384) of this lane (two-lane
         programs: lane 1 writes `slot1`)"""
@@ -731,6 +748,11 @@ def evaluate(prog, inputs, stats=None, trace=None):
         elif k == "load_raw":
             slots = op.imm if isinstance(op.imm, tuple) else (op.imm,) * L
             r = [tuple(gen_fl.limbs(inputs[slots[ln]])) for ln in range(L)]
+        elif k == "tload":
+            r = [tuple(inputs["lines"][counters.get("line", 0)][op.imm])] * L
+        elif k == "tnext":
+            counters["line"] = counters.get("line", 0) + 1
+            return
         elif k == "store_raw":
             slots = op.imm if isinstance(op.imm, tuple) else (op.imm,) * L
             for ln in range(L):

@@ -59,6 +59,9 @@ S_CNT = 20          # s20.. loop counters by depth
 S_MASK = 24         # s[24+2d : 25+2d] branch masks by depth
 S_JMP = 30          # s[30:31] long-branch temporary
 S_VALID = 36        # s[36:37] lane mask: output valid (not infinity / f != 0)
+S_LINE = 96         # s[96:97] current line of a shared line table (MillerLoopSharedCfg)
+ZERO = 17           # v17 = 0 in kernels with a line table (the wave-uniform load offset)
+LINE_BYTES = 6 * NL * 4   # one line: six 14-limb values, 336 B
 
 
 class AllocError(Exception):
@@ -1196,6 +1199,15 @@ class Emitter:
             self.emit_binv(base[0], d, scratch)
         elif k == "load_raw":
             self.cfg.emit_load(self, op.imm, d)
+        elif k == "tload":
+            # every lane reads the same 56 bytes (one cache line request per
+            # load); the value is used after the line's other loads are issued,
+            # so the wait is a counted one at its first use (self.pending)
+            for j in range(7):
+                self.i("global_load_dwordx2_s", d + 2 * j, ZERO, S(S_LINE), NL * 4 * op.imm + 8 * j)
+        elif k == "tnext":
+            self.i("s_add_u32", S(S_LINE), S(S_LINE), K(LINE_BYTES))
+            self.i("s_addc_u32", S(S_LINE + 1), S(S_LINE + 1), K(0))
         elif k == "store_raw":
             self.cfg.emit_store(self, op.imm, base[0])
         else:
@@ -1215,14 +1227,16 @@ class Emitter:
             dvs = self.states[dst.id]
             self.vslot[kk] = dvs
             dvs.locs = {("V", kk)}
-            if self.debug:
+            if k == "tload":
+                self.pending[kk] = ("M", self.vm_issued)
+            if self.debug and k != "tload":   # a table load lands at its counted wait
                 self.i("mark", dst.id, self.vbase(kk))
             if not dvs.uses:
                 self.kill(dvs)
 
     # ---------------- prefetch ----------------
     COST = {"sop": None, "sqr": 460, "red": 62, "norm": 39, "add": 14, "add3": 14, "shladd": 14, "shl": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
-            "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14,
+            "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14, "tload": 7, "tnext": 2,
             "selz": 80, "binv": 33000}
     # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
     AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}

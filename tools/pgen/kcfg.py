@@ -8,8 +8,8 @@ Kernel arguments (5 x 8 bytes, all kernels):
 """
 import gen_fl
 from dsl import Q
-from emit import (A, ACC, ADDR, GID, K, LOFF, ORACC, S, S_ARG, S_EXEC, S_KARG, S_ODD, S_TMP, S_VALID, S_WG,
-                  S_WS, SKQ, SQ, SQINV, NL, MASK, QL, QINV28, KQ)
+from emit import (A, ACC, ADDR, GID, K, LOFF, ORACC, S, S_ARG, S_EXEC, S_KARG, S_LINE, S_ODD, S_TMP, S_VALID,
+                  S_WG, S_WS, SKQ, SQ, SQINV, NL, MASK, QL, QINV28, KQ, ZERO)
 
 ONE_ABI = (1 << 384) % Q          # Montgomery one in the ABI (R = 2^384)
 S_STRIDE = 32
@@ -202,6 +202,35 @@ class FinalExpCfg(KernelCfg):
         self.lane_addr(code, 2, 1)
         code.append(("global_store_byte", ADDR, 0, 0))
         code.append(("label", skip))
+
+
+class MillerLoopSharedCfg(MillerLoopCfg):
+    """miller_loop of every P_i against ONE G2Prepared (kernels.
+    miller_loop_shared_prog).  Arguments: p_aff (G1Affine records), table,
+    out (Fq12), n, workspace.  The table (written by k_shared_line_table,
+    kernels_pairing.hip) is u32 words: word 0 = Q's infinity flag, then from
+    byte TABLE_LINES the 68 lines of six 14-limb values, read at wave-uniform
+    addresses (emit.S_LINE, offset register v17 = 0)."""
+    name = "pa_gen_miller_loop_shared"
+    records = {0: (0, 104, 0), 1: (0, 104, 48)}
+    TABLE_LINES = 64
+    nsgpr = 98          # s[96:97]: the line pointer
+
+    def prologue_masks(self, em, code):
+        i = code.append
+        # valid = P is not the point at infinity and Q is not (the table's flag)
+        i(("v_mov_b32", ZERO, K(0)))
+        self.lane_addr(code, 0, 104)
+        i(("global_load_dword", 0, ADDR, 96))
+        i(("global_load_dwordx2_s", 2, ZERO, S(S_ARG + 2), 0))
+        i(("s_waitcnt_vm0",))
+        i(("v_or_b32", 0, 0, 2))
+        i(("v_and_b32", 0, K(0xff), 0))
+        i(("v_cmp_eq_u32", K(0), 0))
+        i(("s_nop", 1))
+        i(("s_mov_b64", S(S_VALID), S(106)))
+        i(("s_add_u32", S(S_LINE), S(S_ARG + 2), K(self.TABLE_LINES)))
+        i(("s_addc_u32", S(S_LINE + 1), S(S_ARG + 3), K(0)))
 
 
 class MillerLoopCfg2(MillerLoopCfg):

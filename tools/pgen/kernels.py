@@ -128,6 +128,75 @@ def miller_loop_prog(homes=None, lanes=1, lazy=False):
     return p
 
 
+def miller_loop_shared_prog():
+    """Bls12::miller_loop([(P_i, Q)]) for a batch of P_i and ONE prepared Q
+    (lib.rs:88-96 with the same &G2Prepared in every pair; mod.rs:40-102).
+    No G2 arithmetic: the line coefficients come from the kernel's line table
+    (kcfg.MillerLoopSharedCfg), six values per line as written by
+    k_shared_line_table (kernels_pairing.hip):
+      0, 1  c0 = (c0.c0, c0.c1)  raw limbs of the ABI integer (x R, R = 2^384)
+      2, 3  c1                   likewise
+      4, 5  c2                   lazy form (x R', R' = 2^392)
+    and P's coordinates are loaded scaled by 2^408 (x R' (R'/R)), so that
+    mul(raw c, kx) = c P.x R' -- the ABI -> lazy conversion of c0 and c1 rides
+    on the products ell needs anyway (mod.rs:57-69; pairing_fl.h ell_fl).
+      inputs 0 px, 1 py (this lane's G1Affine); outputs 0..11 (Fq12)"""
+    p = Prog("miller_loop_shared", 1, use_norm=_norm(1))
+    T = Tower(p)
+    V = _Vars(p, 1)
+    for n in ("kx", "ky"):
+        p.var(n, 1, "A")
+    p.set("kx", p.load_scaled(0, 1 << 408))
+    p.set("ky", p.load_scaled(1, 1 << 408))
+    V.declare12("f", os.environ.get("PGEN_MLS_F_HOME", "A"))
+    zero = T.const2((0, 0))
+    V.set12("f", ((T.one2(), zero, zero), (zero, zero, zero)))
+
+    def line():
+        c = [p.tload(j) for j in range(6)]
+        p.tnext()
+        kx, ky = p.get("kx"), p.get("ky")
+        a = (p.mul(c[0], ky), p.mul(c[1], ky))     # c0 * P.y
+        b = (p.mul(c[2], kx), p.mul(c[3], kx))     # c1 * P.x
+        V.set12("f", T.mul_by_014(V.get12("f"), (c[4], c[5]), b, a))
+
+    with p.loop(62) as L:
+        line()
+        with p.if_bit(ML_MASK, L):
+            line()
+        V.set12("f", T.sqr12(V.get12("f")))
+    line()
+    V.store12(T.conj12(V.get12("f")))
+    return p
+
+
+def shared_table_lines(coeffs):
+    """the line table values of miller_loop_shared_prog for 68 lines of six
+    ABI integers (c0.c0, c0.c1, c1.c0, c1.c1, c2.c0, c2.c1; x R, canonical):
+    raw limbs for c0 and c1, the lazy form mul(raw, 2^400) for c2 -- exactly
+    the limbs k_shared_line_table (kernels_pairing.hip) writes"""
+    import gen_fl
+    from dsl import mont_sop, Q
+    to = tuple(gen_fl.limbs(pow(2, 400, Q)))
+    out = []
+    for line in coeffs:
+        raw = [tuple(gen_fl.limbs(x)) for x in line]
+        out.append(raw[:4] + [mont_sop([(r, to)]) for r in raw[4:]])
+    return out
+
+
+def shared_table_u64(lines, infinity):
+    """the table as u64 words (kcfg.MillerLoopSharedCfg layout): u32 word 0 the
+    infinity flag, lines from byte 64, 14 u32 limbs per value"""
+    words32 = [1 if infinity else 0] + [0] * 15
+    for line in lines:
+        for v in line:
+            words32 += list(v)
+    if len(words32) % 2:
+        words32.append(0)
+    return [words32[2 * k] | (words32[2 * k + 1] << 32) for k in range(len(words32) // 2)]
+
+
 class _Vars:
     """Fq2 / Fq12 state variables: a one-lane Fq2 is two variables (c0, c1),
     a distributed Fq2 one variable per lane (named <n>0; <n>1 unused)."""

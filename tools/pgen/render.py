@@ -136,7 +136,7 @@ class Renderer:
         return out
 
 
-def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256, mem_slots=None):
+def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256, mem_slots=None, nsgpr=96):
     """mem_slots: the HBM spill slots per wave the code uses, exported as the
     global `<name>_mem_slots` so the loader (gen_launch.hip) can refuse a code
     object that needs a larger workspace than the library allocates"""
@@ -167,7 +167,7 @@ def kernel_asm(name, code, lds_bytes, nargs=5, lanes=1, nvgpr=256, mem_slots=Non
 \t\t.amdhsa_system_sgpr_workgroup_id_x 1
 \t\t.amdhsa_system_vgpr_workitem_id 0
 \t\t.amdhsa_next_free_vgpr {nfree}
-\t\t.amdhsa_next_free_sgpr 96
+\t\t.amdhsa_next_free_sgpr {nsgpr}
 \t\t.amdhsa_accum_offset {aoff}
 \t\t.amdhsa_reserve_vcc 1
 \t\t.amdhsa_float_denorm_mode_32 3
@@ -185,7 +185,7 @@ amdhsa.kernels:
     .group_segment_fixed_size: {lds}
     .private_segment_fixed_size: 0
     .wavefront_size: 64
-    .sgpr_count: 102
+    .sgpr_count: {sgpr_count}
     .vgpr_count: {nfree}
     .agpr_count: {nagpr}
     .max_flat_workgroup_size: 64
@@ -197,7 +197,7 @@ amdhsa.kernels:
            memsym="" if mem_slots is None else
            "\n\t.rodata\n\t.globl {n}_mem_slots\n\t.p2align 2\n\t.type {n}_mem_slots,@object\n"
            "{n}_mem_slots:\n\t.long {m}\n\t.size {n}_mem_slots, 4\n".format(n=name, m=int(mem_slots)),
-           nfree=512 if lanes == 1 and not TWO_WAVES else 256, aoff=nvgpr,
+           nfree=512 if lanes == 1 and not TWO_WAVES else 256, aoff=nvgpr, nsgpr=nsgpr, sgpr_count=nsgpr + 6,
            nagpr=(512 if lanes == 1 and not TWO_WAVES else 256) - nvgpr)
 
 

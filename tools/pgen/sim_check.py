@@ -45,6 +45,17 @@ def check(which, seed=5, lane=3, debug=True):
         bufs = {IN: rec}
         if which == "fei":
             bufs[OUT] = [0] * (72 * lane) + words(ins[12:])
+    elif which == "mls":
+        # P's coordinates and 68 lines of any field values (the loop does not
+        # care whether they come from a real G2Prepared)
+        import kernels
+        ins = [rng.randrange(dsl.Q) for _ in range(2)]
+        coeffs = [[rng.randrange(dsl.Q) for _ in range(6)] for _ in range(68)]
+        lines = kernels.shared_table_lines(coeffs)
+        prec = [0] * (13 * lane) + words(ins) + [0]
+        want = dsl.evaluate(prog, {0: ins[0], 1: ins[1], "lines": lines}, trace=trace)
+        args = [IN, AUX, OUT, lane + 1, WS]
+        bufs = {IN: prec, AUX: kernels.shared_table_u64(lines, infinity=False)}
     else:
         # any field values (the loop does not care whether they are on the curve)
         ins = [rng.randrange(dsl.Q) for _ in range(6)]
