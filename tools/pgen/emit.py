@@ -1059,6 +1059,8 @@ class Emitter:
                 vs.locs.add(loc)
                 self.bump("park_" + loc[0])
 
+    PRIO_TOGGLE = int(os.environ.get("PGEN_PRIO_TOGGLE", "0"))
+
     def run_construct(self, it):
         d = self.depth
         self.depth += 1
@@ -1069,6 +1071,21 @@ class Emitter:
             top, done = self.label(), None
             self.i("s_mov_b32", S(it.sreg), K(it.trips - 1))
             self.i("label", top)
+            if d == 0 and self.PRIO_TOGGLE:
+                # A/B (PGEN_PRIO_TOGGLE=1): wave priority 2 in odd iterations of
+                # the outer loop, 0 in even ones, so two co-resident waves of
+                # one SIMD take turns instead of the older one keeping nearly
+                # every issue slot (profiles/r05_coresidency.md)
+                even, done_ = self.label(), self.label()
+                self.i("s_and_b32", S(S_TMP), S(it.sreg), K(1))
+                self.i("s_cmp_eq_u32", S(S_TMP), K(0))
+                self.i("long_cbranch_scc1", even)
+                self.i("s_setprio", self.PRIO_TOGGLE)
+                self.i("s_cmp_eq_u32", S(S_TMP), S(S_TMP))
+                self.i("long_cbranch_scc1", done_)
+                self.i("label", even)
+                self.i("s_setprio", 0)
+                self.i("label", done_)
             self.untrack_stores()      # the previous iteration's stores
             self.run_block(it.body)
             self.i("s_sub_u32", S(it.sreg), S(it.sreg), K(1))

@@ -121,6 +121,8 @@ class Renderer:
             return ["s_waitcnt vmcnt(%d)" % a[0]]
         if m == "s_waitcnt_lgkm":
             return ["s_waitcnt lgkmcnt(%d)" % a[0]]
+        if m == "s_setprio":
+            return ["s_setprio %d" % a[0]]
         if m == "s_nop":
             return ["s_nop %d" % a[0]]
         if m == "s_and_saveexec_b64":

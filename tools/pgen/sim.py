@@ -358,6 +358,14 @@ class Sim:
             r = rd(a[1]) - rd(a[2])
             wr(a[0], r)
             self.scc = int(r < 0)
+        elif m == "s_and_b32":
+            r = rd(a[1]) & rd(a[2])
+            wr(a[0], r)
+            self.scc = int(r != 0)
+        elif m == "s_cmp_eq_u32":
+            self.scc = int(rd(a[0]) == rd(a[1]))
+        elif m == "s_setprio":
+            pass
         elif m == "s_cmp_ge_i32":
             self.scc = int(sx32(rd(a[0])) >= sx32(rd(a[1])))
         elif m == "s_cmp_eq_u64":
