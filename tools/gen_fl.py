@@ -55,6 +55,18 @@ QS = 40  # q limbs in s[40:53] (low: keeps the hipcc kernels under 80 SGPRs, 8 w
 QI = 54  # qinv in s54
 
 
+
+def _write_if_changed(path, text):
+    """rewrite a generated header only when its text changes, so that a build
+    after an unchanged generator run rebuilds nothing (make compares mtimes)"""
+    import os as _os
+    if _os.path.exists(path):
+        with open(path) as f:
+            if f.read() == text:
+                return
+    with open(path, "w") as f:
+        f.write(text)
+
 def limbs(v, n=NL):
     return [(v >> (LB * i)) & MASK for i in range(n)]
 
@@ -252,8 +264,7 @@ def main():
         H.extend(wrapper(cname, name, nin, out, clob))
         H.append("")
     H.append("}  // namespace pa")
-    with open(out_path, "w") as f:
-        f.write("\n".join(H) + "\n")
+    _write_if_changed(out_path, "\n".join(H) + "\n")
     n_instr = {name: sum(1 for l in body if l and not l.endswith(":") and not l.startswith(".")) for name, body, *_ in leaves}
     print("wrote %s: %s" % (out_path, n_instr))
 

@@ -26,6 +26,18 @@ import os
 PER_BLOCK = 4
 
 
+
+def _write_if_changed(path, text):
+    """rewrite a generated header only when its text changes, so that a build
+    after an unchanged generator run rebuilds nothing (make compares mtimes)"""
+    import os as _os
+    if _os.path.exists(path):
+        with open(path) as f:
+            if f.read() == text:
+                return
+    with open(path, "w") as f:
+        f.write(text)
+
 def block(chains, prods):
     """prods: list of (chain, x_expr, y_expr, y_is_sgpr) for one asm statement."""
     text = []
@@ -207,8 +219,7 @@ def main():
         "}  // namespace pa",
         "",
     ]
-    with open(out, "w") as f:
-        f.write("\n".join(body))
+    _write_if_changed(out, "\n".join(body))
     print("wrote", out)
 
 
