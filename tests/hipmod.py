@@ -21,7 +21,7 @@ def _hip():
     return ctypes.CDLL(path or "libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
 
 
-def launch(name, a0, a1, a2, n, ws_slots=1):
+def launch(name, a0, a1, a2, n, ws_slots=1, lanes=1):
     """run kernel pa_gen_<name> from lib/test/pa_gen_<name>.hsaco over n lanes
     with the generated kernels' five arguments (a0, a1, a2: torch CUDA tensors
     or None; a per-wave spill workspace of ws_slots slots)"""
@@ -34,7 +34,7 @@ def launch(name, a0, a1, a2, n, ws_slots=1):
     assert hip.hipModuleLoad(ctypes.byref(mod), path.encode()) == 0, "hipModuleLoad " + path
     try:
         assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, ("pa_gen_" + name).encode()) == 0
-        blocks = (n + 63) // 64
+        blocks = (n * lanes + 63) // 64
         ws = torch.zeros(blocks * ws_slots * SLOT_BYTES, dtype=torch.uint8, device="cuda")
 
         class Args(ctypes.Structure):

@@ -22,7 +22,7 @@ import unit_progs  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _run(name, prog, rows):
+def _run(name, prog, rows, lanes=1, ws_slots=1):
     """rows: lists of 12 canonical ABI integers; returns (gpu rows, model rows)"""
     import torch
     import hipmod
@@ -34,7 +34,7 @@ def _run(name, prog, rows):
                 words[i, 6 * k + j] = (x >> (64 * j)) & ((1 << 64) - 1)
     src = torch.from_numpy(words.view(np.int64)).cuda()
     out = torch.zeros_like(src)
-    hipmod.launch(name, src, out, None, n)
+    hipmod.launch(name, src, out, None, n, ws_slots=ws_slots, lanes=lanes)
     got = out.cpu().numpy().view(np.uint64)
     gpu = [[sum(int(got[i, 6 * k + j]) << (64 * j) for j in range(6)) for k in range(12)] for i in range(n)]
     model = []
@@ -73,4 +73,16 @@ def test_karabina_decompression_on_gpu():
     elems = [tp._cyclotomic(s) for s in range(20)] + [tp._b0_zero_element(), pm.F12ONE]
     rows = [tp._abi_words(f) for f in elems] * 3
     gpu, model = _run("tdec", unit_progs.dec_prog(), rows)
+    assert gpu == model == rows
+
+
+def test_karabina_decompression_lane_pairs_on_gpu():
+    """the same on the lane-pair tower (round 5: the lane-pair final
+    exponentiation squares compressed too): the b0 == 0 select reads both
+    lanes' coordinates, the norm's binary GCD runs on both lanes"""
+    import test_pgen as tp
+    import pymodel as pm
+    elems = [tp._cyclotomic(s) for s in range(20)] + [tp._b0_zero_element(), pm.F12ONE]
+    rows = [tp._abi_words(f) for f in elems] * 3
+    gpu, model = _run("tdec2", unit_progs.dec_prog(lanes=2), rows, lanes=2, ws_slots=64)
     assert gpu == model == rows

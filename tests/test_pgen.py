@@ -349,14 +349,17 @@ def _abi_words(f):
     return [(x * R384) % dsl.Q for c6 in f for c2 in c6 for x in c2]
 
 
+@pytest.mark.parametrize("lanes", [1, 2])
 @pytest.mark.parametrize("which", ["random", "b0_zero", "identity"])
-def test_dsl_karabina_decompression(which):
+def test_dsl_karabina_decompression(which, lanes):
     """the DSL decompression (both branches of the b0 == 0 select, and the
-    identity whose inversion input is 0) rebuilds the element exactly"""
+    identity whose inversion input is 0) rebuilds the element exactly, on
+    one lane and on the lane-pair tower"""
     import pymodel as pm
+    import unit_progs
     f = {"random": lambda: _cyclotomic(3), "b0_zero": _b0_zero_element, "identity": lambda: pm.F12ONE}[which]()
     ins = _abi_words(f)
-    out = dsl.evaluate(_dec_prog(), {k: ins[k] for k in range(12)})
+    out = dsl.evaluate(unit_progs.dec_prog(lanes=lanes), {k: ins[k] for k in range(12)})
     assert [out[k] for k in range(12)] == ins
 
 
@@ -420,6 +423,26 @@ def test_sim_karabina_decompression_b0_zero():
     ins = _abi_words(_b0_zero_element())
     got, want = _sim_run(_dec_prog(), ins)
     assert got == want == ins
+
+
+def test_sim_karabina_decompression_b0_zero_lane_pairs():
+    """the same for the lane-pair program, both lanes simulated in lockstep"""
+    import kcfg
+    import sim
+    import unit_progs
+    prog = unit_progs.dec_prog(lanes=2)
+    cfg = kcfg.FinalExpCfg2()
+    cfg.name = prog.name
+    code, _ = kcfg.build(prog, cfg, debug=True)
+    ins = _abi_words(_b0_zero_element())
+    trace = []
+    want = dsl.evaluate(prog, {k: ins[k] for k in range(12)}, trace=trace)
+    lane = 3
+    IN, OUT, AUX, WS = 0x100000, 0x200000, 0x300000, 0x400000
+    sm = sim.run_lane(code, [IN, OUT, AUX, lane + 1, WS], {IN: [0] * (72 * lane) + sim_check.words(ins)},
+                      lane=2 * lane, trace=trace, pair=True)
+    got = [sum(sm.mem.get(OUT + 576 * lane + 48 * k + 4 * j, 0) << (32 * j) for j in range(12)) for k in range(12)]
+    assert got == [want[k] for k in range(12)] == ins
 
 
 def test_local_homes_free_dead_variables():

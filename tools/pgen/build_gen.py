@@ -97,6 +97,7 @@ PROGRAMS = {
     # test-only kernels (tools/pgen/unit_progs.py, tests/test_gen_units.py)
     "tdec": _mk(lambda: __import__("unit_progs").dec_prog(), kcfg.FinalExpCfg, "pa_gen_tdec"),
     "tunit": _mk(lambda: __import__("unit_progs").unit_prog(), kcfg.FinalExpCfg, "pa_gen_tunit"),
+    "tdec2": _mk(lambda: __import__("unit_progs").dec_prog(lanes=2), kcfg.FinalExpCfg2, "pa_gen_tdec2"),
     "fe2": _mk(lambda: kernels.final_exp_prog(lanes=2), kcfg.FinalExpCfg2, "pa_gen_final_exp2"),
     # lazy reduction (tower.TowerLazy): wide products, one reduction per output Fq
     # (measured slower; built only on request for A/B runs)
@@ -108,7 +109,7 @@ FILES = {"small": "pa_gen_small.hsaco", "cyc": "pa_gen_cyc.hsaco", "ml": "pa_gen
          "fen": "pa_gen_fe_norm.hsaco", "fei": "pa_gen_fe_inv.hsaco",
          "ml2": "pa_gen_miller_loop2.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
          "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco",
-         "tdec": "test/pa_gen_tdec.hsaco", "tunit": "test/pa_gen_tunit.hsaco"}
+         "tdec": "test/pa_gen_tdec.hsaco", "tunit": "test/pa_gen_tunit.hsaco", "tdec2": "test/pa_gen_tdec2.hsaco"}
 
 
 def build(which, outdir):

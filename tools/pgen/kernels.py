@@ -282,21 +282,25 @@ def exp_by_x_karabina(p, T, V, xv, L, first_skip, tag="k"):
     exp_by_x(x >> 1) call (bits 15, 47, 56, 59, 61, 62)."""
     bits = [i for i in range(X_ABS.bit_length()) if (X_ABS >> i) & 1]
     res, top = "kr%s_" % tag, "kt%s_" % tag
-    # the compressed state's homes are those of the later GS state's first 8
-    # coordinates (the two never live at once)
-    kn = ["%s%d_%d" % (top, j // 2, j % 2) for j in range(8)]
+    one = p.lanes == 1   # lane pairs: a distributed Fq2 is one variable (<n>0)
+    # the compressed state's homes are those of the later GS state's first 4
+    # Fq2 coordinates (the two never live at once)
+    kn = ["%s%d_%d" % (top, j // 2, j % 2) for j in range(8)] if one else ["%s%d_0" % (top, i) for i in range(4)]
     for n in kn:
         p.var(n, 1, os.environ.get("PGEN_KC_HOME", "A"))
     (_, a1, a2), (b0, _, b2) = V.get12(xv)
-    for n, v in zip(kn, [*a1, *a2, *b0, *b2]):
+    for n, v in zip(kn, [*a1, *a2, *b0, *b2] if one else [a1, a2, b0, b2]):
         p.set(n, v)
 
     def getg(names):
         g = [p.get(n) for n in names]
-        return ((g[0], g[1]), (g[2], g[3]), (g[4], g[5]), (g[6], g[7]))
+        return ((g[0], g[1]), (g[2], g[3]), (g[4], g[5]), (g[6], g[7])) if one else tuple(g)
+
+    def flat(g4):
+        return [c for x2 in g4 for c in x2] if one else list(g4)
 
     def ksqr_state():
-        for n, v in zip(kn, [c for x2 in T.ksqr(getg(kn)) for c in x2]):
+        for n, v in zip(kn, flat(T.ksqr(getg(kn)))):
             p.set(n, v)
 
     saved, prev = [], 0
@@ -311,7 +315,7 @@ def exp_by_x_karabina(p, T, V, xv, L, first_skip, tag="k"):
                 ksqr_state()
         prev = b
         if k < 2:
-            sn = ["ks%s%d_%d" % (tag, k, i) for i in range(8)]
+            sn = ["ks%s%d_%d" % (tag, k, i) for i in range(len(kn))]
             for n in sn:
                 p.var(n, 1, os.environ.get("PGEN_KS_HOME", "M"))
             for n, v in zip(sn, [p.get(m) for m in kn]):
@@ -327,11 +331,9 @@ def exp_by_x_karabina(p, T, V, xv, L, first_skip, tag="k"):
     # top: the GS state reuses the 8 compressed-state homes (dead by now) plus
     # four more; res: 6 + 6 coordinates in AGPRs + the workspace
     V.declare12(res, os.environ.get("PGEN_KR_HOME", "AAAAAAMMMMMM"))
-    for i in range(6):
-        for c in (0, 1):
-            j = 2 * i + c
-            if j >= 8:
-                p.var("%s%d_%d" % (top, i, c), 1, os.environ.get("PGEN_KT_HOME", "A"))
+    for i in range(4, 6):
+        for c in ((0, 1) if one else (0,)):
+            p.var("%s%d_%d" % (top, i, c), 1, os.environ.get("PGEN_KT_HOME", "A"))
     if order == "0":
         V.set12(top, F[2])
         V.set12(res, T.mul12(T.mul12(F[0], F[1]), F[2]))
@@ -451,7 +453,10 @@ def final_exp_prog(lanes=1, lazy=False, tower_cls=None, split=None):
     # one-lane programs invert in the kernel by binary GCD (emit.emit_binv) and
     # exponentiate by x with compressed squarings; PGEN_KARABINA=0: Fermat +
     # Granger-Scott (round 2)
-    kara = lanes == 1 and tower_cls is None and split is None and _karabina()
+    # lane pairs (round 5, PGEN_FE2_KARA=0: round 2's form for A/B): the same
+    # Karabina squarings and in-kernel binary GCD (Tower2's kdec_numden / inv2)
+    kara = ((lanes == 1 or os.environ.get("PGEN_FE2_KARA", "1") == "1") and tower_cls is None and split is None
+            and _karabina())
     p.binv_ok = kara
     f = V.load12()
     if split is not None:

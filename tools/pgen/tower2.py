@@ -65,6 +65,29 @@ class Tower2(Tower):
     def one2(self):
         return self.const2((1, 0))
 
+    # ---------------- Karabina decompression (tower.Tower, lane pairs) ----------------
+    def kdec_numden(self, g):
+        """Tower.kdec_numden on distributed Fq2: the b0 == 0 test reads both
+        coordinates (this lane's and the partner's), so both lanes of a pair
+        take the same branch; w = 3 a1 a2 - b0 b2 as two Fq2 products"""
+        t, p = self, self.p
+        a1, a2, b0, b2 = g
+        s1 = t.sqr2(a1)
+        num1 = t.red2(t.sub2(t.add2(t.add2(t.dbl2(s1), s1), t.xi(t.sqr2(b2))), t.dbl2(a2)))
+        den1 = t.red2(t.dbl2(t.dbl2(b0)))
+        num2 = t.red2(t.dbl2(t.mul2(a1, b2)))
+        den2 = t.red2(a2)
+        zb = p.red_full(b0)
+        z = [zb, p.swap(zb)]
+        num = p.selz(z, num2, num1)
+        den = p.selz(z, den2, den1)
+        a13 = t.lim2(t.add2(t.dbl2(a1), a1))
+        w = t.red2(t.sub2(t.mul2(a13, a2), t.mul2(b0, b2)))
+        return num, den, w
+
+    def inv2_direct(self, a, tag):
+        return self.inv2(a, tag)
+
     # ---------------- inversion ----------------
     def inv2(self, a, tag):
         """fq2.rs:138-155: the norm a0^2 + a1^2 is formed on both lanes and

@@ -7,15 +7,17 @@ from dsl import Prog
 from tower import TowerLazySq
 
 
-def dec_prog():
+def dec_prog(lanes=1):
     """load an Fq12, keep its compressed coordinates (a1, a2, b0, b2),
     decompress them (kdec_numden + batch_inv2 over one value + kdec_finish)
-    and store the Fq12"""
+    and store the Fq12.  lanes = 2: the lane-pair tower (tower2.Tower2, the
+    round-5 lane-pair final exponentiation's decompression)"""
     import kernels
-    p = Prog("tdec", use_norm=True)
+    from tower2 import Tower2
+    p = Prog("tdec" if lanes == 1 else "tdec2", lanes, use_norm=lanes == 1)
     p.binv_ok = True
-    T = TowerLazySq(p)
-    V = kernels._Vars(p, 1)
+    T = TowerLazySq(p) if lanes == 1 else Tower2(p)
+    V = kernels._Vars(p, lanes)
     (_, a1, a2), (b0, _, b2) = V.load12()
     g = (a1, a2, b0, b2)
     num, den, w = T.kdec_numden(g)
