@@ -248,7 +248,7 @@ def build(prog, cfg, debug=False):
     import os
     from emit import Emitter, plan_ctab
     from dsl import fuse_adds
-    if prog.lanes == 1 and prog.use_norm and os.environ.get("PGEN_FUSE", "1") == "1":
+    if prog.use_norm and os.environ.get("PGEN_FUSE", "1") == "1":
         fuse_adds(prog)
     plan = None
     if os.environ.get("PGEN_SAD", "1") == "1":

@@ -20,8 +20,11 @@ ML_MASK = (X_ABS >> 1) & ((1 << 62) - 1)  # bits 61..0 below the leading one of 
 
 def _norm(lanes):
     """carry-normalize instead of reducing where value bounds allow (dsl.VB_PROD);
-    one-lane kernels only (PGEN_NORM=0: the full reduction everywhere, A/B)"""
-    return lanes == 1 and os.environ.get("PGEN_NORM", "1") == "1"
+    round 5: lane-pair kernels too (-1 % instructions; PGEN_NORM2=0 keeps the full
+    reduction there); PGEN_NORM=0: the full reduction everywhere, A/B"""
+    if lanes == 2 and os.environ.get("PGEN_NORM2", "1") != "1":
+        return False
+    return os.environ.get("PGEN_NORM", "1") == "1"
 
 
 def doubling_step(T, r):

@@ -14,7 +14,7 @@ def dec_prog(lanes=1):
     round-5 lane-pair final exponentiation's decompression)"""
     import kernels
     from tower2 import Tower2
-    p = Prog("tdec" if lanes == 1 else "tdec2", lanes, use_norm=lanes == 1)
+    p = Prog("tdec" if lanes == 1 else "tdec2", lanes, use_norm=True)
     p.binv_ok = True
     T = TowerLazySq(p) if lanes == 1 else Tower2(p)
     V = kernels._Vars(p, lanes)
