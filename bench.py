@@ -41,6 +41,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # = 1024 waves = the chip's 1024 SIMDs), whose own ceiling is VALU_MAC_1WAVE_T.
 VALU_MAC_PEAK_T = 35.96
 VALU_MAC_1WAVE_T = 21.32
+# two waves per SIMD (the lane-pair kernels at 2^16), same probe
+# (profiles/r03_valu_peak.txt)
+VALU_MAC_2WAVE_T = 29.12
 # issue ceiling of the one-wave-per-SIMD pairing kernels: one wave issues at most
 # one instruction per 4 clk (SQ: one ACTIVE_INST quad-cycle per instruction), at
 # the 2.33 GHz the chip holds under them (GRBM_GUI_ACTIVE, profiles/r02_cyc_probe.txt)
@@ -146,13 +149,14 @@ def make_pairs(n, rank, seed=0, span=None):
 
 def kernel_variant_label(n):
     """the pairing kernels a batch of n per GPU runs on (capi.hip: PA_PAIRING_KERNEL 0 = by
-    batch size, <= PA_COOP_MAX cooperative quad VM, <= PA_PAIR_MAX generated lane pairs, else
-    generated one lane; 1 lane pairs, 2 quad VM, 3 one lane, 4 one-wave VM)"""
+    batch size: <= PA_COOP_MAX cooperative quad VM, <= PA_PAIR_MAX generated lane pairs, <= PA_ONE_MAX
+    generated one lane, else lane pairs again; 1 lane pairs, 2 quad VM, 3 one lane, 4 one-wave VM)"""
     v = int(os.environ.get("PA_PAIRING_KERNEL", "0"))
     if v == 0:
-        if n <= int(os.environ.get("PA_COOP_MAX", "2560")):
+        if n <= int(os.environ.get("PA_COOP_MAX", "2304")):
             return "coop"
-        return "gen2" if n <= int(os.environ.get("PA_PAIR_MAX", "32768")) else "gen"
+        one = int(os.environ.get("PA_PAIR_MAX", "32768")) < n <= int(os.environ.get("PA_ONE_MAX", "38912"))
+        return "gen" if one else "gen2"
     return {1: "gen2", 2: "coop", 3: "gen", 4: "coop1"}.get(v, "variant%d" % v)
 
 
@@ -888,11 +892,12 @@ def main():
             config["parallelism"] = ("shard%d+partial_sums_to_root" if args.workload == "msm" else
                                      "replicas%d" if args.workload == "verify" else "shard%d+rccl_gather") % ws
         achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, traffic_all = None, {}
         tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tr_path):
             with open(tr_path) as f:
-                traffic = json.load(f).get(dom_name)
+                traffic_all = json.load(f)
+            traffic = traffic_all.get(dom_name)
         roof = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "bytes_per_unit": dom_bytes, "avg_launch_ms": round(dom_ms, 4)}
@@ -916,23 +921,40 @@ def main():
             # in-kernel binary-GCD inversions, compressed squarings).  The
             # binary GCD's instructions are counted, its 64-bit approximation
             # steps are not limb MACs.
-            wk = work["final_exp"] if dom_name == "final_exponentiation" else \
-                work["miller_loop_shared"] if dom_name == "miller_loop_shared" else work["miller_loop"]
+            # which code objects ran: the lane-pair kernels' work per pairing (two
+            # lanes) differs from the one-lane kernels'
+            lp = args.workload == "pairing" and kernel_variant_label(n) == "gen2"
+            wk = work["final_exp_lane_pairs" if lp else "final_exp"] if dom_name == "final_exponentiation" else \
+                work["miller_loop_shared"] if dom_name == "miller_loop_shared" else \
+                work["miller_loop_lane_pairs" if lp else "miller_loop"]
+            if lp:
+                roof_kernel = {"final_exponentiation": "pa_gen_final_exp2",
+                               "miller_loop_fused": "pa_gen_miller_loop2"}.get(dom_name, dom_name)
+                traffic = traffic_all.get(dom_name + "_lane_pairs")
             macs = wk["limb_macs"]
             mac_rate = macs * n / (dom_ms * 1e-3) / 1e12
             roof = {"kernel": dom_name, "bound": "valu", "achieved": round(mac_rate, 3),
                     "peak": round(VALU_MAC_PEAK_T, 3), "unit": "T limb-MAC/s (28x28-bit v_mad_u64_u32)",
                     "frac": mac_rate / VALU_MAC_PEAK_T, "traffic": traffic, "macs_per_unit": macs,
                     "avg_launch_ms": round(dom_ms, 4),
-                    "peak_one_wave_per_simd": VALU_MAC_1WAVE_T, "frac_one_wave": mac_rate / VALU_MAC_1WAVE_T,
                     "hbm": {"achieved_GBs": round(achieved, 3), "peak_GBs": HBM_PEAK_GBS,
                             "bytes_per_unit": dom_bytes}}
+            if lp:
+                # the lane-pair code objects, two lanes per pairing, two waves per SIMD at 2^16
+                roof["code_object"] = roof_kernel
+                roof["peak_two_waves_per_simd"] = VALU_MAC_2WAVE_T
+                roof["frac_two_waves"] = mac_rate / VALU_MAC_2WAVE_T
+            else:
+                roof["peak_one_wave_per_simd"] = VALU_MAC_1WAVE_T
+                roof["frac_one_wave"] = mac_rate / VALU_MAC_1WAVE_T
             instr = wk.get("instructions")
-            if instr:
+            if instr and not lp:
                 rate = instr * n / (dom_ms * 1e-3) / 1e12
                 roof["issue"] = {"achieved": round(rate, 3), "peak": round(ISSUE_PEAK_T, 3),
                                  "unit": "T lane-instructions/s (one wave per SIMD)", "frac": rate / ISSUE_PEAK_T,
                                  "instructions_per_unit": instr}
+            elif instr:
+                roof["instructions_per_unit"] = instr
         if args.workload == "wnaf" and dom_name == "g1_glv_comb_mul":
             # VALU bound: each mixed addition (madd-2007-bl, ec.rs:446-526) is
             # 7 products + 4 squarings on the lazy 28-bit core (fl_gen.h

@@ -79,13 +79,15 @@ int pa_set_device(int device);
 int pa_synchronize(void);
 /* Tuning knob: which kernels run the Miller loop / final exponentiation
  * (identical results):
- *   0 = default, by batch size n: n <= PA_COOP_MAX (2560) on the
+ *   0 = default, by batch size n: n <= PA_COOP_MAX (2304) on the
  *       cooperative kernels (a four-wave quad-VM workgroup per pairing,
  *       kernels_coop.hip: the verifier shape, ~1.6 ms), n <= PA_PAIR_MAX
  *       (32768) on the generated kernels with a lane pair per pairing
- *       (~10 ms), larger batches on the generated one-pairing-per-lane
- *       kernels (tools/pgen: own register allocation, code objects
- *       lib/pa_gen_*.hsaco loaded at first use; 2^16 in ~17.4 ms)
+ *       (~8.6-9.3 ms), n <= PA_ONE_MAX (38912) on the generated
+ *       one-pairing-per-lane kernels (~16.1 ms), larger batches on lane
+ *       pairs again, two waves per SIMD (2^16 in ~16.7 ms; tools/pgen: own
+ *       register allocation, code objects lib/pa_gen_*.hsaco loaded at
+ *       first use)
  *   1 = generated kernels with a lane pair per pairing, every size (A/B)
  *   2 = cooperative kernels for every size (A/B, tests)
  *   3 = generated one-pairing-per-lane kernels for every size (A/B, tests)

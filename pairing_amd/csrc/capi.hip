@@ -23,13 +23,17 @@ namespace {
 
 thread_local std::string g_last_error;
 // Pairing kernel selection (pa_set_pairing_kernel).  0 (default) by batch
-// size, each where it is fastest (profiles/r03_s3_batch_regimes.txt):
-//   n <= coop_max() (2560): the cooperative kernels (kernels_coop.hip, a
+// size, each where it is fastest (round 5, profiles/r05_regimes.txt):
+//   n <= coop_max() (2304): the cooperative kernels (kernels_coop.hip, a
 //      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
 //   n <= pair_max() (32768): the generated kernels with a lane pair per
-//      pairing (<= 1 wave per SIMD either way, so half the instructions per
-//      lane is half the time: ~10 ms where one lane takes ~15.7 ms);
-//   larger: one lane per pairing (2^16: 17.3 vs 20.3 ms for lane pairs).
+//      pairing, at most one wave per SIMD: 8.6-9.3 ms whatever n;
+//   n <= one_max() (38912): one lane per pairing (one wave per SIMD at most:
+//      ~16.1 ms, where a second lane-pair wave on some SIMDs costs 16.3-17.5);
+//   larger: lane pairs again, two or more waves per SIMD (2^16: 16.7 ms
+//      against 17.2 ms one lane; 2^17: 33.0 vs 34.1 ms).  Round 5 gave the
+//      lane-pair final exponentiation the Karabina squarings and the
+//      in-kernel binary GCD (8.7 ms at 2^16 instead of 12.3 ms).
 // 1 -> lane pairs for every batch size; 2 -> cooperative for every batch
 // size; 3 -> one lane per pairing for every batch size; 4 -> cooperative for
 // every batch size on the round-2 one-wave VM (A/B against the quad VM).
@@ -42,11 +46,15 @@ size_t env_size(const char* name, size_t dflt) {
     return e ? (size_t)strtoull(e, nullptr, 10) : dflt;
 }
 size_t coop_max() {
-    static const size_t v = env_size("PA_COOP_MAX", 2560);
+    static const size_t v = env_size("PA_COOP_MAX", 2304);
     return v;
 }
 size_t pair_max() {
     static const size_t v = env_size("PA_PAIR_MAX", 32768);
+    return v;
+}
+size_t one_max() {
+    static const size_t v = env_size("PA_ONE_MAX", 38912);
     return v;
 }
 bool use_coop(size_t n) {
@@ -59,7 +67,7 @@ int gen_lanes(size_t n) {
     const int v = pairing_variant();
     if (v == 1) return 2;
     if (v == 3) return 1;
-    return n <= pair_max() ? 2 : 1;
+    return n <= pair_max() || n > one_max() ? 2 : 1;
 }
 // multi-pairings of at most this many pairs multiply their Miller values inside
 // the cooperative final exponentiation (sequential mul12 macros); larger ones

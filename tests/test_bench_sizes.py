@@ -82,9 +82,12 @@ def test_fr_mul_device_bit_exact_at_bench_size(gpu, oracle, n):
     np.testing.assert_array_equal(_host(out), oracle.fr_mul(a, b))
 
 
-def test_pairing_device_bit_exact_at_bench_size(gpu, oracle):
-    """config 4: 2^16 pairings (1024 waves, every wave with its own spill
-    workspace) on the bench's own inputs, every pairing against the oracle"""
+@pytest.mark.parametrize("variant", [0, 3], ids=["default_lane_pairs", "one_lane"])
+def test_pairing_device_bit_exact_at_bench_size(gpu, oracle, variant):
+    """config 4: 2^16 pairings on the bench's own inputs, every pairing against
+    the oracle -- on the default selection (round 5: lane pairs, 2048 waves,
+    two per SIMD) and on the one-lane kernels (1024 waves), every wave with its
+    own spill workspace"""
     import torch
     import bench
     import pairing_amd.device as pdev
@@ -92,8 +95,12 @@ def test_pairing_device_bit_exact_at_bench_size(gpu, oracle):
     p_np, q_np = bench.make_pairs(n, 0)
     out = pdev.empty_records(n, 72, "cuda:0")
     scratch = pdev.empty_records(n, 72, "cuda:0")
-    pdev.pairing(_dev(p_np), _dev(q_np), out, scratch)
-    torch.cuda.synchronize()
+    gpu.set_pairing_kernel(variant)
+    try:
+        pdev.pairing(_dev(p_np), _dev(q_np), out, scratch)
+        torch.cuda.synchronize()
+    finally:
+        gpu.set_pairing_kernel(0)
     got = _host(out)
     exp = oracle.pairing(p_np, q_np, _threads())
     np.testing.assert_array_equal(got, exp)
@@ -105,10 +112,11 @@ def test_pairing_device_bit_exact_at_bench_size(gpu, oracle):
     assert (got[inf] == one).all()
 
 
-@pytest.mark.parametrize("n", [2561, 32768])
+@pytest.mark.parametrize("n", [2305, 32768, 32769, 38912, 38913])
 def test_pairing_default_mid_size_batches(gpu, oracle, n):
-    """The default selection's middle regime (PA_COOP_MAX < n <= PA_PAIR_MAX:
-    the generated kernels with a lane pair per pairing) at both ends, every
+    """The default selection's regime boundaries (PA_COOP_MAX < n <= PA_PAIR_MAX:
+    lane pairs at one wave per SIMD; PA_PAIR_MAX < n <= PA_ONE_MAX: one lane per
+    pairing; above: lane pairs at two waves per SIMD) on both sides, every
     pairing against the oracle"""
     import torch
     import bench

@@ -130,7 +130,7 @@ def _hip_worker(rank, world, port, n, result_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [64, 1000])  # even / ragged shards; the product runs on the cooperative path (<= 2560)
+@pytest.mark.parametrize("n", [64, 1000])  # even / ragged shards; the product runs on the cooperative path (<= 2304)
 def test_sharded_pairing_world2_hip(tmp_path, oracle, n):
     # the parent never touches the GPU (the ranks do; a rank without a device raises)
     world = 2

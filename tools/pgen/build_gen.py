@@ -153,8 +153,9 @@ def write_work_json(outdir):
     rng = random.Random(1)
     out = {}
     for key, name, nin in (("ml", "miller_loop", 6), ("fe", "final_exp", 12), ("fen", "fe_norm", 12),
-                           ("fei", "fe_inv", 13), ("mls", "miller_loop_shared", 2)):
-        if key in ("fen", "fei", "mls") and not PROGRAMS[key].cache:
+                           ("fei", "fe_inv", 13), ("mls", "miller_loop_shared", 2),
+                           ("ml2", "miller_loop_lane_pairs", 6), ("fe2", "final_exp_lane_pairs", 12)):
+        if key in ("fen", "fei", "mls", "ml2", "fe2") and not PROGRAMS[key].cache:
             continue
         prog = PROGRAMS[key]()[0]
         st = dsl.Stats()
@@ -165,7 +166,11 @@ def write_work_json(outdir):
         em = PROGRAMS[key].cache["r"][5]
         # instructions one lane executes (exact: the loop trip counts and branch
         # masks are static, the emitter weights every instruction by them)
-        out[name] = {"limb_macs": macs(st.counts), "ops": st.counts, "instructions": round(em.dyn_instr)}
+        # lane pairs: the DSL counts and the emitter's estimate are per lane;
+        # a pairing is two lanes' work
+        lanes = prog.lanes
+        out[name] = {"limb_macs": lanes * macs(st.counts), "ops": st.counts,
+                     "instructions": round(lanes * em.dyn_instr), "lanes_per_pairing": lanes}
     with open(os.path.join(outdir, "pa_gen_work.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 
@@ -182,7 +187,9 @@ def main():
     for w in args or ["ml", "fe", "ml2", "fe2", "mls"]:
         build(w, outdir)
         meta[w] = PROGRAMS[w].cache["r"][3]
-    if "ml" in meta and "fe" in meta:
+    if "ml" in meta and "fe" in meta or "ml2" in meta and "fe2" in meta:
+        for k in ("ml", "fe", "ml2", "fe2", "mls"):
+            PROGRAMS[k]()   # every program the work file describes
         write_work_json(outdir)
     if all(k in meta for k in ("ml", "fe", "ml2", "fe2", "mls")):
         hdr = os.path.join(ROOT, "pairing_amd", "csrc", "pa_gen_meta.h")
