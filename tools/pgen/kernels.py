@@ -80,10 +80,16 @@ def ell(T, f, c, px, py):
 ML_HOMES = {"px": "L", "py": "L", "qx0": "M", "qx1": "M", "qy0": "M", "qy1": "M",
             "rx0": "A", "rx1": "A", "ry0": "A", "ry1": "A", "rz0": "A", "rz1": "A", "f": "A"}
 # the Fq12 variable names f<i>_<c> carry the home of "f"
+# lane pairs (no AGPRs, 5 LDS slots): f -- read by every line and square -- in
+# five of the LDS slots, P's packed coordinates and the G2 point (read once per
+# step) in the workspace: half the workspace traffic of the AGPR-first homes
+# (1119 -> 545 loads, 657 -> 341 stores per lane; PGEN_ML2_HOMES=0: the old homes)
+ML2_HOMES = {"f": "LLLLLLLLLLMM", "px": "M", "rx0": "M", "ry0": "M", "rz0": "M"}
 
 
 def miller_loop_prog(homes=None, lanes=1, lazy=False):
-    homes = dict(ML_HOMES, **(homes or {}))
+    base = dict(ML_HOMES, **ML2_HOMES) if lanes == 2 and os.environ.get("PGEN_ML2_HOMES", "1") == "1" else ML_HOMES
+    homes = dict(base, **(homes or {}))
     p = Prog("miller_loop" if lanes == 1 else "miller_loop2", lanes, use_norm=_norm(lanes))
     T = (TowerLazy(p) if lazy else Tower(p)) if lanes == 1 else Tower2(p)
     V = _Vars(p, lanes)
