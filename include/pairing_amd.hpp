@@ -638,6 +638,18 @@ struct Bls12 {
               "Bls12::miller_loop");
         return r;
     }
+    // Engine::miller_loop([(p_i, q)]) for every i with ONE prepared q (the same
+    // &G2Prepared in each pair, lib.rs:88-96): a verifying key's prepared gamma /
+    // delta against many points; q's lines are staged once per call
+    static std::vector<Fq12> miller_loop_shared(const std::vector<G1Prepared>& p, const G2Prepared& q) {
+        std::vector<pa_g1_affine> pp(p.size());
+        for (size_t i = 0; i < p.size(); i++) pp[i] = p[i].p.v;
+        std::vector<Fq12> out(p.size());
+        if (!p.empty())
+            check(pa_miller_loop_shared_prepared(pp.data(), pp.size(), q.v.get(), &out[0].v),
+                  "Bls12::miller_loop_shared");
+        return out;
+    }
     // Engine::final_exponentiation (mod.rs:104-160): None iff f == 0
     static std::optional<Fq12> final_exponentiation(const Fq12& f) {
         Fq12 r;

@@ -79,6 +79,24 @@ static void random_bilinearity_tests(const Data& d) {
     EXPECT(Bls12::pairing(d.a_p[0], d.b_q[0]) == d.e_ab[0]);
 }
 
+// one prepared Q shared by many P (lib.rs:88-96 with the same &G2Prepared):
+// every output equals miller_loop over that single pair, and its final
+// exponentiation equals the pairing
+static void shared_prepared_miller_loop_tests(const Data& d) {
+    const G2Prepared q = d.b_q[0].prepare();
+    std::vector<G1Prepared> ps;
+    for (size_t i = 0; i < 6; i++) ps.push_back(d.a_p[i].prepare());
+    ps.push_back(G1Affine::zero().prepare());
+    const auto f = Bls12::miller_loop_shared(ps, q);
+    EXPECT(f.size() == ps.size());
+    for (size_t i = 0; i < ps.size(); i++) {
+        EXPECT(f[i] == Bls12::miller_loop({{&ps[i], &q}}));
+        if (i < 6) EXPECT(Bls12::final_exponentiation(f[i]).value() == Bls12::pairing(d.a_p[i], d.b_q[0]));
+    }
+    EXPECT(f.back() == Fq12::one());
+    EXPECT(Bls12::miller_loop_shared({}, q).empty());
+}
+
 // engine.rs:50-91: miller_loop over two pairs == product of single pairings
 static void random_miller_loop_tests(const Data& d) {
     for (size_t i = 0; i + 1 < d.n && i < 6; i += 2) {
@@ -421,6 +439,7 @@ int main(int argc, char** argv) {
             {"test_pairing_result_against_relic", [&] { test_pairing_result_against_relic(d); }},
             {"random_bilinearity_tests", [&] { random_bilinearity_tests(d); }},
             {"random_miller_loop_tests", [&] { random_miller_loop_tests(d); }},
+            {"shared_prepared_miller_loop_tests", [&] { shared_prepared_miller_loop_tests(d); }},
             {"encoding_tests", [&] { encoding_tests(d); }},
             {"wnaf_batch_normalization_tests", [&] { wnaf_batch_normalization_tests(d); }},
             {"sqrt_tests", [&] { sqrt_tests(); }},
