@@ -923,7 +923,11 @@ def main():
             # steps are not limb MACs.
             # which code objects ran: the lane-pair kernels' work per pairing (two
             # lanes) differs from the one-lane kernels'
-            lp = args.workload == "pairing" and kernel_variant_label(n) == "gen2"
+            # (the prepared workloads' final exponentiation follows the same
+            # selection, pairing_amd/csrc/capi.hip fe_launch; their Miller loops
+            # are other kernels)
+            lp = kernel_variant_label(n) == "gen2" and (args.workload == "pairing" or
+                                                        dom_name == "final_exponentiation")
             wk = work["final_exp_lane_pairs" if lp else "final_exp"] if dom_name == "final_exponentiation" else \
                 work["miller_loop_shared"] if dom_name == "miller_loop_shared" else \
                 work["miller_loop_lane_pairs" if lp else "miller_loop"]

@@ -212,7 +212,7 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
     if (blocks > 0xffffffffull) return hipErrorInvalidValue;
     const size_t table_at = (blocks * wave_bytes() + 255) & ~(size_t)255;
     Workspace* ws = nullptr;
-    if ((e = acquire(d, which == 4 ? table_at + kSharedTableBytes : blocks * wave_bytes(), stream, &ws)) !=
+    if ((e = acquire(d, which == 4 ? table_at + kSharedTableAlloc : blocks * wave_bytes(), stream, &ws)) !=
         hipSuccess)
         return e;
     if (which == 4) {

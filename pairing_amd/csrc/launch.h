@@ -72,6 +72,10 @@ hipError_t launch_miller_loop_prepared(const uint64_t* p_aff, const uint64_t* pr
 constexpr int kSharedLineWords = 6 * 14;
 constexpr int kSharedTableLines = 64;   // byte offset of line 0 (word 0: infinity flag)
 constexpr size_t kSharedTableBytes = kSharedTableLines + 68 * kSharedLineWords * 4;
+// what the generated shared kernel may read: it stages the lines into LDS as
+// 45 rows of 512 bytes (tools/pgen/kcfg.py MillerLoopSharedCfg.pre_exec)
+constexpr size_t kSharedTableAlloc = kSharedTableLines + 45 * 512;
+static_assert(kSharedTableAlloc >= kSharedTableBytes, "staging rows cover the table");
 hipError_t launch_shared_line_table(const uint64_t* prepared, uint32_t* table, hipStream_t stream);
 hipError_t launch_miller_loop_shared_gen(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out, size_t n,
                                          hipStream_t stream);

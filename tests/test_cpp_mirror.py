@@ -57,4 +57,4 @@ def test_cpp_engine_suite_on_gpu(oracle, tmp_path):
     r = subprocess.run([exe, data], capture_output=True, text=True, timeout=600)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count("ok  ") == 9
+    assert r.stdout.count("ok  ") == 10   # tests/cpp/test_engine.cpp main(): ten suites

@@ -114,6 +114,8 @@ class Emitter:
         self.code = []
         self.nlabel = 0
         self.NV, self.NA, self.NL = STORAGE[prog.lanes]
+        if getattr(cfg, "nl", None) is not None:
+            self.NL = cfg.nl
         self.vslot = [None] * self.NV       # ValState or None
         self.aslot = [None] * self.NA       # owner: ("val", vs) | ("var", name) | None
         self.lslot = [None] * self.NL
@@ -1217,14 +1219,22 @@ class Emitter:
         elif k == "load_raw":
             self.cfg.emit_load(self, op.imm, d)
         elif k == "tload":
-            # every lane reads the same 56 bytes (one cache line request per
-            # load); the value is used after the line's other loads are issued,
-            # so the wait is a counted one at its first use (self.pending)
+            # every lane reads the same 56 bytes -- from the wave's LDS copy of
+            # the table (a broadcast read; v17 = the line's LDS offset) or from
+            # global memory (one cache line request per load); the value is
+            # used after the line's other loads are issued, so the wait is a
+            # counted one at its first use (self.pending)
             for j in range(7):
-                self.i("global_load_dwordx2_s", d + 2 * j, ZERO, S(S_LINE), NL * 4 * op.imm + 8 * j)
+                if getattr(self.cfg, "lds_table", False):
+                    self.i("ds_read_b64", d + 2 * j, ZERO, NL * 4 * op.imm + 8 * j)
+                else:
+                    self.i("global_load_dwordx2_s", d + 2 * j, ZERO, S(S_LINE), NL * 4 * op.imm + 8 * j)
         elif k == "tnext":
-            self.i("s_add_u32", S(S_LINE), S(S_LINE), K(LINE_BYTES))
-            self.i("s_addc_u32", S(S_LINE + 1), S(S_LINE + 1), K(0))
+            if getattr(self.cfg, "lds_table", False):
+                self.i("v_add_u32", ZERO, K(LINE_BYTES), ZERO)
+            else:
+                self.i("s_add_u32", S(S_LINE), S(S_LINE), K(LINE_BYTES))
+                self.i("s_addc_u32", S(S_LINE + 1), S(S_LINE + 1), K(0))
         elif k == "store_raw":
             self.cfg.emit_store(self, op.imm, base[0])
         else:
@@ -1245,7 +1255,8 @@ class Emitter:
             self.vslot[kk] = dvs
             dvs.locs = {("V", kk)}
             if k == "tload":
-                self.pending[kk] = ("M", self.vm_issued)
+                self.pending[kk] = (("L", self.lgkm_issued) if getattr(self.cfg, "lds_table", False)
+                                    else ("M", self.vm_issued))
             if self.debug and k != "tload":   # a table load lands at its counted wait
                 self.i("mark", dst.id, self.vbase(kk))
             if not dvs.uses:

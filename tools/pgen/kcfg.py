@@ -40,6 +40,7 @@ class KernelCfg:
             i(("s_lshl_b32", S(S_ARG + 6), S(S_ARG + 6), K(1)))   # 2n active lanes
             i(("s_mov_b32", S(S_ODD), K(0xAAAAAAAA)))
             i(("s_mov_b32", S(S_ODD + 1), K(0xAAAAAAAA)))
+        self.pre_exec(em, code)
         i(("v_cmp_gt_u32", S(S_ARG + 6), GID))
         i(("s_and_saveexec_b64", S(S_EXEC)))
         i(("long_cbranch_execz", end_label))
@@ -58,6 +59,13 @@ class KernelCfg:
 
     def prologue_masks(self, em, code):
         pass
+
+    def pre_exec(self, em, code):
+        """work every lane of the wave does before the lanes past n are masked off"""
+        pass
+
+    nl = None          # LDS spill slots of this kernel (None: emit.STORAGE)
+    extra_lds = 0      # LDS bytes behind the spill slots (a staged table)
 
     def lane_addr(self, code, arg, stride, delta=0):
         """v[12:13] = arg + (pairing index) * stride + (lane role) * delta"""
@@ -209,12 +217,47 @@ class MillerLoopSharedCfg(MillerLoopCfg):
     miller_loop_shared_prog).  Arguments: p_aff (G1Affine records), table,
     out (Fq12), n, workspace.  The table (written by k_shared_line_table,
     kernels_pairing.hip) is u32 words: word 0 = Q's infinity flag, then from
-    byte TABLE_LINES the 68 lines of six 14-limb values, read at wave-uniform
-    addresses (emit.S_LINE, offset register v17 = 0)."""
+    byte TABLE_LINES the 68 lines of six 14-limb values (22 848 B).
+
+    LDS staging (default): every wave copies the lines into its LDS behind
+    its five spill slots before masking the lanes past n (45 coalesced 512-byte
+    rows), and the loop reads them with ds_read_b64 at a wave-uniform address
+    (v17 = the current line's LDS offset; all lanes read the same words, a
+    broadcast).  4 waves x (5 x 3584 + 23 040) B = 160 KiB per CU.
+    PGEN_MLS_LDS=0: read the table from global memory instead (wave-uniform
+    global_load_dwordx2 with v17 = 0 and the line pointer in s[96:97])."""
     name = "pa_gen_miller_loop_shared"
     records = {0: (0, 104, 0), 1: (0, 104, 48)}
     TABLE_LINES = 64
-    nsgpr = 98          # s[96:97]: the line pointer
+    TABLE_ROWS = 45                      # 45 x 512 B >= 68 x 336 B
+    nsgpr = 98          # s[96:97]: the line pointer (global form)
+
+    def __init__(self):
+        import os
+        self.lds_table = os.environ.get("PGEN_MLS_LDS", "1") == "1"
+        if self.lds_table:
+            self.nl = 5
+            self.extra_lds = 512 * self.TABLE_ROWS
+
+    def table_base(self):
+        return self.nl * gen_fl.NL * 4 * 64
+
+    def pre_exec(self, em, code):
+        if not self.lds_table:
+            return
+        i = code.append
+        # rows of 512 B (8 B per lane) from the global table into LDS, seven
+        # loads in flight at a time (v0..v13), offsets within 4 KiB of s[16:17]
+        for b0 in range(0, self.TABLE_ROWS, 7):
+            rows = range(b0, min(b0 + 7, self.TABLE_ROWS))
+            i(("s_add_u32", S(S_TMP), S(S_ARG + 2), K(self.TABLE_LINES + 512 * b0)))
+            i(("s_addc_u32", S(S_TMP + 1), S(S_ARG + 3), K(0)))
+            for k, r in enumerate(rows):
+                i(("global_load_dwordx2_s", 2 * k, LOFF, S(S_TMP), 512 * (r - b0)))
+            i(("s_waitcnt_vm0",))
+            for k, r in enumerate(rows):
+                i(("ds_write_b64", LOFF, 2 * k, self.table_base() + 512 * r))
+        i(("s_waitcnt_lgkm0",))
 
     def prologue_masks(self, em, code):
         i = code.append
@@ -229,8 +272,11 @@ class MillerLoopSharedCfg(MillerLoopCfg):
         i(("v_cmp_eq_u32", K(0), 0))
         i(("s_nop", 1))
         i(("s_mov_b64", S(S_VALID), S(106)))
-        i(("s_add_u32", S(S_LINE), S(S_ARG + 2), K(self.TABLE_LINES)))
-        i(("s_addc_u32", S(S_LINE + 1), S(S_ARG + 3), K(0)))
+        if self.lds_table:
+            i(("v_mov_b32", ZERO, K(self.table_base())))
+        else:
+            i(("s_add_u32", S(S_LINE), S(S_ARG + 2), K(self.TABLE_LINES)))
+            i(("s_addc_u32", S(S_LINE + 1), S(S_ARG + 3), K(0)))
 
 
 class MillerLoopCfg2(MillerLoopCfg):
@@ -268,5 +314,5 @@ def build(prog, cfg, debug=False):
     code.append(("label", end))
     code.append(("s_endpgm",))
     em.code = code
-    em.lds_bytes = len(em.lslot) * gen_fl.NL * 4 * 64
+    em.lds_bytes = len(em.lslot) * gen_fl.NL * 4 * 64 + cfg.extra_lds
     return code, em

@@ -419,10 +419,12 @@ class Sim:
         return None
 
 
-def run_lane(code, args, buffers, lane=0, max_steps=10 ** 9, trace=None, pair=False):
+def run_lane(code, args, buffers, lane=0, max_steps=10 ** 9, trace=None, pair=False, lds=None):
     """args: 5 u64 kernel arguments; buffers: {base_address: list of u64};
-    pair: simulate lanes (lane & ~1, lane | 1) together"""
+    pair: simulate lanes (lane & ~1, lane | 1) together; lds: {byte address:
+    u32} the wave's other lanes write (a table the whole wave stages)"""
     sm = Sim(code, lane, [lane & ~1, lane | 1] if pair else None)
+    sm.lds.update(lds or {})
     sm.trace = iter(trace) if trace is not None else None
     for base, words in buffers.items():
         for i, w in enumerate(words):

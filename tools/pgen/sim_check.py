@@ -31,6 +31,7 @@ def check(which, seed=5, lane=3, debug=True):
     rng = random.Random(seed)
     IN, OUT, AUX, WS = 0x100000, 0x200000, 0x300000, 0x400000
     pair = prog.lanes == 2
+    lds = {}
     if pair:   # lanes 2*lane, 2*lane+1 handle pairing `lane`
         sim_lane = 2 * lane
     else:
@@ -55,7 +56,14 @@ def check(which, seed=5, lane=3, debug=True):
         prec = [0] * (13 * lane) + words(ins) + [0]
         want = dsl.evaluate(prog, {0: ins[0], 1: ins[1], "lines": lines}, trace=trace)
         args = [IN, AUX, OUT, lane + 1, WS]
-        bufs = {IN: prec, AUX: kernels.shared_table_u64(lines, infinity=False)}
+        table = kernels.shared_table_u64(lines, infinity=False)
+        bufs = {IN: prec, AUX: table}
+        if getattr(cfg, "lds_table", False):
+            # the rows the other 63 lanes of the wave copy into LDS
+            t0 = cfg.TABLE_LINES // 8
+            for i, w in enumerate(table[t0:]):
+                lds[cfg.table_base() + 8 * i] = w & 0xffffffff
+                lds[cfg.table_base() + 8 * i + 4] = w >> 32
     else:
         # any field values (the loop does not care whether they are on the curve)
         ins = [rng.randrange(dsl.Q) for _ in range(6)]
@@ -65,7 +73,7 @@ def check(which, seed=5, lane=3, debug=True):
         args = [IN, AUX, OUT, lane + 1, WS]
         bufs = {IN: prec, AUX: qrec}
     t = time.time()
-    sm = sim.run_lane(code, args, bufs, lane=sim_lane, trace=trace if debug else None, pair=pair)
+    sm = sim.run_lane(code, args, bufs, lane=sim_lane, trace=trace if debug else None, pair=pair, lds=lds)
     got = []
     for k in sorted(want):
         base = OUT + 576 * lane + 48 * k
