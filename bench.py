@@ -63,8 +63,8 @@ ML_SHARED_BYTES = G1A_BYTES + FQ12_BYTES
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1 << 16, help="pairings per GPU per step")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="a fixed global batch split over the ranks (contiguous shards, every workload but "
@@ -606,6 +606,24 @@ def main():
                 t_ms.append(e[0].elapsed_time(e[1]))
                 m_ms.append(e[1].elapsed_time(e[2]))
             return float(np.mean(t_ms)), float(np.mean(m_ms))
+
+        def exact_ms(reps=3):
+            """the bit-exact form (the reference's table chain, wnaf_form and
+            wnaf_exp: pa_g1_wnaf_fixed_base_exact_device) on the same scalars,
+            untimed region, for comparison with the comb"""
+            w = int(pdev._lib.pa_g1_recommended_wnaf_for_num_scalars(n))
+            ws_x = pdev.wnaf_exact_workspace(1, n, w, False, dev)
+            out_x = pdev.empty_records(n, 18, dev)
+            t = []
+            for _ in range(reps):
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                e[0].record(stream)
+                pdev.wnaf_fixed_base_exact(1, base, scal, out_x, w, ws_x, stream)
+                e[1].record(stream)
+                torch.cuda.synchronize()
+                t.append(e[0].elapsed_time(e[1]))
+            del ws_x, out_x
+            return float(np.median(t))
     elif args.workload == "decode":
         # SURVEY.md §8 f rank 1: the verifier's front end -- compressed G1 and G2
         # records decoded with the on-curve (square root) and subgroup (r*P) checks
@@ -836,6 +854,7 @@ def main():
         elif args.workload == "wnaf":
             tot_ms, norm_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
             table_ms, mul_ms = comb_parts_ms()
+            x_ms = exact_ms()
             dom_name, dom_ms, dom_bytes = ("g1_glv_comb_mul", mul_ms, 32 + 144) if mul_ms >= norm_ms else \
                 ("g1_batch_normalize", norm_ms, 144 + 144)
             value = n_global * args.steps / elapsed
@@ -844,7 +863,8 @@ def main():
                       "batch_per_gpu": n, "global_batch": n_global,
                       "kernel_ms": {"table+fixed_base_mul (overlapped)": round(tot_ms, 3),
                                     "batch_normalize": round(norm_ms, 3),
-                                    "separately: glv table": round(table_ms, 3), "separately: glv mul": round(mul_ms, 3)}}
+                                    "separately: glv table": round(table_ms, 3), "separately: glv mul": round(mul_ms, 3),
+                                    "separately: bit-exact wnaf (reference chain, same scalars)": round(x_ms, 3)}}
         elif args.workload == "decode":
             g2_ms, g1_ms = float(np.mean(k_ms["a"])), float(np.mean(k_ms["b"]))
             dom_name, dom_ms, dom_bytes = ("g2_decode_compressed", g2_ms, 96 + 200 + 1) if g2_ms >= g1_ms else \

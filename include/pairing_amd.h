@@ -219,6 +219,35 @@ int pa_g2_batch_normalization(pa_g2 *v, size_t n);
  * pa_g1_wnaf_fixed_base); _window: the window given, 1..62 */
 int pa_g2_wnaf_fixed_base(const pa_g2 *base, const pa_fr_repr *scalars, size_t n, pa_g2 *out);
 int pa_g2_wnaf_fixed_base_window(const pa_g2 *base, const pa_fr_repr *scalars, size_t n, int window, pa_g2 *out);
+/* Bit-exact Wnaf (wnaf.rs:1-179): the reference's window table chain
+ * (wnaf_table, wnaf.rs:3-15), wnaf_form (:18-43) and wnaf_exp (:45-71), so the
+ * Jacobian X, Y, Z words equal the reference's -- not only the point, as the
+ * comb behind pa_g{1,2}_wnaf_fixed_base gives.  Slower than the comb (the
+ * table is 2^(w-1) Jacobian entries, the multiply 256 doublings per scalar).
+ * Fixed base: Wnaf::new().base(*base, num).scalar(scalars[i]) for every i
+ * (wnaf.rs:93-107, 169-178); window 1..20, or 0 for
+ * recommended_wnaf_for_num_scalars(n).  The table is rebuilt in parallel from
+ * the chain's closed form (kernels_wnaf_exact.hip); a base whose chain takes a
+ * special branch (outside G1) gets the serial chain. */
+int pa_g1_wnaf_fixed_base_exact(const pa_g1 *base, const pa_fr_repr *scalars, size_t n, int window, pa_g1 *out);
+int pa_g2_wnaf_fixed_base_exact(const pa_g2 *base, const pa_fr_repr *scalars, size_t n, int window, pa_g2 *out);
+/* Fixed scalar: Wnaf::new().scalar(*scalar).base(bases[i]) for every i
+ * (wnaf.rs:111-128, 156-166); window 1..12, or 0 for
+ * recommended_wnaf_for_scalar(*scalar) */
+int pa_g1_wnaf_fixed_scalar_exact(const pa_g1 *bases, size_t n, const pa_fr_repr *scalar, int window, pa_g1 *out);
+int pa_g2_wnaf_fixed_scalar_exact(const pa_g2 *bases, size_t n, const pa_fr_repr *scalar, int window, pa_g2 *out);
+/* device forms: `workspace` holds pa_wnaf_exact_workspace_bytes(group, n,
+ * window, fixed_scalar) bytes (window as resolved: 1..20 / 1..12; the fixed-
+ * scalar device form takes its window explicitly, its scalar being device memory) */
+size_t pa_wnaf_exact_workspace_bytes(int group, size_t n, int window, int fixed_scalar);
+int pa_g1_wnaf_fixed_base_exact_device(const pa_g1 *base, const pa_fr_repr *scalars, pa_g1 *out, size_t n,
+                                       int window, void *workspace, size_t workspace_bytes, void *stream);
+int pa_g2_wnaf_fixed_base_exact_device(const pa_g2 *base, const pa_fr_repr *scalars, pa_g2 *out, size_t n,
+                                       int window, void *workspace, size_t workspace_bytes, void *stream);
+int pa_g1_wnaf_fixed_scalar_exact_device(const pa_g1 *bases, size_t n, const pa_fr_repr *scalar, pa_g1 *out,
+                                         int window, void *workspace, size_t workspace_bytes, void *stream);
+int pa_g2_wnaf_fixed_scalar_exact_device(const pa_g2 *bases, size_t n, const pa_fr_repr *scalar, pa_g2 *out,
+                                         int window, void *workspace, size_t workspace_bytes, void *stream);
 /* CurveProjective::recommended_wnaf_for_scalar / _for_num_scalars
  * (lib.rs:166-174; G1 ec.rs:895-921, G2 ec.rs:1586-1612): the window the
  * reference's Wnaf would pick (returned as a positive int).  The GPU

@@ -421,6 +421,8 @@ template <> struct GroupAbi<1> {
     static constexpr auto mul_assign = &pa_g1_mul_assign_batch;
     static constexpr auto affine_mul = &pa_g1_affine_mul_batch;
     static constexpr auto fixed_base = &pa_g1_wnaf_fixed_base_window;
+    static constexpr auto fixed_base_exact = &pa_g1_wnaf_fixed_base_exact;
+    static constexpr auto fixed_scalar_exact = &pa_g1_wnaf_fixed_scalar_exact;
     static constexpr auto window_for_scalar = &pa_g1_recommended_wnaf_for_scalar;
     static constexpr auto window_for_count = &pa_g1_recommended_wnaf_for_num_scalars;
     static constexpr auto multiexp = &pa_g1_multiexp;
@@ -442,6 +444,8 @@ template <> struct GroupAbi<2> {
     static constexpr auto mul_assign = &pa_g2_mul_assign_batch;
     static constexpr auto affine_mul = &pa_g2_affine_mul_batch;
     static constexpr auto fixed_base = &pa_g2_wnaf_fixed_base_window;
+    static constexpr auto fixed_base_exact = &pa_g2_wnaf_fixed_base_exact;
+    static constexpr auto fixed_scalar_exact = &pa_g2_wnaf_fixed_scalar_exact;
     static constexpr auto window_for_scalar = &pa_g2_recommended_wnaf_for_scalar;
     static constexpr auto window_for_count = &pa_g2_recommended_wnaf_for_num_scalars;
     static constexpr auto multiexp = &pa_g2_multiexp;
@@ -690,13 +694,16 @@ inline Fq12 G2Affine::pairing_with(const G1Affine& other) const { return Bls12::
 // Wnaf::new_().base(g, num_scalars).scalar(s): fixed base (wnaf.rs:93-107,
 // 169-178); Wnaf::new_().scalar(s).base(g): fixed scalar (wnaf.rs:111-128,
 // 156-166); shared() hands a copy to another thread (wnaf.rs:131-154).  The
-// window is the reference's recommended_wnaf_* choice (window()), but the GPU
-// multiplies with a signed base-256 comb (fixed base) or the reference's
-// mul_assign (fixed scalar), so the resulting POINTS equal the reference's
-// (PartialEq, ec.rs:45-85) while Jacobian words may differ.  That includes
-// the reference's wnaf_form wrap (add_nocarry, wnaf.rs:30-35): for an odd repr
-// whose bits window..255 are all ones its digits spell s - 2^256, and so does
-// the product here (wnaf_wraps below; the fixed-base entries do it on device).
+// window is the reference's recommended_wnaf_* choice (window()).
+//   * fixed scalar: the reference's own table chain, wnaf_form and wnaf_exp on
+//     the GPU (pa_g{1,2}_wnaf_fixed_scalar_exact): Jacobian words identical;
+//   * fixed base: scalars() multiplies with the signed base-256 comb, so the
+//     POINTS equal the reference's (PartialEq, ec.rs:45-85) while Jacobian words
+//     may differ; scalars_exact() runs the reference's chain instead
+//     (pa_g{1,2}_wnaf_fixed_base_exact, bit-identical words, slower).
+// Both include the reference's wnaf_form wrap (add_nocarry, wnaf.rs:30-35):
+// for an odd repr whose bits window..255 are all ones its digits spell
+// s - 2^256, and so does the product here.
 //
 // wnaf_wraps(s, w): whether wnaf_form(s, w) wraps; t = 2^256 - s then.
 inline bool wnaf_wraps(const FrRepr& s, size_t window, FrRepr* t) {
@@ -722,6 +729,14 @@ public:
         return out;
     }
     P scalar(const FrRepr& s) const { return scalars({s})[0]; }
+    // bit-identical Jacobian words (window <= 20)
+    std::vector<P> scalars_exact(const std::vector<FrRepr>& s) const {
+        std::vector<P> out(s.size());
+        if (!s.empty())
+            check(P::Abi::fixed_base_exact(&base_.v, &s[0].v, s.size(), (int)window_, &out[0].v),
+                  "Wnaf::scalar (exact)");
+        return out;
+    }
 
 private:
     P base_;
@@ -737,11 +752,10 @@ public:
     }
     template <class P>
     std::vector<P> bases(const std::vector<P>& g) const {
-        FrRepr t;
-        const bool wraps = wnaf_wraps(s_, window_for<P>(s_), &t);
-        auto out = P::mul_assign_batch(g, std::vector<FrRepr>(g.size(), wraps ? t : s_));
-        if (wraps)
-            for (auto& r : out) r.negate();   // the digits spell s - 2^256 = -t
+        std::vector<P> out(g.size());
+        if (!g.empty())
+            check(P::Abi::fixed_scalar_exact(&g[0].v, g.size(), &s_.v, (int)window_for<P>(s_), &out[0].v),
+                  "Wnaf::base");
         return out;
     }
     template <class P>

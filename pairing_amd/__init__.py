@@ -35,6 +35,7 @@ __all__ = [
     "g1_eq", "g2_eq", "g1_double", "g2_double", "g1_add", "g2_add", "g1_add_mixed", "g2_add_mixed", "g1_negate", "g2_negate",
     "g1_sub", "g2_sub", "g1_into_affine", "g2_into_affine", "g1_into_projective", "g2_into_projective",
     "g2_batch_normalization", "g2_wnaf_fixed_base",
+    "g1_wnaf_fixed_base_exact", "g2_wnaf_fixed_base_exact", "g1_wnaf_fixed_scalar_exact", "g2_wnaf_fixed_scalar_exact",
     "g1_recommended_wnaf_for_scalar", "g2_recommended_wnaf_for_scalar",
     "g1_recommended_wnaf_for_num_scalars", "g2_recommended_wnaf_for_num_scalars",
 ]
@@ -277,6 +278,44 @@ def g1_wnaf_fixed_base(base, scalars, window=None):
     else:
         call("pa_g1_wnaf_fixed_base_window", ptr(b), ptr(s), s.shape[0], int(window), ptr(out))
     return out
+
+
+def _wnaf_exact(group, fixed_scalar, bases, scalars, window):
+    wj = W_G1 if group == 1 else W_G2
+    b = as_rows(bases, wj, "base" if not fixed_scalar else "bases")
+    s = as_rows(scalars, 4, "scalar" if fixed_scalar else "scalars")
+    n = b.shape[0] if fixed_scalar else s.shape[0]
+    out = np.empty((n, wj), np.uint64)
+    w = 0 if window is None else int(window)
+    if fixed_scalar:
+        call("pa_g%d_wnaf_fixed_scalar_exact" % group, ptr(b), n, ptr(s), w, ptr(out))
+    else:
+        call("pa_g%d_wnaf_fixed_base_exact" % group, ptr(b), ptr(s), n, w, ptr(out))
+    return out
+
+
+def g1_wnaf_fixed_base_exact(base, scalars, window=None):
+    """Wnaf::new().base(base, n).scalar(s_i) with the reference's exact table chain,
+    wnaf_form and wnaf_exp (wnaf.rs:1-179): Jacobian words bit-identical to the
+    reference's.  `window`: 1..20 (default recommended_wnaf_for_num_scalars(n))."""
+    return _wnaf_exact(1, False, base, scalars, window)
+
+
+def g2_wnaf_fixed_base_exact(base, scalars, window=None):
+    """G2 form of g1_wnaf_fixed_base_exact."""
+    return _wnaf_exact(2, False, base, scalars, window)
+
+
+def g1_wnaf_fixed_scalar_exact(bases, scalar, window=None):
+    """Wnaf::new().scalar(s).base(g_i) (wnaf.rs:111-128, 156-166) for every Jacobian
+    base, bit-identical Jacobian words.  `window`: 1..12 (default
+    recommended_wnaf_for_scalar(s))."""
+    return _wnaf_exact(1, True, bases, scalar, window)
+
+
+def g2_wnaf_fixed_scalar_exact(bases, scalar, window=None):
+    """G2 form of g1_wnaf_fixed_scalar_exact."""
+    return _wnaf_exact(2, True, bases, scalar, window)
 
 
 # ---- multi-pairing (SURVEY.md §8 f rank 2) and in-process multi-device ----

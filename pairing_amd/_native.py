@@ -156,6 +156,10 @@ for _g in (1, 2):
     for _op in ("add", "add_mixed", "eq"):
         _SIGS["pa_g%d_%s_batch_device" % (_g, _op)] = [_P, _P, _P, _N, _P]
     _SIGS["pa_g%d_recommended_wnaf_for_scalar" % _g] = [_P]
+    _SIGS["pa_g%d_wnaf_fixed_base_exact" % _g] = [_P, _P, _N, ctypes.c_int, _P]
+    _SIGS["pa_g%d_wnaf_fixed_scalar_exact" % _g] = [_P, _N, _P, ctypes.c_int, _P]
+    _SIGS["pa_g%d_wnaf_fixed_base_exact_device" % _g] = [_P, _P, _P, _N, ctypes.c_int, _P, _N, _P]
+    _SIGS["pa_g%d_wnaf_fixed_scalar_exact_device" % _g] = [_P, _N, _P, _P, ctypes.c_int, _P, _N, _P]
     _SIGS["pa_g%d_recommended_wnaf_for_num_scalars" % _g] = [_N]
 _SIGS.update({
     "pa_fq2_inverse_batch": [_P, _P, _P, _N],
@@ -185,6 +189,8 @@ _lib.pa_g2_fixed_base_workspace_words.restype = ctypes.c_size_t
 _lib.pa_last_error.restype = ctypes.c_char_p
 _lib.pa_multiexp_workspace_bytes.argtypes = [ctypes.c_int, _N]
 _lib.pa_multiexp_workspace_bytes.restype = ctypes.c_size_t
+_lib.pa_wnaf_exact_workspace_bytes.argtypes = [ctypes.c_int, _N, ctypes.c_int, ctypes.c_int]
+_lib.pa_wnaf_exact_workspace_bytes.restype = ctypes.c_size_t
 
 
 def version():

@@ -884,6 +884,109 @@ int pa_g1_wnaf_fixed_base_window(const pa_g1* base, const pa_fr_repr* scalars, s
     return download(out, dout, sizeof(pa_g1) * n);
 }
 
+// ---- bit-exact Wnaf (kernels_wnaf_exact.hip) ----
+namespace {
+// window 0 -> the reference's recommendation; else checked against the limit
+int wx_window(int window, int dflt, int max) { return window == 0 ? dflt : (window < 1 || window > max ? -1 : window); }
+
+int wx_host(int group, bool fixed_scalar, const void* base_or_bases, size_t n, const pa_fr_repr* s, size_t ns,
+            int window, void* out) {
+    if (n == 0) return PA_OK;
+    const size_t jb = group == 1 ? sizeof(pa_g1) : sizeof(pa_g2);
+    DevBuf db, ds, dw, dout;
+    int rc;
+    if ((rc = upload(db, base_or_bases, jb * (fixed_scalar ? n : 1))) ||
+        (rc = upload(ds, s, sizeof(pa_fr_repr) * ns)))
+        return rc;
+    const size_t bytes = fixed_scalar ? pa::wx_scalar_layout(group, n, window).bytes
+                                      : pa::wx_layout(group, n, window).bytes;
+    PA_TRY(dw.alloc(bytes), "device scratch");
+    PA_TRY(dout.alloc(jb * n), "device scratch");
+    if (fixed_scalar)
+        PA_TRY(pa::launch_wnaf_exact_fixed_scalar(group, db.as<uint64_t>(), n, ds.as<uint64_t>(), dout.as<uint64_t>(),
+                                                  window, dw.p, call_stream()),
+               "kernel launch");
+    else
+        PA_TRY(pa::launch_wnaf_exact_fixed_base(group, db.as<uint64_t>(), ds.as<uint64_t>(), dout.as<uint64_t>(), n,
+                                                window, dw.p, call_stream()),
+               "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
+    return download(out, dout, jb * n);
+}
+int wx_device(int group, bool fixed_scalar, const void* base_or_bases, size_t n, const pa_fr_repr* s, int window,
+              void* out, void* workspace, size_t workspace_bytes, void* stream) {
+    if (n == 0) return PA_OK;
+    if (!base_or_bases || !s || !out || !workspace) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const size_t need = fixed_scalar ? pa::wx_scalar_layout(group, n, window).bytes
+                                     : pa::wx_layout(group, n, window).bytes;
+    if (workspace_bytes < need) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf exact workspace too small");
+    if (fixed_scalar)
+        PA_TRY(pa::launch_wnaf_exact_fixed_scalar(group, (const uint64_t*)base_or_bases, n, (const uint64_t*)s,
+                                                  (uint64_t*)out, window, workspace, (hipStream_t)stream),
+               "kernel launch");
+    else
+        PA_TRY(pa::launch_wnaf_exact_fixed_base(group, (const uint64_t*)base_or_bases, (const uint64_t*)s,
+                                                (uint64_t*)out, n, window, workspace, (hipStream_t)stream),
+               "kernel launch");
+    return PA_OK;
+}
+}  // namespace
+
+int pa_g1_wnaf_fixed_base_exact(const pa_g1* base, const pa_fr_repr* scalars, size_t n, int window, pa_g1* out) {
+    if (n && (!base || !scalars || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const int w = wx_window(window, pa_g1_recommended_wnaf_for_num_scalars(n), pa::kWxMaxWindow);
+    if (w < 0) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range (exact: 1..20)");
+    return wx_host(1, false, base, n, scalars, n, w, out);
+}
+int pa_g2_wnaf_fixed_base_exact(const pa_g2* base, const pa_fr_repr* scalars, size_t n, int window, pa_g2* out) {
+    if (n && (!base || !scalars || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const int w = wx_window(window, pa_g2_recommended_wnaf_for_num_scalars(n), pa::kWxMaxWindow);
+    if (w < 0) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range (exact: 1..20)");
+    return wx_host(2, false, base, n, scalars, n, w, out);
+}
+int pa_g1_wnaf_fixed_scalar_exact(const pa_g1* bases, size_t n, const pa_fr_repr* scalar, int window, pa_g1* out) {
+    if (n && (!bases || !scalar || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const int w = n ? wx_window(window, pa_g1_recommended_wnaf_for_scalar(scalar), pa::kWxMaxScalarWindow) : 1;
+    if (w < 0) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range (exact fixed scalar: 1..12)");
+    return wx_host(1, true, bases, n, scalar, 1, w, out);
+}
+int pa_g2_wnaf_fixed_scalar_exact(const pa_g2* bases, size_t n, const pa_fr_repr* scalar, int window, pa_g2* out) {
+    if (n && (!bases || !scalar || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const int w = n ? wx_window(window, pa_g2_recommended_wnaf_for_scalar(scalar), pa::kWxMaxScalarWindow) : 1;
+    if (w < 0) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range (exact fixed scalar: 1..12)");
+    return wx_host(2, true, bases, n, scalar, 1, w, out);
+}
+size_t pa_wnaf_exact_workspace_bytes(int group, size_t n, int window, int fixed_scalar) {
+    const int max = fixed_scalar ? pa::kWxMaxScalarWindow : pa::kWxMaxWindow;
+    if ((group != 1 && group != 2) || window < 1 || window > max) return 0;
+    return fixed_scalar ? pa::wx_scalar_layout(group, n, window).bytes : pa::wx_layout(group, n, window).bytes;
+}
+int pa_g1_wnaf_fixed_base_exact_device(const pa_g1* base, const pa_fr_repr* scalars, pa_g1* out, size_t n,
+                                       int window, void* workspace, size_t workspace_bytes, void* stream) {
+    const int w = wx_window(window, pa_g1_recommended_wnaf_for_num_scalars(n), pa::kWxMaxWindow);
+    if (w < 0) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range (exact: 1..20)");
+    return wx_device(1, false, base, n, scalars, w, out, workspace, workspace_bytes, stream);
+}
+int pa_g2_wnaf_fixed_base_exact_device(const pa_g2* base, const pa_fr_repr* scalars, pa_g2* out, size_t n,
+                                       int window, void* workspace, size_t workspace_bytes, void* stream) {
+    const int w = wx_window(window, pa_g2_recommended_wnaf_for_num_scalars(n), pa::kWxMaxWindow);
+    if (w < 0) return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range (exact: 1..20)");
+    return wx_device(2, false, base, n, scalars, w, out, workspace, workspace_bytes, stream);
+}
+// the scalar is device memory here: the window must be given (1..12)
+int pa_g1_wnaf_fixed_scalar_exact_device(const pa_g1* bases, size_t n, const pa_fr_repr* scalar, pa_g1* out,
+                                         int window, void* workspace, size_t workspace_bytes, void* stream) {
+    if (window < 1 || window > pa::kWxMaxScalarWindow)
+        return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range (exact fixed scalar, device: 1..12)");
+    return wx_device(1, true, bases, n, scalar, window, out, workspace, workspace_bytes, stream);
+}
+int pa_g2_wnaf_fixed_scalar_exact_device(const pa_g2* bases, size_t n, const pa_fr_repr* scalar, pa_g2* out,
+                                         int window, void* workspace, size_t workspace_bytes, void* stream) {
+    if (window < 1 || window > pa::kWxMaxScalarWindow)
+        return fail(PA_ERR_INVALID_ARGUMENT, "wnaf window out of range (exact fixed scalar, device: 1..12)");
+    return wx_device(2, true, bases, n, scalar, window, out, workspace, workspace_bytes, stream);
+}
+
 // ---- device-resident variants ----
 int pa_g1_decode_batch_device(const uint8_t* enc, size_t n, int compressed, int checked, pa_g1_affine* out,
                               uint8_t* status, void* stream) {

@@ -1,0 +1,435 @@
+// Bit-exact Wnaf (wnaf.rs:1-179) for G1 and G2: the reference's table chain,
+// wNAF recoding and exponentiation, so the Jacobian X, Y, Z words equal the
+// reference's -- not only the point (the comb of kernels_curve.hip /
+// kernels_group.hip is equal as a point, PartialEq ec.rs:45-85).
+//
+// Fixed scalar (Wnaf::new().scalar(s).base(g), wnaf.rs:111-128, 156-166):
+//   k_wx_scalar_digits  wnaf_form of the one scalar (1 lane)
+//   k_wx_fixed_scalar   per lane: its base's window table (wnaf_table: the
+//                       2^(w-1) entries B, B + 2B, ... by add_assign) and
+//                       wnaf_exp over the shared digits
+// Fixed base (Wnaf::new().base(g, n).scalar(s_i), wnaf.rs:93-107, 169-178):
+//   the table T_k = T_(k-1) + D (D = B.double(), T_0 = B) is a serial chain in
+//   the reference.  With add-2007-bl (ec.rs:356-444) on T_(k-1) and D:
+//     H = U2 - U1 = Z1^2 Z_D^2 (x_D - x_(k-1)),  Z_k = 2 Z1 Z_D H
+//       = c_k Z_(k-1)^3,  c_k = 2 Z_D^3 (x_D - x_(k-1))
+//   (x = affine coordinates) and X_k = x_k Z_k^2, Y_k = y_k Z_k^3, since the
+//   formula's outputs represent T_k = (2k+1) B and field values are canonical.
+//   So the chain is rebuilt in parallel:
+//     k_wx_prep     D (the reference's doubling), x_D, 2 Z_D^3         (1 lane)
+//     k_wx_affine   affine (2k+1) B per lane (any addition chain)
+//     k_wx_coef     C_0 = Z_B, C_k = c_k
+//     k_wx_scan     log2(N) steps C_i <- C_i * C_(i-2^s)^(3^(2^s)): after
+//                   the last step C_k = Z_k (a Hillis-Steele scan over the
+//                   maps z -> c z^(3^e); exponents: wnaf_exact_consts.h)
+//     k_wx_finish   T_k = (x_k Z_k^2, y_k Z_k^3, Z_k), T_0 = B's own words
+//   The closed form needs the generic branch of every addition (T_(k-1) and
+//   D nonzero, x_(k-1) != x_D).  A base for which some step is special (zero,
+//   a point of small order: B outside G1) raises a flag in the workspace and
+//   k_wx_serial replays the reference's chain on one lane instead; both
+//   paths are stream-ordered, no host round trip.
+//   k_wx_fixed_base_mul  per scalar: wnaf_form into a digit-major scratch
+//                        column, then wnaf_exp over the table.
+#include "curve.h"
+#include "launch.h"
+#include "wnaf_exact_consts.h"
+
+namespace pa {
+namespace {
+
+template <int G> struct Wx;
+template <> struct Wx<1> {
+    using F = Fq;
+    static constexpr int W = 6;
+};
+template <> struct Wx<2> {
+    using F = Fq2;
+    static constexpr int W = 12;
+};
+
+inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// wnaf_form (wnaf.rs:18-43) of a 4 x u64 FrRepr for window <= kWxMaxWindow:
+// digit j to d[j * stride]; returns the count.  sub_noborrow / add_nocarry
+// wrap modulo 2^256 as the reference's do (wnaf.rs:30-35).
+PA_DEV int wnaf_digits(const uint64_t* s, int window, int32_t* d, size_t stride) {
+    uint64_t c0 = s[0], c1 = s[1], c2 = s[2], c3 = s[3];
+    const uint64_t mod_mask = (1ull << (window + 1)) - 1;
+    const int64_t half = (int64_t)1 << window;
+    int len = 0;
+    while ((c0 | c1 | c2 | c3) != 0) {
+        int64_t u = 0;
+        if (c0 & 1) {
+            u = (int64_t)(c0 & mod_mask);
+            if (u > half) u -= (int64_t)1 << (window + 1);
+            if (u > 0) {
+                const uint64_t t = (uint64_t)u;
+                const uint64_t b0 = c0 < t;
+                c0 -= t;
+                const uint64_t b1 = c1 < b0;
+                c1 -= b0;
+                const uint64_t b2 = c2 < b1;
+                c2 -= b1;
+                c3 -= b2;
+            } else {
+                const uint64_t t = (uint64_t)(-u);
+                c0 += t;
+                const uint64_t k0 = c0 < t;
+                c1 += k0;
+                const uint64_t k1 = k0 && c1 == 0;
+                c2 += k1;
+                const uint64_t k2 = k1 && c2 == 0;
+                c3 += k2;
+            }
+        }
+        d[(size_t)len * stride] = (int32_t)u;
+        len++;
+        c0 = (c0 >> 1) | (c1 << 63);
+        c1 = (c1 >> 1) | (c2 << 63);
+        c2 = (c2 >> 1) | (c3 << 63);
+        c3 >>= 1;
+    }
+    return len;
+}
+
+// wnaf_exp (wnaf.rs:45-71): entry e of the table at table + 3W estride e (u64),
+// digit j at d[j dstride]
+template <int G>
+PA_DEV void wnaf_exp(Jac<typename Wx<G>::F>& r, const uint64_t* table, size_t estride, const int32_t* d,
+                     size_t dstride, int len) {
+    using F = typename Wx<G>::F;
+    constexpr int JW = 3 * Wx<G>::W;
+    jac_zero(r);
+    bool found = false;
+    for (int j = len - 1; j >= 0; j--) {
+        if (found) jac_double(r);
+        const int32_t v = d[(size_t)j * dstride];
+        if (v != 0) {
+            found = true;
+            Jac<F> t;
+            load_jac(t, table + (size_t)JW * estride * (size_t)((v > 0 ? v : -v) / 2));
+            if (v > 0)
+                jac_add(r, t);
+            else
+                jac_sub(r, t);
+        }
+    }
+}
+
+// ---------------- fixed scalar ----------------
+__global__ void __launch_bounds__(64) k_wx_scalar_digits(const uint64_t* __restrict__ scalar, int window,
+                                                         int32_t* __restrict__ digits, int32_t* __restrict__ len) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) len[0] = wnaf_digits(scalar, window, digits, 1);
+}
+
+// tables: entry e of lane i at tables[(e n + i) JW] (entry-major, so a wave's
+// stores of one entry are adjacent records)
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_fixed_scalar(const uint64_t* __restrict__ bases, size_t n,
+                                                        const int32_t* __restrict__ digits,
+                                                        const int32_t* __restrict__ len, int window,
+                                                        uint64_t* __restrict__ tables, uint64_t* __restrict__ out) {
+    using F = typename Wx<G>::F;
+    constexpr int JW = 3 * Wx<G>::W;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    // wnaf_table (wnaf.rs:3-15)
+    Jac<F> base, dbl;
+    load_jac(base, bases + (size_t)JW * i);
+    dbl = base;
+    jac_double(dbl);
+    const size_t entries = (size_t)1 << (window - 1);
+    uint64_t* t = tables + (size_t)JW * i;
+    for (size_t e = 0; e < entries; e++) {
+        store_jac(t + (size_t)JW * n * e, base);
+        jac_add(base, dbl);
+    }
+    // wnaf_exp over this lane's entries (stride n) and the shared digits
+    Jac<F> r;
+    wnaf_exp<G>(r, t, n, digits, 1, len[0]);
+    store_jac(out + (size_t)JW * i, r);
+}
+
+// ---------------- fixed base: the table ----------------
+// meta (u64): [0, 3W) D, [3W, 4W) x_D, [4W, 5W) 2 Z_D^3, [5W] special-step flag
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_prep(const uint64_t* __restrict__ base, uint64_t* __restrict__ meta) {
+    using F = typename Wx<G>::F;
+    constexpr int W = Wx<G>::W;
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    Jac<F> b, d;
+    load_jac(b, base);
+    d = b;
+    jac_double(d);
+    store_jac(meta, d);
+    uint64_t flag = jac_is_zero(b) || jac_is_zero(d) ? 1 : 0;
+    if (!flag) {
+        Aff<F> a;
+        jac_to_affine(a, d);
+        F z3, k2;
+        sqr(z3, d.z);
+        mul(z3, z3, d.z);
+        dbl(k2, z3);
+        store(meta + 3 * W, a.x);
+        store(meta + 4 * W, k2);
+    }
+    meta[5 * W] = flag;
+}
+
+// affine (2k + 1) B for k < N (a plain double-and-add: affine values do not
+// depend on the chain)
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_affine(const uint64_t* __restrict__ base, size_t N,
+                                                  uint64_t* __restrict__ aff, uint64_t* __restrict__ meta) {
+    using F = typename Wx<G>::F;
+    constexpr int W = Wx<G>::W;
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    Jac<F> b, r;
+    load_jac(b, base);
+    const uint64_t m = 2 * (uint64_t)k + 1;
+    r = b;
+    for (int bit = 62 - __builtin_clzll(m); bit >= 0; bit--) {
+        jac_double(r);
+        if ((m >> bit) & 1) jac_add(r, b);
+    }
+    Aff<F> a;
+    jac_to_affine(a, r);
+    if (a.inf) meta[5 * W] = 1;
+    store(aff + (size_t)2 * W * k, a.x);
+    store(aff + (size_t)2 * W * k + W, a.y);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_coef(const uint64_t* __restrict__ base, const uint64_t* __restrict__ aff,
+                                                size_t N, uint64_t* __restrict__ coef, uint64_t* __restrict__ meta) {
+    using F = typename Wx<G>::F;
+    constexpr int W = Wx<G>::W;
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N || meta[5 * W]) return;
+    F c;
+    if (k == 0) {
+        load(c, base + 2 * W);   // Z_B
+    } else {
+        F xp, xd, k2;
+        load(xp, aff + (size_t)2 * W * (k - 1));
+        load(xd, meta + 3 * W);
+        load(k2, meta + 4 * W);
+        if (eq(xp, xd)) meta[5 * W] = 1;   // T_(k-1) = +-D: add_assign's special branch
+        sub(c, xd, xp);
+        mul(c, c, k2);
+    }
+    store(coef + (size_t)W * k, c);
+}
+
+// z^(3^(2^s)) with the reduced exponents of wnaf_exact_consts.h
+PA_DEV int top_bit(const uint64_t* e) {
+    for (int w = 5; w >= 0; w--)
+        if (e[w]) return 64 * w + 63 - __builtin_clzll(e[w]);
+    return -1;
+}
+PA_DEV void pow3(Fq& r, const Fq& z, int s) {
+    const uint64_t* e = PA_WX_E1[s];
+    one(r);
+    for (int b = top_bit(e); b >= 0; b--) {
+        sqr(r, r);
+        if ((e[b >> 6] >> (b & 63)) & 1) mul(r, r, z);
+    }
+}
+PA_DEV void pow3(Fq2& r, const Fq2& z, int s) {
+    // z^(e0 + e1 q) = z^e0 conj(z)^e1 (q = 3 mod 4: z^q = conj(z)), one run of squarings
+    const uint64_t* e0 = PA_WX_E2[s][0];
+    const uint64_t* e1 = PA_WX_E2[s][1];
+    Fq2 zc, zz;
+    zc.c0 = z.c0;
+    neg(zc.c1, z.c1);
+    mul(zz, z, zc);
+    one(r);
+    const int t0 = top_bit(e0), t1 = top_bit(e1);
+    for (int b = t0 > t1 ? t0 : t1; b >= 0; b--) {
+        sqr(r, r);
+        const bool x0 = (e0[b >> 6] >> (b & 63)) & 1, x1 = (e1[b >> 6] >> (b & 63)) & 1;
+        if (x0 && x1)
+            mul(r, r, zz);
+        else if (x0)
+            mul(r, r, z);
+        else if (x1)
+            mul(r, r, zc);
+    }
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_scan(const uint64_t* __restrict__ cin, uint64_t* __restrict__ cout,
+                                                size_t N, size_t off, int s, const uint64_t* __restrict__ meta) {
+    using F = typename Wx<G>::F;
+    constexpr int W = Wx<G>::W;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N || meta[5 * W]) return;
+    F v;
+    load(v, cin + (size_t)W * i);
+    if (i >= off) {
+        F p, t;
+        load(p, cin + (size_t)W * (i - off));
+        pow3(t, p, s);
+        mul(v, v, t);
+    }
+    store(cout + (size_t)W * i, v);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_finish(const uint64_t* __restrict__ base, const uint64_t* __restrict__ aff,
+                                                  const uint64_t* __restrict__ zs, size_t N,
+                                                  uint64_t* __restrict__ table, const uint64_t* __restrict__ meta) {
+    using F = typename Wx<G>::F;
+    constexpr int W = Wx<G>::W;
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N || meta[5 * W]) return;
+    uint64_t* t = table + (size_t)3 * W * k;
+    if (k == 0) {
+        for (int j = 0; j < 3 * W; j++) t[j] = base[j];   // T_0 = B, its own words
+        return;
+    }
+    F z, x, y, z2;
+    load(z, zs + (size_t)W * k);
+    load(x, aff + (size_t)2 * W * k);
+    load(y, aff + (size_t)2 * W * k + W);
+    sqr(z2, z);
+    mul(x, x, z2);
+    mul(z2, z2, z);
+    mul(y, y, z2);
+    store(t, x);
+    store(t + W, y);
+    store(t + 2 * W, z);
+}
+
+// the reference's chain itself, for bases whose chain takes a special branch
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_serial(const uint64_t* __restrict__ base, size_t N,
+                                                  uint64_t* __restrict__ table, const uint64_t* __restrict__ meta) {
+    using F = typename Wx<G>::F;
+    constexpr int W = Wx<G>::W;
+    if (blockIdx.x != 0 || threadIdx.x != 0 || !meta[5 * W]) return;
+    Jac<F> b, d;
+    load_jac(b, base);
+    d = b;
+    jac_double(d);
+    for (size_t k = 0; k < N; k++) {
+        store_jac(table + (size_t)3 * W * k, b);
+        jac_add(b, d);
+    }
+}
+
+// ---------------- fixed base: the multiply ----------------
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_fixed_base_mul(const uint64_t* __restrict__ table,
+                                                          const uint64_t* __restrict__ scalars, size_t n, int window,
+                                                          int32_t* __restrict__ digits, uint64_t* __restrict__ out) {
+    using F = typename Wx<G>::F;
+    constexpr int JW = 3 * Wx<G>::W;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int len = wnaf_digits(scalars + 4 * i, window, digits + i, n);
+    Jac<F> r;
+    wnaf_exp<G>(r, table, 1, digits + i, n, len);
+    store_jac(out + (size_t)JW * i, r);
+}
+
+template <int G>
+hipError_t wx_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n, int window,
+                         void* workspace, hipStream_t stream) {
+    constexpr int W = Wx<G>::W;
+    const size_t N = (size_t)1 << (window - 1);
+    WxLayout L = wx_layout(G, n, window);
+    char* ws = static_cast<char*>(workspace);
+    uint64_t* meta = reinterpret_cast<uint64_t*>(ws + L.meta);
+    uint64_t* table = reinterpret_cast<uint64_t*>(ws + L.table);
+    uint64_t* aff = reinterpret_cast<uint64_t*>(ws + L.aff);
+    uint64_t* c0 = reinterpret_cast<uint64_t*>(ws + L.c0);
+    uint64_t* c1 = reinterpret_cast<uint64_t*>(ws + L.c1);
+    int32_t* digits = reinterpret_cast<int32_t*>(ws + L.digits);
+    const unsigned gb = blocks_for(N, 64);
+    hipLaunchKernelGGL(k_wx_prep<G>, dim3(1), dim3(64), 0, stream, base, meta);
+    hipLaunchKernelGGL(k_wx_affine<G>, dim3(gb), dim3(64), 0, stream, base, N, aff, meta);
+    hipLaunchKernelGGL(k_wx_coef<G>, dim3(gb), dim3(64), 0, stream, base, aff, N, c0, meta);
+    int s = 0;
+    for (size_t off = 1; off < N; off <<= 1, s++) {
+        hipLaunchKernelGGL(k_wx_scan<G>, dim3(gb), dim3(64), 0, stream, c0, c1, N, off, s, meta);
+        uint64_t* t = c0;
+        c0 = c1;
+        c1 = t;
+    }
+    hipLaunchKernelGGL(k_wx_finish<G>, dim3(gb), dim3(64), 0, stream, base, aff, c0, N, table, meta);
+    hipLaunchKernelGGL(k_wx_serial<G>, dim3(1), dim3(64), 0, stream, base, N, table, meta);
+    if (n) hipLaunchKernelGGL(k_wx_fixed_base_mul<G>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table, scalars, n,
+                              window, digits, out);
+    (void)W;
+    return hipGetLastError();
+}
+
+template <int G>
+hipError_t wx_fixed_scalar(const uint64_t* bases, size_t n, const uint64_t* scalar, uint64_t* out, int window,
+                           void* workspace, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    WxLayout L = wx_scalar_layout(G, n, window);
+    char* ws = static_cast<char*>(workspace);
+    int32_t* digits = reinterpret_cast<int32_t*>(ws + L.digits);
+    int32_t* len = reinterpret_cast<int32_t*>(ws + L.meta);
+    uint64_t* tables = reinterpret_cast<uint64_t*>(ws + L.table);
+    hipLaunchKernelGGL(k_wx_scalar_digits, dim3(1), dim3(64), 0, stream, scalar, window, digits, len);
+    hipLaunchKernelGGL(k_wx_fixed_scalar<G>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, bases, n, digits, len,
+                       window, tables, out);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// workspace of the fixed-base path: meta, table, affine multiples, two scan
+// buffers, the digit columns of the n scalars
+WxLayout wx_layout(int group, size_t n, int window) {
+    const size_t W = group == 1 ? 6 : 12, N = (size_t)1 << (window - 1);
+    WxLayout L;
+    size_t at = 0;
+    L.meta = at;
+    at = align256(at + 8 * (5 * W + 1));
+    L.table = at;
+    at = align256(at + 8 * 3 * W * N);
+    L.aff = at;
+    at = align256(at + 8 * 2 * W * N);
+    L.c0 = at;
+    at = align256(at + 8 * W * N);
+    L.c1 = at;
+    at = align256(at + 8 * W * N);
+    L.digits = at;
+    at = align256(at + 4 * (size_t)kWxMaxDigits * n);
+    L.bytes = at;
+    return L;
+}
+// fixed scalar: digit count, the digits, a table of 2^(w-1) entries per base
+WxLayout wx_scalar_layout(int group, size_t n, int window) {
+    const size_t W = group == 1 ? 6 : 12, N = (size_t)1 << (window - 1);
+    WxLayout L{};
+    size_t at = 0;
+    L.meta = at;
+    at = align256(at + 8);
+    L.digits = at;
+    at = align256(at + 4 * (size_t)kWxMaxDigits);
+    L.table = at;
+    at = align256(at + 8 * 3 * W * N * n);
+    L.bytes = at;
+    return L;
+}
+
+hipError_t launch_wnaf_exact_fixed_base(int group, const uint64_t* base, const uint64_t* scalars, uint64_t* out,
+                                        size_t n, int window, void* workspace, hipStream_t stream) {
+    return group == 1 ? wx_fixed_base<1>(base, scalars, out, n, window, workspace, stream)
+                      : wx_fixed_base<2>(base, scalars, out, n, window, workspace, stream);
+}
+hipError_t launch_wnaf_exact_fixed_scalar(int group, const uint64_t* bases, size_t n, const uint64_t* scalar,
+                                          uint64_t* out, int window, void* workspace, hipStream_t stream) {
+    return group == 1 ? wx_fixed_scalar<1>(bases, n, scalar, out, window, workspace, stream)
+                      : wx_fixed_scalar<2>(bases, n, scalar, out, window, workspace, stream);
+}
+
+}  // namespace pa

@@ -185,4 +185,18 @@ hipError_t launch_fr_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* 
                         const uint64_t* exp, int exp_words, size_t n, hipStream_t stream);
 hipError_t launch_fr_mul_batch(const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, hipStream_t stream);
 
+// ---- bit-exact Wnaf (kernels_wnaf_exact.hip) ----
+constexpr int kWxMaxWindow = 20;         // fixed base: 2^19 table entries, int32 digits
+constexpr int kWxMaxScalarWindow = 12;   // fixed scalar: a table per base
+constexpr int kWxMaxDigits = 260;        // wnaf_form of a 256-bit repr: at most 257 digits
+struct WxLayout {
+    size_t meta, table, aff, c0, c1, digits, bytes;
+};
+WxLayout wx_layout(int group, size_t n, int window);
+WxLayout wx_scalar_layout(int group, size_t n, int window);
+hipError_t launch_wnaf_exact_fixed_base(int group, const uint64_t* base, const uint64_t* scalars, uint64_t* out,
+                                        size_t n, int window, void* workspace, hipStream_t stream);
+hipError_t launch_wnaf_exact_fixed_scalar(int group, const uint64_t* bases, size_t n, const uint64_t* scalar,
+                                          uint64_t* out, int window, void* workspace, hipStream_t stream);
+
 }  // namespace pa

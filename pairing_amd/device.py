@@ -272,3 +272,33 @@ def multiexp(group, bases, scalars, out, workspace, stream=None):
     call("pa_g%d_multiexp_device" % group, _dptr(bases, aw, "bases"), _dptr(scalars, 4, "scalars"),
          bases.shape[0], _dptr(out, jw, "out"), ctypes.c_void_p(workspace.data_ptr()), workspace.numel(),
          _stream_ptr(stream))
+
+
+def wnaf_exact_workspace(group, n, window, fixed_scalar, device):
+    """A device workspace for the bit-exact Wnaf device entries (window as resolved)."""
+    nbytes = int(_lib.pa_wnaf_exact_workspace_bytes(int(group), int(n), int(window), int(bool(fixed_scalar))))
+    if nbytes == 0:
+        raise ValueError("wnaf exact: group %r / window %r out of range" % (group, window))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def wnaf_fixed_base_exact(group, base, scalars, out, window, workspace, stream=None):
+    """Wnaf::new().base(base, n).scalar(s_i) with the reference's Jacobian words
+    (pa_g{1,2}_wnaf_fixed_base_exact_device); base (1, 18|36), scalars (n, 4)."""
+    jw = W_G1 if group == 1 else W_G2
+    n = scalars.shape[0]
+    _rows(out, n, "out")
+    call("pa_g%d_wnaf_fixed_base_exact_device" % group, _dptr(base, jw, "base"), _dptr(scalars, 4, "scalars"),
+         _dptr(out, jw, "out"), n, int(window), ctypes.c_void_p(workspace.data_ptr()), workspace.numel(),
+         _stream_ptr(stream))
+
+
+def wnaf_fixed_scalar_exact(group, bases, scalar, out, window, workspace, stream=None):
+    """Wnaf::new().scalar(s).base(g_i) with the reference's Jacobian words
+    (pa_g{1,2}_wnaf_fixed_scalar_exact_device); bases (n, 18|36), scalar (1, 4)."""
+    jw = W_G1 if group == 1 else W_G2
+    n = bases.shape[0]
+    _rows(out, n, "out")
+    call("pa_g%d_wnaf_fixed_scalar_exact_device" % group, _dptr(bases, jw, "bases"), n,
+         _dptr(scalar, 4, "scalar"), _dptr(out, jw, "out"), int(window), ctypes.c_void_p(workspace.data_ptr()),
+         workspace.numel(), _stream_ptr(stream))

@@ -358,6 +358,12 @@ static void curve_tests(int iters) {
         e.mul_assign(no_wrap);
         EXPECT(edge[1] == e);
         EXPECT(Wnaf::new_().scalar(all_ones).base(g) == neg_g);
+        // the reference's own chain (bit-exact words; Python suites compare the words)
+        auto exact = shared.scalars_exact(sc);
+        for (size_t k = 0; k < sc.size(); k++) EXPECT(exact[k] == fixed[k]);
+        auto exact_edge = shared.scalars_exact({all_ones, no_wrap});
+        EXPECT(exact_edge[0] == neg_g);
+        EXPECT(exact_edge[1] == e);
     }
 }
 
