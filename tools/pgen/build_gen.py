@@ -91,14 +91,16 @@ PROGRAMS = {
     # inversion (no longer loaded by gen_launch.hip; built only on request)
     "fen": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="norm"), kcfg.FinalExpCfg, "pa_gen_fe_norm"),
     "fei": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="inv"), kcfg.FinalExpCfg, "pa_gen_fe_inv"),
-    "ml2": _mk(lambda: kernels.miller_loop_prog(lanes=2), kcfg.MillerLoopCfg2, "pa_gen_miller_loop2"),
+    "ml2": _mk(__import__("tower2").two_pass(lambda: kernels.miller_loop_prog(lanes=2)), kcfg.MillerLoopCfg2,
+                "pa_gen_miller_loop2"),
     # one G2Prepared shared by the whole batch: the line table in place of G2 arithmetic
     "mls": _mk(kernels.miller_loop_shared_prog, kcfg.MillerLoopSharedCfg, "pa_gen_miller_loop_shared"),
     # test-only kernels (tools/pgen/unit_progs.py, tests/test_gen_units.py)
     "tdec": _mk(lambda: __import__("unit_progs").dec_prog(), kcfg.FinalExpCfg, "pa_gen_tdec"),
     "tunit": _mk(lambda: __import__("unit_progs").unit_prog(), kcfg.FinalExpCfg, "pa_gen_tunit"),
     "tdec2": _mk(lambda: __import__("unit_progs").dec_prog(lanes=2), kcfg.FinalExpCfg2, "pa_gen_tdec2"),
-    "fe2": _mk(lambda: kernels.final_exp_prog(lanes=2), kcfg.FinalExpCfg2, "pa_gen_final_exp2"),
+    "fe2": _mk(__import__("tower2").two_pass(lambda: kernels.final_exp_prog(lanes=2)), kcfg.FinalExpCfg2,
+                "pa_gen_final_exp2"),
     # lazy reduction (tower.TowerLazy): wide products, one reduction per output Fq
     # (measured slower; built only on request for A/B runs)
     "mlz": _mk(lambda: kernels.miller_loop_prog(lazy=True), kcfg.MillerLoopCfg, "pa_gen_miller_loop_lazy"),

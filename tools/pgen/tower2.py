@@ -10,7 +10,31 @@ both as the same two-term leaf sop(X, b, Z, b'), with b' = swap(b) and
 X = (a0 | a0), Z = (-a1 | a1) formed by selects.  Every field value equals
 the one-lane tower's (checked by dsl.evaluate against the C oracle).
 """
+import os
+
 from dsl import SUBCU
+
+PREP_REUSE = os.environ.get("PGEN_PREP_REUSE", "1") == "1"
+MUL2_USES = {}       # value id -> mul2 operand uses, from a first build (two_pass)
+MUL2_COUNT = None
+
+
+def two_pass(progf):
+    """build a lane-pair program twice: the first build counts how often each
+    value is a mul2 operand (value ids are deterministic), the second lets
+    mul2 form the (x, z) pair of the more used operand"""
+    global MUL2_USES, MUL2_COUNT
+
+    def f():
+        global MUL2_USES, MUL2_COUNT
+        MUL2_USES, MUL2_COUNT = {}, {}
+        progf()
+        MUL2_USES, MUL2_COUNT = MUL2_COUNT, None
+        try:
+            return progf()
+        finally:
+            MUL2_USES = {}
+    return f
 from tower import Tower
 
 
@@ -33,10 +57,35 @@ class Tower2(Tower):
         p = self.p
         return p.sel(a, p.neg(a))
 
+    def _prepped(self, a):
+        """a's operand pair (x, z) of mul2 is already formed in this block"""
+        memo = self.p.cur.__dict__.get("memo", {})
+        return ("swap", (a.id,), None) in memo
+
+    def _fits(self, a, b):
+        p = self.p
+        zu = max(p.neg_u(a), a.u)
+        if a.u * b.u + zu * b.u > 17:
+            return False
+        if p.use_norm:
+            zv = max(p.sub_bounds(p.sub_key(a))[1], a.vb)
+            return a.vb * b.vb + zv * b.vb <= 600
+        return True
+
     def mul2(self, a, b):
         p = self.p
         if SUBCU[a.u] * b.u > a.u * SUBCU[b.u]:
             a, b = b, a
+        # the (x, z) pair costs 56 instructions, the partner swap of b 14: let
+        # the operand whose pair is already formed be a -- or, neither being
+        # formed, the one more products will use (MUL2_USES, a first build's
+        # count) -- if the bounds allow
+        if PREP_REUSE and not self._prepped(a) and self._fits(b, a):
+            if self._prepped(b) or MUL2_USES.get(b.id, 0) > MUL2_USES.get(a.id, 0):
+                a, b = b, a
+        if MUL2_COUNT is not None:
+            MUL2_COUNT[a.id] = MUL2_COUNT.get(a.id, 0) + 1
+            MUL2_COUNT[b.id] = MUL2_COUNT.get(b.id, 0) + 1
         oa, ob = p.swap(a), p.swap(b)
         x = p.sel(a, oa)              # a0 on both lanes
         z = p.sel(p.neg(oa), a)       # -a1 | a1
