@@ -310,6 +310,13 @@ class Prog:
         assert self.lanes == 2
         return self._cse("swap", [a], a.u, vb=a.vb)
 
+    def dppadd(self, a, b, perm):
+        """lane r: b + a of lane perm[r] of the pair (one v_add_u32_dpp per limb,
+        quad_perm [perm0, perm1, perm0 + 2, perm1 + 2])"""
+        assert self.lanes == 2
+        self._full(a, b)
+        return self._cse("dppadd", [a, b], a.u + b.u, imm=tuple(perm), vb=a.vb + b.vb)
+
     def sel(self, a, b):
         """lane 0 takes a, lane 1 takes b"""
         assert self.lanes == 2
@@ -764,6 +771,8 @@ def evaluate(prog, inputs, stats=None, trace=None):
             r = [s[0][1 - ln] for ln in range(L)]
         elif k == "sel":
             r = [s[ln][ln] for ln in range(L)]
+        elif k == "dppadd":
+            r = [tuple(x + y for x, y in zip(s[0][op.imm[ln]], s[1][ln])) for ln in range(L)]
         elif k in ("wsop", "wnorm"):
             if k == "wsop":
                 st.bump("wsop%d" % (len(op.srcs) // 2))

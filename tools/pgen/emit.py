@@ -628,6 +628,11 @@ class Emitter:
         for i in range(NL):
             self.i("v_mov_b32_dpp_swap", d + i, a + i)
 
+    def emit_dppadd(self, a, b, d, perm):
+        self.i("s_nop", 1)   # VALU write -> DPP read of the same VGPR: 2 wait states
+        for i in range(NL):
+            self.i("v_add_u32_dpp", d + i, a + i, b + i, perm)
+
     def emit_sel(self, a, b, d):
         for i in range(NL):
             self.i("v_cndmask_b32_e64", d + i, a + i, b + i, S(S_ODD))
@@ -1151,7 +1156,7 @@ class Emitter:
             # in place over a dying source (safe for every op kind below)
             dk = None
             for vs, kk in zip(srcs, sk):
-                if (vs in dying and self.vslot[kk] is vs and k != "swap"
+                if (vs in dying and self.vslot[kk] is vs and k not in ("swap", "dppadd")
                         and not (k in ("sub", "csub") and op.srcs[0].id == op.srcs[1].id)):
                     dk = kk
                     break
@@ -1211,6 +1216,8 @@ class Emitter:
             self.emit_swap(base[0], d)
         elif k == "sel":
             self.emit_sel(base[0], base[1], d)
+        elif k == "dppadd":
+            self.emit_dppadd(base[0], base[1], d, op.imm)
         elif k == "selz":
             nt = op.imm
             self.emit_selz(base[:nt], base[nt], base[nt + 1], d)
@@ -1264,7 +1271,7 @@ class Emitter:
 
     # ---------------- prefetch ----------------
     COST = {"sop": None, "sqr": 460, "red": 62, "norm": 39, "add": 14, "add3": 14, "shladd": 14, "shl": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
-            "sel": 14, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14, "tload": 7, "tnext": 2,
+            "sel": 14, "dppadd": 15, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14, "tload": 7, "tnext": 2,
             "selz": 80, "binv": 33000}
     # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
     AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}

@@ -95,6 +95,10 @@ class Renderer:
             return ["v_cndmask_b32 %s, %s, %s, vcc" % (o[0], o[1], o[2])]
         if m == "v_cndmask_b32_e64":
             return ["v_cndmask_b32_e64 %s, %s, %s, %s" % (o[0], o[1], o[2], reg(a[3], True))]
+        if m == "v_add_u32_dpp":
+            q = a[3]
+            return ["v_add_u32_dpp %s, %s, %s quad_perm:[%d,%d,%d,%d] row_mask:0xf bank_mask:0xf" % (
+                o[0], o[1], o[2], q[0], q[1], q[0] + 2, q[1] + 2)]
         if m == "v_mov_b32_dpp_swap":
             return ["v_mov_b32_dpp %s, %s quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" % (o[0], o[1])]
         if m == "ds_write_b64":

@@ -194,6 +194,14 @@ class Sim:
                     for ln in self.lanes:
                         self.vf[ln][t[1]] = src[ln ^ 1] if (ln ^ 1) in src else 0
                     nxt = None
+                elif m == "v_add_u32_dpp":
+                    # lane ln reads src0 from lane (ln & ~1) | perm[ln & 1] of its pair
+                    src = {ln: self.vf[ln][t[2]] for ln in self.lanes}
+                    val = {ln: (src[(ln & ~1) | t[4][ln & 1]] + self.vf[ln][t[3]]) & 0xffffffff
+                           for ln in self.lanes}
+                    for ln in self.lanes:
+                        self.vf[ln][t[1]] = val[ln]
+                    nxt = None
                 else:
                     for ln in self.lanes:
                         self.lane, self.v, self.a = ln, self.vf[ln], self.af[ln]

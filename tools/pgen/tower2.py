@@ -15,6 +15,7 @@ import os
 from dsl import SUBCU
 
 PREP_REUSE = os.environ.get("PGEN_PREP_REUSE", "1") == "1"
+DPP_ADD = os.environ.get("PGEN_DPP_ADD", "1") == "1"
 MUL2_USES = {}       # value id -> mul2 operand uses, from a first build (two_pass)
 MUL2_COUNT = None
 
@@ -97,7 +98,10 @@ class Tower2(Tower):
         if a.u > 1:
             a = p.red(a)
         o = p.swap(a)
-        x = p.add(o, p.sel(a, o))     # a0 + a1 | 2 a0
+        if DPP_ADD:
+            x = p.dppadd(a, o, (0, 0))    # o + a0: a0 + a1 | 2 a0, one v_add_u32_dpp per limb
+        else:
+            x = p.add(o, p.sel(a, o))     # a0 + a1 | 2 a0
         y = p.sel(p.sub(a, o), a)     # a0 - a1 | a1
         return p.mul(x, y)
 
