@@ -91,7 +91,8 @@ PROGRAMS = {
     # inversion (no longer loaded by gen_launch.hip; built only on request)
     "fen": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="norm"), kcfg.FinalExpCfg, "pa_gen_fe_norm"),
     "fei": _mk(lambda: kernels.final_exp_prog(lazy="sq", split="inv"), kcfg.FinalExpCfg, "pa_gen_fe_inv"),
-    "ml2": _mk(__import__("tower2").two_pass(lambda: kernels.miller_loop_prog(lanes=2)), kcfg.MillerLoopCfg2,
+    "ml2": _mk(__import__("tower2").two_pass(lambda: kernels.miller_loop_prog(lanes=2), xi_dpp=False),
+                kcfg.MillerLoopCfg2,
                 "pa_gen_miller_loop2"),
     # one G2Prepared shared by the whole batch: the line table in place of G2 arithmetic
     "mls": _mk(kernels.miller_loop_shared_prog, kcfg.MillerLoopSharedCfg, "pa_gen_miller_loop_shared"),

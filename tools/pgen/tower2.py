@@ -18,23 +18,37 @@ PREP_REUSE = os.environ.get("PGEN_PREP_REUSE", "1") == "1"
 DPP_ADD = os.environ.get("PGEN_DPP_ADD", "1") == "1"
 MUL2_USES = {}       # value id -> mul2 operand uses, from a first build (two_pass)
 MUL2_COUNT = None
+SWAPPED = set()      # value ids whose partner swap a first build formed (outside xi)
+XI_DPP = True        # xi by dppadd (two_pass(xi_dpp=...): measured per kernel)
 
 
-def two_pass(progf):
+def two_pass(progf, xi_dpp=True):
     """build a lane-pair program twice: the first build counts how often each
     value is a mul2 operand (value ids are deterministic), the second lets
     mul2 form the (x, z) pair of the more used operand"""
     global MUL2_USES, MUL2_COUNT
 
     def f():
-        global MUL2_USES, MUL2_COUNT
-        MUL2_USES, MUL2_COUNT = {}, {}
-        progf()
-        MUL2_USES, MUL2_COUNT = MUL2_COUNT, None
+        global MUL2_USES, MUL2_COUNT, SWAPPED, XI_DPP
+        import dsl
+        XI_DPP = xi_dpp
+        MUL2_USES, MUL2_COUNT, SWAPPED = {}, {}, set()
+        seen = set()
+        swap0 = dsl.Prog.swap
+
+        def swap(self, a):
+            seen.add(a.id)
+            return swap0(self, a)
+        dsl.Prog.swap = swap
+        try:
+            progf()
+        finally:
+            dsl.Prog.swap = swap0
+        MUL2_USES, MUL2_COUNT, SWAPPED = MUL2_COUNT, None, seen
         try:
             return progf()
         finally:
-            MUL2_USES = {}
+            MUL2_USES, SWAPPED, XI_DPP = {}, set(), True
     return f
 from tower import Tower
 
@@ -49,8 +63,13 @@ class Tower2(Tower):
     def u2(self, a): return a.u
 
     def xi(self, a):
-        """(a0 - a1, a0 + a1): mine + (lane 0 ? -other : other)"""
+        """(a0 - a1, a0 + a1): mine + the partner's entry of conj(a) = (a0 | -a1),
+        one v_add_u32_dpp per limb"""
         p = self.p
+        # one v_add_u32_dpp per limb unless a's swap is formed anyway (by mul2 or
+        # sqr2 of a, counted by the first build of two_pass): then 3 ops over it
+        if DPP_ADD and XI_DPP and a.id not in SWAPPED:
+            return p.dppadd(self.conj2(a), a, (1, 0))
         o = p.swap(a)
         return p.add(a, p.sel(p.neg(o), o))
 
