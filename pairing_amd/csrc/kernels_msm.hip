@@ -35,6 +35,8 @@
 // the next part accumulates, so only the last part's tail is exposed.
 // Work: n*W mixed additions + ~2*W*2^(c-1) additions + ~256 doublings.
 
+#include <vector>
+
 #include "curve_fl.h"
 #include "curve_fl2.h"
 #include "dec_quad.h"
@@ -1363,7 +1365,22 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
     for (; made < nev; made++)
         if (!ck(hipEventCreateWithFlags(&ev[made], hipEventDisableTiming))) break;
     // ev[2q]: part q accumulated; ev[2q + 1]: part q reduced; ev[2 parts]: the upper Horner legs done
-    auto wlo = [&](uint32_t q) { return (uint32_t)(((uint64_t)p.W * (parts - 1 - q)) / parts); };
+    // part q covers windows [wlo(q), wlo(q - 1)); PA_MSM_WLO="b0,b1,..." (descending
+    // lower bounds, A/B of unequal parts) overrides the even split
+    static const std::vector<uint32_t> wlo_env = [] {
+        std::vector<uint32_t> v;
+        if (const char* e = getenv("PA_MSM_WLO"))
+            for (const char* c = e; *c;) {
+                v.push_back((uint32_t)strtoul(c, const_cast<char**>(&c), 10));
+                if (*c == ',') c++;
+                else break;
+            }
+        return v;
+    }();
+    auto wlo = [&](uint32_t q) {
+        if (wlo_env.size() + 1 == parts && q + 1 < parts && wlo_env[q] < p.W) return wlo_env[q];
+        return q + 1 == parts ? 0u : (uint32_t)(((uint64_t)p.W * (parts - 1 - q)) / parts);
+    };
     for (uint32_t q = 0; q < parts && err == hipSuccess; q++) {
         const uint32_t w1 = q == 0 ? p.W : wlo(q - 1), w0 = wlo(q);
         if (!ck(accumulate(w0, w1, s))) break;
