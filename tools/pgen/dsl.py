@@ -296,6 +296,15 @@ class Prog:
         assert a.vb <= VB_RED, "red value bound %d" % a.vb
         return self._cse("red", [a], 1, vb=1)
 
+    def norm_only(self, a):
+        """the carry pass whatever VN says (limbs back below 2^28, value bound
+        unchanged): for callers that check the bound their use needs"""
+        self._full(a)
+        assert self.use_norm and a.u <= 15
+        if a.u == 1:
+            return a
+        return self._cse("norm", [a], 1, vb=a.vb)
+
     def _cse(self, kind, srcs, u, imm=None, vb=None):
         """pure ops on the same operands in the same block are computed once"""
         memo = self.cur.__dict__.setdefault("memo", {})
@@ -333,7 +342,9 @@ class Prog:
     def var(self, name, u=1, home=None):
         # under norm a variable may hold a carry-normalized value (bound VN;
         # PGEN_VARVB overrides it for A/B); set() fully reduces anything larger
-        vb = int(os.environ.get("PGEN_VARVB", str(VN)))
+        # (lane pairs: 5, so that x + y of two variables stays within the Fq2
+        # squaring's product bound after a carry pass; tower2.Tower2.sqr2)
+        vb = int(os.environ.get("PGEN_VARVB", str(VN if self.lanes == 1 else 5)))
         self.vars[name] = Var(name, u, home, max(u, vb) if self.use_norm else u)
 
     def get(self, name):

@@ -27,6 +27,9 @@ class NormStop(Exception):
     args[0] is the Fq value the base-field inversion would invert"""
 
 
+KSQR_LAZY_XI = __import__("os").environ.get("PGEN_KSQR_LAZY_XI", "1") == "1"
+
+
 class Tower:
     # split final exponentiation (kernels.final_exp_prog(split=...)): "norm"
     # stops at the base-field value to invert (NormStop), "inv" reads its
@@ -220,7 +223,9 @@ class Tower:
             s = t.red2(t.add2(sx, t.xi(sy)))
             c = t.red2(t.sub2(sxy, t.add2(sx, sy)))
             if xi_on_cross:
-                c = t.red2(t.xi(c))
+                # carry-normalized programs leave xi(c) as it is: 3 c + 2 zy below
+                # is reduced anyway, and its bounds hold (checked by dsl.evaluate)
+                c = t.xi(c) if t.p.use_norm and KSQR_LAZY_XI else t.red2(t.xi(c))
             nz = t.red2(t.add2(t.dbl2(t.sub2(s, z)), s))
             nzy = t.red2(t.add2(t.dbl2(t.add2(c, zy)), c))
             return nz, nzy

@@ -16,6 +16,7 @@ from dsl import SUBCU
 
 PREP_REUSE = os.environ.get("PGEN_PREP_REUSE", "1") == "1"
 DPP_ADD = os.environ.get("PGEN_DPP_ADD", "1") == "1"
+SQR_NORM = os.environ.get("PGEN_SQR_NORM", "1") == "1"
 MUL2_USES = {}       # value id -> mul2 operand uses, from a first build (two_pass)
 MUL2_COUNT = None
 SWAPPED = set()      # value ids whose partner swap a first build formed (outside xi)
@@ -77,6 +78,11 @@ class Tower2(Tower):
         p = self.p
         return p.sel(a, p.neg(a))
 
+    def _sqr_fits(self, vb):
+        p = self.p
+        cv = p.sub_bounds((1, vb) if vb > 1 else 1)[1]
+        return 2 * vb * max(vb + cv, vb) <= 600
+
     def _prepped(self, a):
         """a's operand pair (x, z) of mul2 is already formed in this block"""
         memo = self.p.cur.__dict__.get("memo", {})
@@ -115,7 +121,12 @@ class Tower2(Tower):
         """lane 0: (a0 + a1)(a0 - a1); lane 1: 2 a0 a1"""
         p = self.p
         if a.u > 1:
-            a = p.red(a)
+            # a carry pass (value unchanged) where the product's value bound still
+            # holds for it: x = o + a0 has 2 vb, y = a - o about 2.2 vb + 1
+            if SQR_NORM and p.use_norm and a.u <= 15 and self._sqr_fits(a.vb):
+                a = p.norm_only(a)
+            else:
+                a = p.red(a)
         o = p.swap(a)
         if DPP_ADD:
             x = p.dppadd(a, o, (0, 0))    # o + a0: a0 + a1 | 2 a0, one v_add_u32_dpp per limb
