@@ -48,6 +48,9 @@ VALU_MAC_2WAVE_T = 29.12
 # one instruction per 4 clk (SQ: one ACTIVE_INST quad-cycle per instruction), at
 # the 2.33 GHz the chip holds under them (GRBM_GUI_ACTIVE, profiles/r02_cyc_probe.txt)
 ISSUE_PEAK_T = 1024 * 64 / 4 * 2.33e9 / 1e12
+# the same at the ~2.15 GHz two dense waves per SIMD leave (GRBM_GUI_ACTIVE per
+# dispatch, profiles/r05_coresidency.md): the lane-pair kernels' practical ceiling
+ISSUE_2WAVE_T = 1024 * 64 / 4 * 2.15e9 / 1e12
 FQ12_BYTES = 576
 G1A_BYTES, G2A_BYTES = 104, 200  # ABI records (coordinates + infinity flag + pad)
 # algorithmic HBM bytes per pairing, per kernel (DESIGN.md "Roofline")
@@ -978,7 +981,16 @@ def main():
                                  "unit": "T lane-instructions/s (one wave per SIMD)", "frac": rate / ISSUE_PEAK_T,
                                  "instructions_per_unit": instr}
             elif instr:
-                roof["instructions_per_unit"] = instr
+                # lane pairs: instructions of both lanes per pairing; the issue
+                # ceiling is the same one instruction per 4 clk per SIMD, but two
+                # dense waves per SIMD hold the clock at ~2.15 GHz instead of
+                # 2.33 (power cap, profiles/r05_coresidency.md)
+                rate = instr * n / (dom_ms * 1e-3) / 1e12
+                roof["issue"] = {"achieved": round(rate, 3), "peak": round(ISSUE_PEAK_T, 3),
+                                 "unit": "T lane-instructions/s (any waves per SIMD, at 2.33 GHz)",
+                                 "frac": rate / ISSUE_PEAK_T, "instructions_per_unit": instr,
+                                 "peak_at_two_wave_clock": round(ISSUE_2WAVE_T, 3),
+                                 "frac_at_two_wave_clock": rate / ISSUE_2WAVE_T}
         if args.workload == "wnaf" and dom_name == "g1_glv_comb_mul":
             # VALU bound: each mixed addition (madd-2007-bl, ec.rs:446-526) is
             # 7 products + 4 squarings on the lazy 28-bit core (fl_gen.h

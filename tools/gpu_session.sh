@@ -52,7 +52,7 @@ for step in "$@"; do
         profwnaf) run prof_wnaf 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_wnaf -o run -- python bench.py --workload wnaf --steps 3 --warmup 1 --no-cpu-baseline ;;
         profdec) run prof_dec 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dec -o run -- python bench.py --workload decode --steps 3 --warmup 1 --no-cpu-baseline ;;
         fqbench) run bench_fq 300 python bench.py --workload fq_mul --steps 20 --warmup 3 --no-cpu-baseline ;;
-        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         frbench_nc) run bench_fr 300 python bench.py --workload fr_mul --steps 20 --warmup 3 --no-cpu-baseline ;;
         proffq) run prof_fq 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fq -o run -- python bench.py --workload fq_mul --steps 10 --warmup 2 --no-cpu-baseline ;;
         pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline &&
@@ -84,7 +84,10 @@ for step in "$@"; do
         preptests) run pytest_prep 600 python -u -m pytest tests/test_bench_sizes.py tests/test_gpu_parity.py -m gpu -k "prepare or miller_loop" -x -v --timeout 300 --timeout-method thread ;;
         verifycpu) run bench_verify_cpu 300 python bench.py --workload verify --steps 10 --warmup 2 ;;
         allbench) run bench 600 python bench.py &&
+                  run bench_prepared 300 python bench.py --workload prepared --steps 20 --warmup 5 &&
+                  run bench_prepared_shared 300 python bench.py --workload prepared_shared --steps 20 --warmup 5 &&
                   run bench_verify_cpu 300 python bench.py --workload verify --steps 10 --warmup 2 &&
+                  run bench_verify_decode 300 python bench.py --workload verify --decode --steps 10 --warmup 2 &&
                   run bench_decode 300 python bench.py --workload decode --steps 5 --warmup 1 &&
                   run bench_msm 400 python bench.py --workload msm --steps 5 --warmup 1 &&
                   run bench_wnaf 300 python bench.py --workload wnaf --steps 5 --warmup 1 &&
