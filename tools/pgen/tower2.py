@@ -17,6 +17,7 @@ from dsl import SUBCU
 PREP_REUSE = os.environ.get("PGEN_PREP_REUSE", "1") == "1"
 DPP_ADD = os.environ.get("PGEN_DPP_ADD", "1") == "1"
 SQR_NORM = os.environ.get("PGEN_SQR_NORM", "1") == "1"
+PAIR_SUM = os.environ.get("PGEN_PAIR_SUM", "0") == "1"   # measured: more live pairs, more spills
 MUL2_USES = {}       # value id -> mul2 operand uses, from a first build (two_pass)
 MUL2_COUNT = None
 SWAPPED = set()      # value ids whose partner swap a first build formed (outside xi)
@@ -55,12 +56,25 @@ from tower import Tower
 
 
 class Tower2(Tower):
+    def __init__(self, p):
+        super().__init__(p)
+        self.sums = {}    # value id -> (a, b): the value is a + b (add2, or lim2 / red2 of such a sum)
+        self.pairs = {}   # (block, value id) -> mul2's operand pair (x, z) formed in that block
+
     # ---------------- distributed Fq2 ----------------
-    def add2(self, a, b): return self.p.add(a, b)
+    def add2(self, a, b):
+        r = self.p.add(a, b)
+        if PAIR_SUM:
+            self.sums[r.id] = (a, b)
+        return r
     def sub2(self, a, b): return self.p.sub(a, b)
     def neg2(self, a): return self.p.neg(a)
     def dbl2(self, a): return self.p.add(a, a)
-    def red2(self, a): return self.p.red(a)
+    def red2(self, a):
+        r = self.p.red(a)
+        if r is not a and a.id in self.sums:
+            self.sums[r.id] = self.sums[a.id]
+        return r
     def u2(self, a): return a.u
 
     def xi(self, a):
@@ -86,7 +100,51 @@ class Tower2(Tower):
     def _prepped(self, a):
         """a's operand pair (x, z) of mul2 is already formed in this block"""
         memo = self.p.cur.__dict__.get("memo", {})
-        return ("swap", (a.id,), None) in memo
+        return ("swap", (a.id,), None) in memo or (id(self.p.cur), a.id) in self.pairs
+
+    def _pair_direct(self, a):
+        p = self.p
+        oa = p.swap(a)
+        return p.sel(a, oa), p.sel(p.neg(oa), a)     # a0 on both lanes; -a1 | a1
+
+    def _summed(self, a):
+        """the pairs of a's summands, both formed already in this block, or None"""
+        s = self.sums.get(a.id) if PAIR_SUM else None
+        if s is None or not all((id(self.p.cur), v.id) in self.pairs for v in s):
+            return None
+        return [self.pairs[(id(self.p.cur), v.id)] for v in s]
+
+    def _pair_cost(self, a):
+        if self._prepped(a):
+            return 0
+        return 28 if self._summed(a) is not None else 56
+
+    def _pair_fits(self, x, z, b):
+        p = self.p
+        if x.u * b.u + z.u * b.u > 17:
+            return False
+        return not p.use_norm or x.vb * b.vb + z.vb * b.vb <= 600
+
+    def pair(self, a, b):
+        """mul2's operand pair of a (against partner operand b): the pair of a
+        sum is the sum of its summands' pairs (x and z are linear in a) when
+        those are formed and the product's bounds hold -- 2 adds instead of a
+        swap, a negation and two selects"""
+        p = self.p
+        key = (id(p.cur), a.id)
+        if key in self.pairs:
+            return self.pairs[key]
+        s = self._summed(a)
+        r = None
+        if s is not None:
+            (x0, z0), (x1, z1) = s
+            x, z = p.add(x0, x1), p.add(z0, z1)
+            if self._pair_fits(x, z, b):
+                r = (x, z)
+        if r is None:
+            r = self._pair_direct(a)
+        self.pairs[key] = r
+        return r
 
     def _fits(self, a, b):
         p = self.p
@@ -106,15 +164,15 @@ class Tower2(Tower):
         # the operand whose pair is already formed be a -- or, neither being
         # formed, the one more products will use (MUL2_USES, a first build's
         # count) -- if the bounds allow
-        if PREP_REUSE and not self._prepped(a) and self._fits(b, a):
-            if self._prepped(b) or MUL2_USES.get(b.id, 0) > MUL2_USES.get(a.id, 0):
+        if PREP_REUSE and self._fits(b, a):
+            ca, cb = self._pair_cost(a), self._pair_cost(b)
+            if cb < ca or (cb == ca and cb and MUL2_USES.get(b.id, 0) > MUL2_USES.get(a.id, 0)):
                 a, b = b, a
         if MUL2_COUNT is not None:
             MUL2_COUNT[a.id] = MUL2_COUNT.get(a.id, 0) + 1
             MUL2_COUNT[b.id] = MUL2_COUNT.get(b.id, 0) + 1
-        oa, ob = p.swap(a), p.swap(b)
-        x = p.sel(a, oa)              # a0 on both lanes
-        z = p.sel(p.neg(oa), a)       # -a1 | a1
+        x, z = self.pair(a, b)
+        ob = p.swap(b)
         return p.sop(x, b, z, ob)     # lane 0: a0 b0 - a1 b1; lane 1: a0 b1 + a1 b0
 
     def sqr2(self, a):
@@ -139,7 +197,7 @@ class Tower2(Tower):
         return self.p.mul(a, b)       # b replicated
 
     def lim2(self, a):
-        return a if a.u <= 2 else self.p.red(a)
+        return a if a.u <= 2 else self.red2(a)
 
     def const2(self, c):
         p = self.p
