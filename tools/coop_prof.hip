@@ -8,18 +8,21 @@
 #include <vector>
 
 static void report(const char* what, float ms) {
-    unsigned long long h[8][3];
+    unsigned long long h[8][3], wk[8];
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(pa::g_coop_prof), sizeof h);
+    (void)hipMemcpyFromSymbol(wk, HIP_SYMBOL(pa::g_coop_prof_work), sizeof wk);
     const char* names[8] = {"LIN", "P1", "P2", "SQ", "INV", "LC", "k6", "k7"};
     unsigned long long tot = 0;
     for (int k = 0; k < 8; k++) tot += h[k][0];
     printf("%s: %.3f ms, %llu profiled cycles\n", what, ms, tot);
     for (int k = 0; k < 8; k++)
         if (h[k][1])
-            printf("  %-4s steps %6llu  cycles/step %8.0f  lanes/step %5.1f  share %5.1f%%\n", names[k], h[k][1],
-                   (double)h[k][0] / h[k][1], (double)h[k][2] / h[k][1], 100.0 * h[k][0] / tot);
-    unsigned long long z[8][3] = {};
+            printf("  %-4s steps %6llu  cycles/step %8.0f  (lane 0's own work %6.0f)  lanes/step %5.1f  share %5.1f%%\n",
+                   names[k], h[k][1], (double)h[k][0] / h[k][1], (double)wk[k] / h[k][1], (double)h[k][2] / h[k][1],
+                   100.0 * h[k][0] / tot);
+    unsigned long long z[8][3] = {}, zw[8] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(pa::g_coop_prof), z, sizeof z);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(pa::g_coop_prof_work), zw, sizeof zw);
 }
 
 int main() {
