@@ -55,6 +55,40 @@ def gather_rows_to_root(local, n_global, root=0, group=None):
     return torch.cat([bufs[r][:sizes[r]] for r in range(world)], dim=0)
 
 
+class RowGatherer:
+    """gather_rows_to_root with preallocated buffers in `slots` rotating sets,
+    so that the gather of one batch can run asynchronously (RCCL's stream, or
+    gloo's thread) while the next batch computes into another output buffer.
+    gather(local, slot) returns the collective's work handle; the caller
+    waits on it before it writes `local` again."""
+
+    def __init__(self, n_global, width, like, root=0, group=None, slots=2):
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.root, self.group = root, group
+        self.sizes = [b - a for a, b in (shard_range(n_global, self.world, r) for r in range(self.world))]
+        self.cap = max(self.sizes)
+        mk = lambda: torch.empty((self.cap, width), dtype=like.dtype, device=like.device)  # noqa: E731
+        self.send = [mk() for _ in range(slots)] if self.sizes[self.rank] < self.cap else None
+        self.recv = [[mk() for _ in range(self.world)] for _ in range(slots)] if self.rank == root else None
+
+    def gather(self, local, slot=0, async_op=True):
+        if local.shape[0] != self.sizes[self.rank]:
+            raise ValueError("rank %d holds %d rows, shard is %d" % (self.rank, local.shape[0], self.sizes[self.rank]))
+        send = local
+        if self.send is not None:
+            send = self.send[slot]
+            send[:local.shape[0]].copy_(local)
+        bufs = self.recv[slot] if self.recv is not None else None
+        return dist.gather(send.contiguous(), bufs, dst=self.root, group=self.group, async_op=async_op)
+
+    def result(self, slot=0):
+        """the (n_global, w) rows of a finished gather, on root (None elsewhere)"""
+        if self.recv is None:
+            return None
+        return torch.cat([self.recv[slot][r][:self.sizes[r]] for r in range(self.world)], dim=0)
+
+
 def sharded_batch_from(load, n, compute, root=0, group=None):
     """out[i] over a global batch of n pairings, sharded across ranks, where
     each rank stages ONLY its own shard: load(start, stop) -> (p_shard,

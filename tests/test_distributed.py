@@ -237,3 +237,44 @@ def test_sharded_other_batches_world2_gloo(tmp_path, oracle, n):
     # shard's Jacobian words may differ from the whole batch's: equal as points
     assert oracle.g1_eq(u(r["wnaf"]), oracle.g1_wnaf_fixed_base(r["base"], r["s"])).all()
     assert oracle.g1_eq(u(r["msm"]), oracle.g1_multiexp(r["bases"], r["s"])).all()
+
+
+def _gather_worker(rank, world, port, n_global, result_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pairing_amd.shard import RowGatherer
+    a, b = shard_range(n_global, world, rank)
+    outs = [torch.empty((b - a, 5), dtype=torch.int64) for _ in range(2)]
+    g = RowGatherer(n_global, 5, outs[0])
+    works, got = [None, None], []
+    # the bench's pattern: batch k in slot k % 2, its gather asynchronous, the
+    # slot rewritten only after its gather finished
+    for k in range(5):
+        slot = k % 2
+        if works[slot] is not None:
+            works[slot].wait()
+            if rank == 0:
+                got.append(g.result(slot).clone())
+        outs[slot].copy_(torch.arange(a, b, dtype=torch.int64).view(-1, 1) * 10 + k)
+        works[slot] = g.gather(outs[slot], slot)
+    for slot in (1, 0):      # batches 3 and 4 still outstanding: 3 sits in slot 1
+        works[slot].wait()
+        if rank == 0:
+            got.append(g.result(slot).clone())
+    if rank == 0:
+        torch.save(torch.stack(got), result_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_global", [8, 7])
+def test_row_gatherer_async_double_buffered(tmp_path, n_global):
+    """bench.py's multi-GPU pairing step: double-buffered results, each batch's
+    gather to rank 0 asynchronous (RowGatherer), ragged shards padded"""
+    out = str(tmp_path / "g.pt")
+    mp.spawn(_gather_worker, args=(2, _free_port(), n_global, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    rows = torch.arange(n_global, dtype=torch.int64).view(-1, 1) * 10
+    for k in range(5):
+        assert torch.equal(got[k], (rows + k).expand(-1, 5)), k
