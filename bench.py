@@ -958,7 +958,8 @@ def main():
             roof["frac_of_copy"] = achieved / copy_gbs
         work_path = os.path.join(ROOT, "pairing_amd", "lib", "pa_gen_work.json")
         if args.workload == "pairing" or (args.workload in ("prepared", "prepared_shared") and
-                                          dom_name in ("final_exponentiation", "miller_loop_shared")):
+                                          dom_name in ("final_exponentiation", "miller_loop_shared",
+                                                       "miller_loop_prepared")):
             _check_work_json(work_path)
             # the pairing kernels are VALU-issue bound (multiply-accumulate
             # chains), not HBM bound: report that roofline, with the HBM view
@@ -977,7 +978,7 @@ def main():
             lp = kernel_variant_label(n) == "gen2" and (args.workload == "pairing" or
                                                         dom_name == "final_exponentiation")
             wk = work["final_exp_lane_pairs" if lp else "final_exp"] if dom_name == "final_exponentiation" else \
-                work["miller_loop_shared"] if dom_name == "miller_loop_shared" else \
+                work[dom_name] if dom_name in ("miller_loop_shared", "miller_loop_prepared") else \
                 work["miller_loop_lane_pairs" if lp else "miller_loop"]
             if lp:
                 roof_kernel = {"final_exponentiation": "pa_gen_final_exp2",

@@ -82,6 +82,14 @@ hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t
     if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s, coop_vm());
     return pa::launch_miller_loop_gen(gen_lanes(n), p, q, out, n, s);
 }
+// Miller loop of (P_i, G2Prepared_i) pairs: the generated kernel (tools/pgen
+// miller_loop_prepared_prog); PA_ML_PREPARED=hipcc selects round 4's HIP C++
+// kernel (kernels_pairing.hip) for A/B runs
+hipError_t mlp_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
+    static const bool hipcc = getenv("PA_ML_PREPARED") && strcmp(getenv("PA_ML_PREPARED"), "hipcc") == 0;
+    if (hipcc) return pa::launch_miller_loop_prepared(p, q, out, n, s);
+    return pa::launch_miller_loop_prepared_gen(p, q, out, n, s);
+}
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s, coop_vm());
     return pa::launch_final_exp_gen(gen_lanes(n), in, out, ok, n, s);
@@ -448,7 +456,7 @@ int pa_miller_loop_batch(const pa_g1_affine* p, const pa_g2_prepared* q, pa_fq12
     if ((rc = upload(dp, p, sizeof(pa_g1_affine) * n)) || (rc = upload(dq, q, sizeof(pa_g2_prepared) * n)))
         return rc;
     PA_TRY(dout.alloc(576 * n), "device scratch");
-    PA_TRY(pa::launch_miller_loop_prepared(dp.as<uint64_t>(), dq.as<uint64_t>(), dout.as<uint64_t>(), n, call_stream()),
+    PA_TRY(mlp_launch(dp.as<uint64_t>(), dq.as<uint64_t>(), dout.as<uint64_t>(), n, call_stream()),
            "kernel launch");
     PA_TRY(call_sync(), "kernel execution");
     return download(out, dout, 576 * n);
@@ -486,7 +494,7 @@ int pa_multi_miller_loop(const pa_g1_affine* p, const pa_g2_prepared* q, size_t 
         return rc;
     PA_TRY(dwork.alloc(576 * n), "device scratch");
     PA_TRY(dout.alloc(576), "device scratch");
-    PA_TRY(pa::launch_miller_loop_prepared(dp.as<uint64_t>(), dq.as<uint64_t>(), dwork.as<uint64_t>(), n, call_stream()),
+    PA_TRY(mlp_launch(dp.as<uint64_t>(), dq.as<uint64_t>(), dwork.as<uint64_t>(), n, call_stream()),
            "kernel launch");
     PA_TRY(pa::launch_fq12_product(dwork.as<uint64_t>(), n, dout.as<uint64_t>(), call_stream()), "kernel launch");
     PA_TRY(call_sync(), "kernel execution");
@@ -1081,7 +1089,7 @@ int pa_g2_prepare_batch_device(const pa_g2_affine* q, pa_g2_prepared* out, size_
 int pa_miller_loop_batch_device(const pa_g1_affine* p, const pa_g2_prepared* q, pa_fq12* out, size_t n,
                                 void* stream) {
     if (n && (!p || !q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
-    PA_TRY(pa::launch_miller_loop_prepared((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n,
+    PA_TRY(mlp_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n,
                                            (hipStream_t)stream),
            "kernel launch");
     return PA_OK;

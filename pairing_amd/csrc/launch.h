@@ -79,6 +79,10 @@ static_assert(kSharedTableAlloc >= kSharedTableBytes, "staging rows cover the ta
 hipError_t launch_shared_line_table(const uint64_t* prepared, uint32_t* table, hipStream_t stream);
 hipError_t launch_miller_loop_shared_gen(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out, size_t n,
                                          hipStream_t stream);
+// the generated Miller loop of (P_i, G2Prepared_i) pairs (tools/pgen
+// MillerLoopPreparedCfg): each lane reads its own record's lines
+hipError_t launch_miller_loop_prepared_gen(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out,
+                                           size_t n, hipStream_t stream);
 // non-empty after a generated code object failed to load (names the file)
 const char* gen_error_detail();
 // The generated Miller-loop / final-exponentiation kernels (tools/pgen,

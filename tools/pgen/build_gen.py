@@ -96,6 +96,8 @@ PROGRAMS = {
                 "pa_gen_miller_loop2"),
     # one G2Prepared shared by the whole batch: the line table in place of G2 arithmetic
     "mls": _mk(kernels.miller_loop_shared_prog, kcfg.MillerLoopSharedCfg, "pa_gen_miller_loop_shared"),
+    # a G2Prepared per pairing (the north-star call): the lines read from each lane's record
+    "mlp": _mk(kernels.miller_loop_prepared_prog, kcfg.MillerLoopPreparedCfg, "pa_gen_miller_loop_prepared"),
     # test-only kernels (tools/pgen/unit_progs.py, tests/test_gen_units.py)
     "tdec": _mk(lambda: __import__("unit_progs").dec_prog(), kcfg.FinalExpCfg, "pa_gen_tdec"),
     "tunit": _mk(lambda: __import__("unit_progs").unit_prog(), kcfg.FinalExpCfg, "pa_gen_tunit"),
@@ -108,7 +110,7 @@ PROGRAMS = {
     "fez": _mk(lambda: kernels.final_exp_prog(lazy=True), kcfg.FinalExpCfg, "pa_gen_final_exp_lazy"),
 }
 FILES = {"small": "pa_gen_small.hsaco", "cyc": "pa_gen_cyc.hsaco", "ml": "pa_gen_miller_loop.hsaco", "fe": "pa_gen_final_exp.hsaco",
-         "mls": "pa_gen_miller_loop_shared.hsaco",
+         "mls": "pa_gen_miller_loop_shared.hsaco", "mlp": "pa_gen_miller_loop_prepared.hsaco",
          "fen": "pa_gen_fe_norm.hsaco", "fei": "pa_gen_fe_inv.hsaco",
          "ml2": "pa_gen_miller_loop2.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
          "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco",
@@ -157,14 +159,16 @@ def write_work_json(outdir):
     out = {}
     for key, name, nin in (("ml", "miller_loop", 6), ("fe", "final_exp", 12), ("fen", "fe_norm", 12),
                            ("fei", "fe_inv", 13), ("mls", "miller_loop_shared", 2),
+                           ("mlp", "miller_loop_prepared", 2),
                            ("ml2", "miller_loop_lane_pairs", 6), ("fe2", "final_exp_lane_pairs", 12)):
-        if key in ("fen", "fei", "mls", "ml2", "fe2") and not PROGRAMS[key].cache:
+        if key in ("fen", "fei", "mls", "mlp", "ml2", "fe2") and not PROGRAMS[key].cache:
             continue
         prog = PROGRAMS[key]()[0]
         st = dsl.Stats()
         ins = {k: rng.randrange(dsl.Q) for k in range(nin)}
-        if key == "mls":
-            ins["lines"] = kernels.shared_table_lines([[rng.randrange(dsl.Q) for _ in range(6)] for _ in range(68)])
+        if key in ("mls", "mlp"):
+            coeffs = [[rng.randrange(dsl.Q) for _ in range(6)] for _ in range(68)]
+            ins["lines"] = (kernels.shared_table_lines if key == "mls" else kernels.prepared_table_lines)(coeffs)
         dsl.evaluate(prog, ins, st)
         em = PROGRAMS[key].cache["r"][5]
         # instructions one lane executes (exact: the loop trip counts and branch
@@ -187,19 +191,19 @@ def main():
         del args[i:i + 2]
     os.makedirs(outdir, exist_ok=True)
     meta = {}
-    for w in args or ["ml", "fe", "ml2", "fe2", "mls"]:
+    for w in args or ["ml", "fe", "ml2", "fe2", "mls", "mlp"]:
         build(w, outdir)
         meta[w] = PROGRAMS[w].cache["r"][3]
     if "ml" in meta and "fe" in meta or "ml2" in meta and "fe2" in meta:
-        for k in ("ml", "fe", "ml2", "fe2", "mls"):
+        for k in ("ml", "fe", "ml2", "fe2", "mls", "mlp"):
             PROGRAMS[k]()   # every program the work file describes
         write_work_json(outdir)
-    if all(k in meta for k in ("ml", "fe", "ml2", "fe2", "mls")):
+    if all(k in meta for k in ("ml", "fe", "ml2", "fe2", "mls", "mlp")):
         hdr = os.path.join(ROOT, "pairing_amd", "csrc", "pa_gen_meta.h")
         with open(hdr, "w") as f:
             f.write("// GENERATED by tools/pgen/build_gen.py -- spill workspace per wave (M slots)\n#pragma once\n")
             for k, name in (("ml", "MILLER_LOOP"), ("fe", "FINAL_EXP"), ("ml2", "MILLER_LOOP2"), ("fe2", "FINAL_EXP2"),
-                            ("mls", "MILLER_LOOP_SHARED")):
+                            ("mls", "MILLER_LOOP_SHARED"), ("mlp", "MILLER_LOOP_PREPARED")):
                 f.write("#define PA_GEN_%s_MEM_SLOTS %d\n" % (name, meta[k]))
 
 

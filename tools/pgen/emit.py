@@ -133,6 +133,7 @@ class Emitter:
         self.weight = 1
         self.ensuring = None
         self.pending = {}            # V slot -> ("L" | "M", issue count after its last load)
+        self.split_pending = {}      # V slot -> True: raw record words, split when they land
         self.vm_issued = 0
         self.lgkm_issued = 0
         self.items = None            # the block being allocated (prefetch lookahead)
@@ -168,7 +169,7 @@ class Emitter:
 
     # ---------------- emission helpers ----------------
     VMEM = ("global_load_dwordx2", "global_load_dword", "global_store_dwordx2", "global_store_byte",
-            "global_store_dwordx2_s", "global_load_dwordx2_s")
+            "global_store_dwordx2_s", "global_load_dwordx2_s", "global_load_lds_dwordx4")
 
     def i(self, *t):
         self.code.append(t)
@@ -179,11 +180,11 @@ class Emitter:
         elif m.startswith("ds_"):
             self.lgkm_issued += 1
         elif m == "s_waitcnt_vm0":
-            self.pending = {k: v for k, v in self.pending.items() if v[0] != "M"}
+            self.retire_pending(lambda v: v[0] == "M")
             self.mstore = {}
             self.mem_stores_pending = False
         elif m == "s_waitcnt_lgkm0":
-            self.pending = {k: v for k, v in self.pending.items() if v[0] != "L"}
+            self.retire_pending(lambda v: v[0] == "L")
 
     def label(self):
         self.nlabel += 1
@@ -211,6 +212,16 @@ class Emitter:
                 return u
         return 1 << 30
 
+    def retire_pending(self, done):
+        """drop the pending entries done(entry) says have landed; a raw record
+        value (split_pending: a per-lane tload) is split into its limbs now"""
+        gone = [k for k, v in self.pending.items() if done(v)]
+        for k in gone:
+            del self.pending[k]
+        for k in gone:
+            if self.split_pending.pop(k, False):
+                self.cfg.emit_split(self, self.vbase(k))
+
     def wait_pending(self, slots=None):
         """complete the in-flight prefetches of the given V slots (default all),
         with counters that leave younger memory operations outstanding"""
@@ -222,20 +233,20 @@ class Emitter:
         if need["L"] is not None:
             n = min(15, self.lgkm_issued - need["L"])
             self.i("s_waitcnt_lgkm", n)
-            for k in [k for k, v in self.pending.items() if v[0] == "L" and v[1] <= self.lgkm_issued - n]:
-                del self.pending[k]
+            done = self.lgkm_issued - n
+            self.retire_pending(lambda v: v[0] == "L" and v[1] <= done)
         if need["M"] is not None:
             n = min(63, self.vm_issued - need["M"])
             self.i("s_waitcnt_vm", n)
-            for k in [k for k, v in self.pending.items() if v[0] == "M" and v[1] <= self.vm_issued - n]:
-                del self.pending[k]
+            done = self.vm_issued - n
+            self.retire_pending(lambda v: v[0] == "M" and v[1] <= done)
 
     def wait_vm_count(self, n):
         """s_waitcnt vmcnt(n); retire the tracked stores / prefetches it completes"""
         self.i("s_waitcnt_vm", n)
         done = self.vm_issued - n
         self.mstore = {k: q for k, q in self.mstore.items() if q > done}
-        self.pending = {k: v for k, v in self.pending.items() if v[0] != "M" or v[1] > done}
+        self.retire_pending(lambda v: v[0] == "M" and v[1] <= done)
 
     def untrack_stores(self):
         """control-flow merge / loop back edge: the static issue counts no longer
@@ -1225,6 +1236,10 @@ class Emitter:
             self.emit_binv(base[0], d, scratch)
         elif k == "load_raw":
             self.cfg.emit_load(self, op.imm, d)
+        elif k == "tload" and getattr(self.cfg, "per_lane_table", False):
+            self.cfg.emit_tload(self, op.imm, d)
+        elif k == "tnext" and getattr(self.cfg, "per_lane_table", False):
+            self.cfg.emit_tnext(self)
         elif k == "tload":
             # every lane reads the same 56 bytes -- from the wave's LDS copy of
             # the table (a broadcast read; v17 = the line's LDS offset) or from
@@ -1262,8 +1277,10 @@ class Emitter:
             self.vslot[kk] = dvs
             dvs.locs = {("V", kk)}
             if k == "tload":
-                self.pending[kk] = (("L", self.lgkm_issued) if getattr(self.cfg, "lds_table", False)
-                                    else ("M", self.vm_issued))
+                lds = getattr(self.cfg, "lds_table", False) or getattr(self.cfg, "per_lane_table", False)
+                self.pending[kk] = ("L", self.lgkm_issued) if lds else ("M", self.vm_issued)
+                if getattr(self.cfg, "per_lane_table", False):
+                    self.split_pending[kk] = True
             if self.debug and k != "tload":   # a table load lands at its counted wait
                 self.i("mark", dst.id, self.vbase(kk))
             if not dvs.uses:

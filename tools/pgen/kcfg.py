@@ -6,6 +6,8 @@ Kernel arguments (5 x 8 bytes, all kernels):
   miller_loop: p_aff (G1Affine, 13 u64), q_aff (G2Affine, 25 u64), out (Fq12, 72 u64), n, workspace
   final_exp:   in (Fq12), out (Fq12), ok (u8 per lane, may be null), n, workspace
 """
+import os
+
 import gen_fl
 from dsl import Q
 from emit import (A, ACC, ADDR, GID, K, LOFF, ORACC, S, S_ARG, S_EXEC, S_KARG, S_LINE, S_ODD, S_TMP, S_VALID,
@@ -277,6 +279,126 @@ class MillerLoopSharedCfg(MillerLoopCfg):
         else:
             i(("s_add_u32", S(S_LINE), S(S_ARG + 2), K(self.TABLE_LINES)))
             i(("s_addc_u32", S(S_LINE + 1), S(S_ARG + 3), K(0)))
+
+
+class MillerLoopPreparedCfg(MillerLoopSharedCfg):
+    """miller_loop of (P_i, G2Prepared_i) pairs (kernels.miller_loop_prepared_prog).
+    Arguments: p_aff (G1Affine records), prepared (G2Prepared records of
+    RECORD bytes: 68 lines of (c0, c1, c2) Fq2 in the ABI form, the infinity
+    flag at FLAG), out (Fq12), n, workspace.
+
+    The wave copies the current line of its 64 records (64 x 288 B) into an
+    LDS buffer one line AHEAD, with 18 global_load_lds_dwordx4: slot s = tid +
+    64 t of copy t is piece s % 18 (16 B) of record s / 18, so the buffer holds
+    record r's line at 288 r and every copy instruction reads 4-5 contiguous
+    288-byte runs -- not 64 records 19.6 KB apart (measured at 2^16: 6.53 ms
+    against 6.66 for the per-lane scatter).  What the copy still costs (6.07
+    ms with no copy at all, 6.15 with every lane copying one address) is not
+    its latency: waiting for it right after issue costs 0.08 ms more, not
+    waiting at all (wrong results) nothing less, and L2-resident source lines
+    (line 0 every time) 0.05 ms less.  The copy runs with every lane
+    of the wave on (the record index clamped to n - 1), since lanes past n
+    still copy pieces for lanes below it.
+
+    tnext (after the line's values are in registers) waits for the buffer's
+    reads and issues the next line's copy, which lands under mul_by_014 and the
+    squaring; the first tload of a line waits for it (vmcnt 0); each value is
+    read with ds_read_b64 at v17 = 288 tid and split into its 14 limbs when it
+    lands (emit_split).  s[96] = the line's byte offset in a record; the copy
+    after the last line re-reads line 67 (s[97] = min(s[96], 67 lines)).  LDS
+    per wave: five spill slots + the 18 KiB buffer (36 352 B; four waves per
+    CU).  s[98:99] exec saved around a copy, s100 = n - 1, s101 = the wave's
+    first record."""
+    name = "pa_gen_miller_loop_prepared"
+    RECORD, FLAG, LINE = 19592, 19584, 288
+    PIECES = 18                 # 288 B per lane / 16 B per global_load_lds_dwordx4
+    nsgpr = 102
+
+    def __init__(self):
+        self.lds_table = False
+        self.per_lane_table = True
+        self.nl = 5
+        self.extra_lds = 1024 * self.PIECES
+
+    def pre_exec(self, em, code):
+        pass
+
+    def emit_copy(self, put):
+        """line s[97] of the wave's 64 records -> the LDS buffer (in flight)"""
+        put("wave_begin")                               # simulator: every lane runs the copy
+        put("s_or_saveexec_b64", S(98), K(-1))
+        put("v_lshrrev_b32", 3, K(3), LOFF)             # tid
+        for t in range(self.PIECES):
+            put("v_add_u32", 0, K(64 * t), 3)           # slot s
+            put("v_mul_u32_u24", 1, K(3641), 0)
+            put("v_lshrrev_b32", 1, K(16), 1)           # r = s / 18 (exact for s < 1152)
+            put("v_mul_u32_u24", 2, K(18), 1)
+            put("v_sub_u32", 2, 0, 2)                   # piece j = s - 18 r
+            put("v_add_u32", 1, S(101), 1)
+            put("v_min_u32", 1, S(100), 1)              # record, clamped to n - 1
+            put("v_lshlrev_b32", 2, K(4), 2)
+            put("v_add_u32", 2, S(S_LINE + 1), 2)       # byte offset in the record
+            put("v_mov_b64", ADDR, S(S_ARG + 2))
+            put("v_mad_u64_u32", ADDR, 1, S(S_STRIDE), ADDR)
+            put("v_mad_u64_u32", ADDR, 2, K(1), ADDR)
+            put("s_mov_m0", K(self.table_base() + 1024 * t))
+            put("s_nop", 0)
+            put("global_load_lds_dwordx4", ADDR)
+        put("s_mov_b64_exec", S(98))
+        put("wave_end")
+
+    def prologue_masks(self, em, code):
+        i = code.append
+        # valid = neither P nor this lane's prepared Q is the point at infinity
+        self.lane_addr(code, 0, 104)
+        i(("global_load_dword", 0, ADDR, 96))
+        self.lane_addr(code, 1, self.RECORD)
+        i(("v_mov_b32", 14, K(self.FLAG)))
+        i(("v_mad_u64_u32", ADDR, 14, K(1), ADDR))
+        i(("global_load_dword", 1, ADDR, 0))
+        i(("s_waitcnt_vm0",))
+        i(("v_or_b32", 0, 0, 1))
+        i(("v_and_b32", 0, K(0xff), 0))
+        i(("v_cmp_eq_u32", K(0), 0))
+        i(("s_nop", 1))
+        i(("s_mov_b64", S(S_VALID), S(106)))
+        i(("v_mul_u32_u24", ZERO, K(36), LOFF))          # 288 tid: this lane's line in the buffer
+        i(("s_mov_b32", S(S_LINE), K(0)))
+        i(("s_mov_b32", S(S_LINE + 1), K(0)))
+        i(("s_sub_u32", S(100), S(S_ARG + 6), K(1)))
+        i(("s_lshl_b32", S(101), S(S_WG), K(6)))
+        i(("s_mov_b32", S(S_STRIDE), K(self.RECORD)))
+        self.emit_copy(lambda *t: i(t))                  # line 0
+
+    def emit_tload(self, em, imm, d):
+        """value imm of the current line: its 12 words from the LDS buffer into
+        d..d+11, in flight (a counted lgkm wait and the split at first use)"""
+        if imm == 0:
+            em.i("s_waitcnt_vm0")      # the line's copy has landed
+        for j in range(6):
+            em.i("ds_read_b64", d + 2 * j, ZERO, self.table_base() + 48 * imm + 8 * j)
+
+    @staticmethod
+    def emit_split(em, d):
+        """12 x 32-bit words in d..d+11 -> 14 x 28-bit limbs in d..d+13, in place:
+        limb k reads words <= k only, so from the top limb down"""
+        for li in reversed(range(NL)):
+            bit = 28 * li
+            wi, sh = bit // 32, bit % 32
+            if sh == 0:
+                em.i("v_and_b32", d + li, K(MASK), d + wi)
+            elif sh + 28 == 32 or wi + 1 == 12:     # the limb's top bits end the word
+                em.i("v_lshrrev_b32", d + li, K(sh), d + wi)
+            else:
+                em.i("v_alignbit_b32", d + li, d + wi + 1, d + wi, K(sh))
+                em.i("v_and_b32", d + li, K(MASK), d + li)
+
+    def emit_tnext(self, em):
+        em.i("s_waitcnt_lgkm0")        # this line's reads of the buffer are done
+        em.i("s_add_u32", S(S_LINE), S(S_LINE), K(self.LINE))
+        em.i("s_min_u32", S(S_LINE + 1), S(S_LINE), K(self.FLAG - self.LINE))
+        em.i("s_mov_b32", S(S_STRIDE), K(self.RECORD))
+        self.emit_copy(em.i)
 
 
 class MillerLoopCfg2(MillerLoopCfg):

@@ -137,7 +137,23 @@ def miller_loop_prog(homes=None, lanes=1, lazy=False):
     return p
 
 
-def miller_loop_shared_prog():
+def miller_loop_prepared_prog():
+    """Bls12::miller_loop over (G1Affine_i, G2Prepared_i) pairs -- the
+    north-star call shape (mod.rs:40-102 with each pair's own prepared record):
+    miller_loop_shared_prog with the lines read from this lane's G2Prepared
+    record (kcfg.MillerLoopPreparedCfg) in the ABI form, all six values raw;
+    c2 takes its lazy form by one product each (prepared_table_lines)"""
+    return miller_loop_shared_prog(per_lane=True)
+
+
+def prepared_table_lines(coeffs):
+    """the values tload gives miller_loop_prepared_prog: raw limbs of the six
+    ABI integers of every line (the record as written by k_g2_prepare)"""
+    import gen_fl
+    return [[tuple(gen_fl.limbs(x)) for x in line] for line in coeffs]
+
+
+def miller_loop_shared_prog(per_lane=False):
     """Bls12::miller_loop([(P_i, Q)]) for a batch of P_i and ONE prepared Q
     (lib.rs:88-96 with the same &G2Prepared in every pair; mod.rs:40-102).
     No G2 arithmetic: the line coefficients come from the kernel's line table
@@ -150,7 +166,7 @@ def miller_loop_shared_prog():
     mul(raw c, kx) = c P.x R' -- the ABI -> lazy conversion of c0 and c1 rides
     on the products ell needs anyway (mod.rs:57-69; pairing_fl.h ell_fl).
       inputs 0 px, 1 py (this lane's G1Affine); outputs 0..11 (Fq12)"""
-    p = Prog("miller_loop_shared", 1, use_norm=_norm(1))
+    p = Prog("miller_loop_prepared" if per_lane else "miller_loop_shared", 1, use_norm=_norm(1))
     T = Tower(p)
     V = _Vars(p, 1)
     for n in ("kx", "ky"):
@@ -163,10 +179,24 @@ def miller_loop_shared_prog():
 
     def line():
         c = [p.tload(j) for j in range(6)]
-        p.tnext()
+        if not per_lane:
+            p.tnext()
+        if per_lane:
+            # c2 raw from the record (c2 R): its lazy form c2 R' = raw 2^8 mod q,
+            # two rounds of x16 (limbs < 2^32) and a reduction -- in place of a
+            # product by 2^400 (R'^2 / R)
+            for j in (4, 5):
+                for _ in range(2):
+                    for _ in range(4):
+                        c[j] = p.add(c[j], c[j])
+                    c[j] = p.red(c[j])
         kx, ky = p.get("kx"), p.get("ky")
         a = (p.mul(c[0], ky), p.mul(c[1], ky))     # c0 * P.y
         b = (p.mul(c[2], kx), p.mul(c[3], kx))     # c1 * P.x
+        if per_lane:
+            # every value of the line is in registers: the next line's copy into
+            # the LDS buffer (kcfg.MillerLoopPreparedCfg) lands under mul_by_014
+            p.tnext()
         V.set12("f", T.mul_by_014(V.get12("f"), (c[4], c[5]), b, a))
 
     with p.loop(62) as L:

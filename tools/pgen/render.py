@@ -13,7 +13,7 @@ W64 = {  # operand positions that are 64-bit register pairs, per mnemonic
     "v_lshrrev_b64": (0, 2), "v_ashrrev_i64": (0, 2), "v_lshl_add_u64": (0, 1, 3),
     "ds_write_b64": (1,), "ds_read_b64": (0,),
     "global_load_dwordx2": (0, 1), "global_load_dword": (1,), "global_store_dwordx2": (0, 1),
-    "global_store_byte": (0,), "global_store_dwordx2_s": (1, 2), "global_load_dwordx2_s": (0, 2),
+    "global_store_byte": (0,), "global_load_lds_dwordx4": (0,), "global_store_dwordx2_s": (1, 2), "global_load_dwordx2_s": (0, 2),
     "s_load_dwordx2": (0, 1), "s_mov_b64": (0, 1), "s_and_saveexec_b64": (0,), "s_bitcmp1_b64": (0,),
     "s_cmp_eq_u64": (0,), "v_cmp_eq_u32_e64": (0,), "v_cmp_ne_u32_e64": (0,),
     "v_cmp_lt_u64_e64": (0, 1, 2), "s_and_b64": (0, 1, 2), "s_or_b64": (0, 1, 2),
@@ -115,6 +115,16 @@ class Renderer:
             return ["global_store_dwordx2 %s, %s, %s offset:%d" % (o[0], o[1], o[2], a[3])]
         if m == "global_load_dwordx2_s":
             return ["global_load_dwordx2 %s, %s, %s offset:%d" % (o[0], o[1], o[2], a[3])]
+        if m in ("wave_begin", "wave_end"):
+            return []
+        if m == "s_or_saveexec_b64":
+            return ["s_or_saveexec_b64 %s, %s" % (reg(a[0], True), o[1])]
+        if m == "s_mov_b64_exec":
+            return ["s_mov_b64 exec, %s" % reg(a[0], True)]
+        if m == "s_mov_m0":
+            return ["s_mov_b32 m0, %s" % o[0]]
+        if m == "global_load_lds_dwordx4":
+            return ["global_load_lds_dwordx4 %s, off" % o[0]]
         if m == "s_load_dwordx2":
             return ["s_load_dwordx2 %s, %s, 0x%x" % (o[0], o[1], a[2])]
         if m == "s_waitcnt_lgkm0":

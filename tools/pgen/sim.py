@@ -37,6 +37,8 @@ class Sim:
         self.scc = 0
         self.mem = {}       # dword address -> u32
         self.lds = {}
+        self.lds_dma = {}     # LDS byte address -> (vm seq, word): global_load_lds data not yet waited for
+        self.m0 = 0
         self.lane = lane
         self.labels = {t[1]: i for i, t in enumerate(code) if t[0] == "label"}
         self.count = 0
@@ -159,6 +161,9 @@ class Sim:
         if kind == "vm":
             for ad in [ad for ad, sq in self.st_inflight.items() if sq <= limit]:
                 del self.st_inflight[ad]
+        if kind == "vm":
+            for ad in [ad for ad, (sq, _) in self.lds_dma.items() if sq <= limit]:
+                self.lds[ad] = self.lds_dma.pop(ad)[1]
         for key in [k for k, (kd, sq, _) in self.inflight.items() if kd == kind and sq <= limit]:
             ln, x = key
             self.vf[ln][x] = self.inflight.pop(key)[2]
@@ -177,6 +182,9 @@ class Sim:
         while pc < n:
             self.pc = pc
             t = code[pc]
+            if t[0] == "wave_begin":
+                pc = self.run_wave(pc)
+                continue
             self.count += 1
             if self.count > max_steps:
                 raise RuntimeError("step limit")
@@ -211,6 +219,43 @@ class Sim:
             if nxt == "end":
                 return
             pc = self.labels[nxt] if nxt is not None else pc + 1
+
+    LOFF = 16     # v16 = tid * 8 (emit.LOFF)
+
+    def run_wave(self, pc):
+        """a wave_begin .. wave_end region (straight-line code, e.g. a copy in
+        which every lane of the wave loads for other lanes): run for all 64
+        lanes, the lanes outside the simulated ones starting from a copy of the
+        first simulated lane's registers with their own tid; returns the pc
+        after the region"""
+        code = self.code
+        end = next(k for k in range(pc, len(code)) if code[k][0] == "wave_end")
+        main = self.lanes[0]
+        files = {}
+        for ln in range(64):
+            if ln in self.vf:
+                files[ln] = (self.vf[ln], self.af[ln])
+            else:
+                v = list(self.vf[main])
+                v[self.LOFF] = 8 * ln
+                files[ln] = (v, list(self.af[main]))
+        for k in range(pc + 1, end):
+            t = code[k]
+            self.pc = k
+            m = t[0]
+            self.count += 1
+            self.hist[m] = self.hist.get(m, 0) + 1
+            self.ws += (t[1] + 1) if m == "s_nop" else 1
+            if m.startswith("global_"):
+                self.seq["vm"] += 1
+            if m.startswith("v_") or m.startswith("global_"):
+                for ln in range(64):
+                    self.lane, (self.v, self.a) = ln, files[ln]
+                    self.step(t)
+            else:
+                self.step(t)
+        self.lane, self.v, self.a = main, self.vf[main], self.af[main]
+        return end + 1
 
     def step(self, t):
         m = t[0]
@@ -316,12 +361,21 @@ class Sim:
             self.lds[addr + 4] = rd(a[1] + 1)
         elif m == "ds_read_b64":
             addr = rd(a[1]) + a[2]
+            if addr in self.lds_dma or addr + 4 in self.lds_dma:
+                raise AssertionError("LDS read of 0x%x before its global_load_lds was waited for (instr %d)" % (
+                    addr, self.count))
             self.async_wr("lgkm", a[0], self.lds.get(addr, 0))
             self.async_wr("lgkm", a[0] + 1, self.lds.get(addr + 4, 0))
         elif m == "global_load_dwordx2":
             addr = rd64(a[1]) + a[2]
             wr(a[0], self.ld32(addr))
             wr(a[0] + 1, self.ld32(addr + 4))
+        elif m == "global_load_lds_dwordx4":
+            # 16 bytes from this lane's address into LDS at M0 + 16 lane, landing
+            # at a vmcnt wait (the instruction offset is always 0 here)
+            addr = rd64(a[0])
+            for w in range(4):
+                self.lds_dma[self.m0 + 16 * (self.lane % 64) + 4 * w] = (self.seq["vm"], self.ld32(addr + 4 * w))
         elif m == "global_load_dword":
             wr(a[0], self.ld32(rd64(a[1]) + a[2]))
         elif m == "global_store_dwordx2":
@@ -352,6 +406,14 @@ class Sim:
             wr(a[0] + 1, self.ld32(addr + 4))
         elif m == "s_mov_b32":
             wr(a[0], rd(a[1]))
+        elif m in ("s_or_saveexec_b64", "s_mov_b64_exec"):
+            pass          # exec: the simulator runs the lanes it is given
+        elif m == "v_min_u32":
+            wr(a[0], min(rd(a[1]), rd(a[2])))
+        elif m == "s_mov_m0":
+            self.m0 = rd(a[0])
+        elif m == "s_min_u32":
+            wr(a[0], min(rd(a[1]), rd(a[2])))
         elif m == "s_mov_b64":
             wr64(a[0], rd64(a[1]))
         elif m == "s_add_u32":

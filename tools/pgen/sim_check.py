@@ -64,6 +64,18 @@ def check(which, seed=5, lane=3, debug=True):
             for i, w in enumerate(table[t0:]):
                 lds[cfg.table_base() + 8 * i] = w & 0xffffffff
                 lds[cfg.table_base() + 8 * i + 4] = w >> 32
+    elif which == "mlp":
+        # lane `lane`'s G2Prepared record (68 lines of six ABI integers, flag 0)
+        import kernels
+        ins = [rng.randrange(dsl.Q) for _ in range(2)]
+        coeffs = [[rng.randrange(dsl.Q) for _ in range(6)] for _ in range(68)]
+        prec = [0] * (13 * lane) + words(ins) + [0]
+        want = dsl.evaluate(prog, {0: ins[0], 1: ins[1], "lines": kernels.prepared_table_lines(coeffs)},
+                            trace=trace)
+        rw = cfg.RECORD // 8
+        qrec = [0] * (rw * lane) + sum((words(line) for line in coeffs), []) + [0]
+        args = [IN, AUX, OUT, lane + 1, WS]
+        bufs = {IN: prec, AUX: qrec}
     else:
         # any field values (the loop does not care whether they are on the curve)
         ins = [rng.randrange(dsl.Q) for _ in range(6)]
