@@ -504,7 +504,8 @@ def main():
             out = outs[slot]
             if timed:
                 ev[0].record(stream)
-            pdev.miller_loop(p, q, scratch, stream)
+            # pa_pairing_batch_device's two stages, timed apart
+            pdev.pairing_miller_loop(p, q, scratch, stream)
             if timed:
                 ev[1].record(stream)
             if works[slot] is not None:
@@ -979,10 +980,11 @@ def main():
                                                         dom_name == "final_exponentiation")
             wk = work["final_exp_lane_pairs" if lp else "final_exp"] if dom_name == "final_exponentiation" else \
                 work[dom_name] if dom_name in ("miller_loop_shared", "miller_loop_prepared") else \
-                work["miller_loop_lane_pairs" if lp else "miller_loop"]
+                work[("miller_loop_lane_pairs_pairing_only" if args.workload == "pairing" else
+                      "miller_loop_lane_pairs") if lp else "miller_loop"]
             if lp:
                 roof_kernel = {"final_exponentiation": "pa_gen_final_exp2",
-                               "miller_loop_fused": "pa_gen_miller_loop2"}.get(dom_name, dom_name)
+                               "miller_loop_fused": "pa_gen_miller_loop2p"}.get(dom_name, dom_name)
                 traffic = traffic_all.get(dom_name + "_lane_pairs")
             macs = wk["limb_macs"]
             mac_rate = macs * n / (dom_ms * 1e-3) / 1e12

@@ -403,6 +403,16 @@ int pa_g1_eq_batch_device(const pa_g1 *a, const pa_g1 *b, uint8_t *eq, size_t n,
 int pa_g2_eq_batch_device(const pa_g2 *a, const pa_g2 *b, uint8_t *eq, size_t n, void *stream);
 int pa_miller_loop_fused_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
                                       void *stream);
+/* The first stage of pa_pairing_batch_device, on its own (so a caller can time
+ * or overlap the two stages): Miller values from which
+ * pa_final_exponentiation_batch_device gives exactly e(p[i], q[i]).  They equal
+ * the reference's miller_loop values only up to an Fq2 factor per pair (the
+ * lane-pair kernel's G2 steps use homogeneous coordinates and their own line
+ * scaling; the final exponentiation removes any Fq2 factor, since
+ * (q^12 - 1) / r is a multiple of q^2 - 1), so do not use them as Miller
+ * values -- pa_miller_loop_fused_batch_device gives those. */
+int pa_pairing_miller_loop_batch_device(const pa_g1_affine *p, const pa_g2_affine *q, pa_fq12 *out, size_t n,
+                                        void *stream);
 /* final_exponentiation (mod.rs:104-160) on device records: one kernel launch
  * on `stream` (the cooperative kernel up to PA_COOP_MAX records, the generated
  * one above); `out` may equal `in` (in place) or lie apart from it, in which

@@ -108,6 +108,7 @@ _SIGS = {
     "pa_fq_mul_batch_device": [_P, _P, _P, _N, _P],
     "pa_fq_mul_batch_soa_device": [_P, _P, _P, _N, _P],
     "pa_miller_loop_fused_batch_device": [_P, _P, _P, _N, _P],
+    "pa_pairing_miller_loop_batch_device": [_P, _P, _P, _N, _P],
     "pa_g2_prepare_batch_device": [_P, _P, _N, _P],
     "pa_miller_loop_batch_device": [_P, _P, _P, _N, _P],
     "pa_miller_loop_shared_prepared_device": [_P, _N, _P, _P, _P],

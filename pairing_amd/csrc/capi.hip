@@ -90,6 +90,17 @@ hipError_t mlp_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_
     if (hipcc) return pa::launch_miller_loop_prepared(p, q, out, n, s);
     return pa::launch_miller_loop_prepared_gen(p, q, out, n, s);
 }
+// The Miller loop in front of a final exponentiation (pa_pairing_batch[_device],
+// pa_multi_pairing_device): on lane pairs the pairing-only kernel, whose Miller
+// values differ from the reference's by Fq2 factors that the final
+// exponentiation removes ((q^12 - 1) / r is a multiple of q^2 - 1) -- 3.5 %
+// fewer instructions (tools/pgen/kernels.py doubling_step_h).  The Miller-loop
+// entries themselves keep ml_launch.  PA_PAIRING_ML=ref: ml_launch (A/B).
+hipError_t pairing_ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
+    static const bool ref = getenv("PA_PAIRING_ML") && strcmp(getenv("PA_PAIRING_ML"), "ref") == 0;
+    if (ref || use_coop(n) || gen_lanes(n) != 2) return ml_launch(p, q, out, n, s);
+    return pa::launch_miller_loop_pairing_gen(p, q, out, n, s);
+}
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s, coop_vm());
     return pa::launch_final_exp_gen(gen_lanes(n), in, out, ok, n, s);
@@ -647,7 +658,7 @@ int pa_pairing_batch(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out,
         stamp("staged in", ci);
         PA_TRY(hipStreamWaitEvent(ks, h2d[k], 0), "stream wait");
         if (ci >= 2) PA_TRY(hipStreamWaitEvent(ks, outk[k], 0), "stream wait");
-        PA_TRY(ml_launch((const uint64_t*)dev_p, (const uint64_t*)dev_q, dev_ml, cnt, ks), "kernel launch");
+        PA_TRY(pairing_ml_launch((const uint64_t*)dev_p, (const uint64_t*)dev_q, dev_ml, cnt, ks), "kernel launch");
         // Engine::pairing unwraps: a Miller-loop value is never zero, ok is not reported
         PA_TRY(fe_launch(dev_ml, dev_out, nullptr, cnt, ks), "kernel launch");
         PA_TRY(hipEventRecord(done[k], ks), "event");
@@ -757,7 +768,7 @@ int pa_multi_pairing_device(const pa_g1_affine* p, const pa_g2_affine* q, size_t
         PA_TRY(hipStreamSynchronize(s), "H2D copy");   // the host sources go out of scope
         return PA_OK;
     }
-    PA_TRY(ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)work, n, s), "kernel launch");
+    PA_TRY(pairing_ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)work, n, s), "kernel launch");
     if (n <= kCoopProductMax && use_coop(1)) {
         // the product of a few Miller values inside the cooperative final
         // exponentiation (mul12 macros, ~6 us each) instead of the one-lane
@@ -1076,6 +1087,13 @@ int pa_miller_loop_fused_batch_device(const pa_g1_affine* p, const pa_g2_affine*
            "kernel launch");
     return PA_OK;
 }
+int pa_pairing_miller_loop_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, size_t n,
+                                        void* stream) {
+    if (n && (!p || !q || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pairing_ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)out, n, (hipStream_t)stream),
+           "kernel launch");
+    return PA_OK;
+}
 int pa_final_exponentiation_batch_device(const pa_fq12* in, pa_fq12* out, uint8_t* ok, size_t n, void* stream) {
     if (n && (!in || !out)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
     PA_TRY(fe_launch((const uint64_t*)in, (uint64_t*)out, ok, n, (hipStream_t)stream), "kernel launch");
@@ -1105,7 +1123,7 @@ int pa_miller_loop_shared_prepared_device(const pa_g1_affine* p, size_t n, const
 int pa_pairing_batch_device(const pa_g1_affine* p, const pa_g2_affine* q, pa_fq12* out, pa_fq12* scratch,
                             size_t n, void* stream) {
     if (n && (!p || !q || !out || !scratch)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
-    PA_TRY(ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)scratch, n, (hipStream_t)stream),
+    PA_TRY(pairing_ml_launch((const uint64_t*)p, (const uint64_t*)q, (uint64_t*)scratch, n, (hipStream_t)stream),
            "kernel launch");
     PA_TRY(fe_launch((const uint64_t*)scratch, (uint64_t*)out, nullptr, n, (hipStream_t)stream), "kernel launch");
     return PA_OK;

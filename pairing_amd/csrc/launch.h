@@ -79,6 +79,11 @@ static_assert(kSharedTableAlloc >= kSharedTableBytes, "staging rows cover the ta
 hipError_t launch_shared_line_table(const uint64_t* prepared, uint32_t* table, hipStream_t stream);
 hipError_t launch_miller_loop_shared_gen(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out, size_t n,
                                          hipStream_t stream);
+// the pairing-only lane-pair Miller loop (homogeneous G2 steps, own line
+// scaling): for e(P, Q) paths only -- its values equal the reference's Miller
+// values up to Fq2 factors, which the final exponentiation removes
+hipError_t launch_miller_loop_pairing_gen(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+                                          hipStream_t stream);
 // the generated Miller loop of (P_i, G2Prepared_i) pairs (tools/pgen
 // MillerLoopPreparedCfg): each lane reads its own record's lines
 hipError_t launch_miller_loop_prepared_gen(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out,

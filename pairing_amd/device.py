@@ -87,6 +87,17 @@ def miller_loop(p, q, out, stream=None):
     call("pa_miller_loop_fused_batch_device", *args, n, _stream_ptr(stream))
 
 
+def pairing_miller_loop(p, q, out, stream=None):
+    """The Miller-loop stage of pairing(): final_exponentiation(out) = e(p[i], q[i]);
+    out equals the reference's Miller values only up to Fq2 factors (see
+    pa_pairing_miller_loop_batch_device)."""
+    n = p.shape[0]
+    args = (_dptr(p, W_G1A, "p"), _dptr(q, W_G2A, "q"), _dptr(out, W_FQ12, "out"))
+    _rows(q, n, "q")
+    _rows(out, n, "out")
+    call("pa_pairing_miller_loop_batch_device", *args, n, _stream_ptr(stream))
+
+
 def g2_prepare(q, out, stream=None):
     """G2Prepared::from_affine over a batch (mod.rs:168-358): out (n, W_G2P) int64 records."""
     n = q.shape[0]

@@ -237,7 +237,7 @@ def test_prepared_path_device_bit_exact_at_bench_size(gpu, oracle, n):
     np.testing.assert_array_equal(_host(out), oracle.pairing(p_np, q_np, _threads()))
 
 
-@pytest.mark.parametrize("n", [0, 1, 2, 5, 16, 17, 300])
+@pytest.mark.parametrize("n", [0, 1, 2, 5, 16, 17, 300, 3001])
 def test_multi_pairing_device_matches_oracle(gpu, oracle, n):
     """bench.py --workload verify: pa_multi_pairing_device (cooperative Miller
     loops; up to 16 pairs the Miller values' product inside the cooperative
@@ -265,6 +265,37 @@ def test_multi_pairing_device_matches_oracle(gpu, oracle, n):
         exp = exp[0]
     assert int(ok.item()) == 1
     np.testing.assert_array_equal(_host(out)[0], exp)
+
+
+@pytest.mark.parametrize("n", [4099, 1 << 16])
+def test_pairing_miller_loop_stage_then_final_exp(gpu, oracle, n):
+    """bench.py's timed pairing step: pa_pairing_miller_loop_batch_device (the
+    pairing-only lane-pair Miller loop: homogeneous G2 steps, its own line
+    scaling) then pa_final_exponentiation_batch_device == the oracle's pairing,
+    bit for bit, with infinity P and Q mixed in; its Miller values differ from
+    the reference's (by Fq2 factors) where neither point is at infinity"""
+    import torch
+    import bench
+    import pairing_amd.device as pdev
+    p_np, q_np = bench.make_pairs(n, 0, seed=29)
+    q_np[5::301, :24] = 0
+    q_np[5::301, 12:18] = limbs(pow(2, 384, Q))
+    q_np[5::301, 24] = 1
+    dp, dq = _dev(p_np), _dev(q_np)
+    f = pdev.empty_records(n, 72, "cuda:0")
+    out = pdev.empty_records(n, 72, "cuda:0")
+    pdev.pairing_miller_loop(dp, dq, f)
+    pdev.final_exponentiation(f, out)
+    torch.cuda.synchronize()
+    want = np.concatenate([oracle.pairing(p_np[k:k + 8192], q_np[k:k + 8192], _threads())
+                           for k in range(0, n, 8192)])
+    np.testing.assert_array_equal(_host(out), want)
+    ref = pdev.empty_records(64, 72, "cuda:0")
+    pdev.miller_loop(dp[:64], dq[:64], ref)
+    torch.cuda.synchronize()
+    fin = (p_np[:64, 12] & 0xff) | (q_np[:64, 24] & 0xff)
+    differ = (_host(f)[:64] != _host(ref)).any(axis=1)
+    assert differ[fin == 0].all() and not differ[fin != 0].any()
 
 
 @pytest.mark.parametrize("which", ["subgroup", "outside"])

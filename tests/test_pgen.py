@@ -109,7 +109,21 @@ SIM_ALL = os.environ.get("PA_SIM_ALL") == "1"
 _ab_only = pytest.mark.skipif(not SIM_ALL, reason="A/B-only code object (PA_SIM_ALL=1 runs it)")
 
 
-@pytest.mark.parametrize("which", ["ml", "ml2", pytest.param("mlz", marks=_ab_only)])
+def test_dsl_pairing_only_miller_loop_gives_the_pairing(ref_pair):
+    """the pairing-only lane-pair Miller loop (homogeneous G2 steps with their
+    own line scaling, kernels.doubling_step_h / addition_step_h): its value
+    differs from the reference's Miller value, and the final exponentiation of
+    it is the reference's pairing, bit for bit"""
+    import tower2
+    ins, ml, fe = ref_pair
+    prog = tower2.two_pass(lambda: kernels.miller_loop_prog(lanes=2, pairing_only=True), xi_dpp=False)()
+    f = dsl.evaluate(prog, ins)
+    assert [f[k] for k in range(12)] != ml
+    out = dsl.evaluate(kernels.final_exp_prog(), {k: f[k] for k in range(12)})
+    assert [out[k] for k in range(12)] == fe
+
+
+@pytest.mark.parametrize("which", ["ml", "ml2", "ml2p", pytest.param("mlz", marks=_ab_only)])
 def test_sim_miller_loop_kernel(which):
     assert sim_check.check(which, debug=True)
 

@@ -406,6 +406,12 @@ class MillerLoopCfg2(MillerLoopCfg):
     lanes = 2
 
 
+class MillerLoopCfg2p(MillerLoopCfg2):
+    """the pairing-only lane-pair Miller loop (kernels.miller_loop_prog(pairing_only=True)):
+    same records, masks and output slots as MillerLoopCfg2"""
+    name = "pa_gen_miller_loop2p"
+
+
 class FinalExpCfg2(FinalExpCfg):
     name = "pa_gen_final_exp2"
     lanes = 2

@@ -72,6 +72,54 @@ def addition_step(T, r, qx, qy):
     return (c0, c1, c2), (nx, ny, nz)
 
 
+def doubling_step_h(T, r):
+    """doubling with its tangent line in homogeneous coordinates (x = X/Z,
+    y = Y/Z) on E': y^2 = x^3 + b', b' = 4 (1 + u) (Costello-Lange-Naehrig,
+    eprint 2009/615, scaled by 4 to avoid halvings): 3 M + 6 S against
+    doubling_step's 3 M + 8 S.  The line is the reference's scaled by an Fq2
+    factor (Z^2 / 2 Z_J^6): c0 = 2 Y Z (y_P), c1 = -3 X^2 (x_P), c2 = Y^2 - 3 b' Z^2
+    -- equal after the final exponentiation, not as a Miller value
+    (pairing-only kernels)"""
+    x, y, z = r
+    B = T.sqr2(y)
+    C = T.sqr2(z)
+    xc = T.red2(T.xi(C))
+    E = T.red2(T.dbl2(T.dbl2(T.add2(T.dbl2(xc), xc))))          # 12 (1 + u) Z^2 = 3 b' Z^2
+    H = T.red2(T.sub2(T.sqr2(T.add2(y, z)), T.add2(B, C)))        # 2 Y Z
+    X2 = T.sqr2(x)
+    E3 = T.red2(T.add2(T.dbl2(E), E))
+    nx = T.red2(T.dbl2(T.mul2(T.mul2(x, y), T.red2(T.sub2(B, E3)))))   # 2 X Y (Y^2 - 9 b' Z^2)
+    ee = T.sqr2(E)
+    e12 = T.dbl2(T.dbl2(T.add2(T.dbl2(ee), ee)))
+    ny = T.red2(T.sub2(T.sqr2(T.red2(T.add2(B, E3))), e12))   # (Y^2 + 9 b' Z^2)^2 - 108 b'^2 Z^4
+    nz = T.red2(T.dbl2(T.dbl2(T.mul2(B, H))))                 # 8 Y^3 Z
+    c1 = T.red2(T.neg2(T.add2(T.dbl2(X2), X2)))
+    c2 = T.red2(T.sub2(B, E))
+    return (H, c1, c2), (nx, ny, nz)
+
+
+def addition_step_h(T, r, qx, qy):
+    """mixed addition R + Q (R homogeneous, Q affine) with the line through
+    them: theta = Y1 - y2 Z1, lambda = X1 - x2 Z1; the line lambda y_P -
+    theta x_P + (theta x2 - lambda y2) is the reference's scaled by an Fq2
+    factor (pairing-only kernels)"""
+    X1, Y1, Z1 = r
+    th = T.red2(T.sub2(Y1, T.mul2(qy, Z1)))
+    la = T.red2(T.sub2(X1, T.mul2(qx, Z1)))
+    cc = T.sqr2(th)
+    d = T.sqr2(la)
+    e = T.mul2(la, d)
+    f = T.mul2(Z1, cc)
+    g = T.mul2(X1, d)
+    h = T.red2(T.sub2(T.add2(e, f), T.dbl2(g)))
+    nx = T.mul2(la, h)
+    ny = T.red2(T.sub2(T.mul2(th, T.red2(T.sub2(g, h))), T.mul2(Y1, e)))
+    nz = T.mul2(Z1, e)
+    c1 = T.red2(T.neg2(th))
+    c2 = T.red2(T.sub2(T.mul2(th, qx), T.mul2(la, qy)))
+    return (la, c1, c2), (nx, ny, nz)
+
+
 def ell(T, f, c, px, py):
     """mod.rs:57-69: f.mul_by_014(c2, c1 * P.x, c0 * P.y)"""
     return T.mul_by_014(f, c[2], T.mul_fq(c[1], px), T.mul_fq(c[0], py))
@@ -87,10 +135,16 @@ ML_HOMES = {"px": "L", "py": "L", "qx0": "M", "qx1": "M", "qy0": "M", "qy1": "M"
 ML2_HOMES = {"f": "LLLLLLLLLLMM", "px": "M", "rx0": "M", "ry0": "M", "rz0": "M"}
 
 
-def miller_loop_prog(homes=None, lanes=1, lazy=False):
+def miller_loop_prog(homes=None, lanes=1, lazy=False, pairing_only=False):
+    """pairing_only: the G2 steps in homogeneous coordinates with their own
+    line scaling (doubling_step_h / addition_step_h): f differs from the
+    reference's Miller value by an Fq2 factor, which the final exponentiation
+    removes ((q^12 - 1) / r is a multiple of q^2 - 1) -- for e(P, Q) only"""
     base = dict(ML_HOMES, **ML2_HOMES) if lanes == 2 and os.environ.get("PGEN_ML2_HOMES", "1") == "1" else ML_HOMES
     homes = dict(base, **(homes or {}))
-    p = Prog("miller_loop" if lanes == 1 else "miller_loop2", lanes, use_norm=_norm(lanes))
+    name = ("miller_loop" if lanes == 1 else "miller_loop2") + ("p" if pairing_only else "")
+    p = Prog(name, lanes, use_norm=_norm(lanes))
+    dbl, add = (doubling_step_h, addition_step_h) if pairing_only else (doubling_step, addition_step)
     T = (TowerLazy(p) if lazy else Tower(p)) if lanes == 1 else Tower2(p)
     V = _Vars(p, lanes)
     for n in ("px", "py"):
@@ -114,9 +168,9 @@ def miller_loop_prog(homes=None, lanes=1, lazy=False):
     def line(step):
         r = tuple(V.get2(n) for n in ("rx", "ry", "rz"))
         if step == "dbl":
-            c, r = doubling_step(T, r)
+            c, r = dbl(T, r)
         else:
-            c, r = addition_step(T, r, V.get2("qx"), V.get2("qy"))
+            c, r = add(T, r, V.get2("qx"), V.get2("qy"))
         for n, v in zip(("rx", "ry", "rz"), r):
             V.set2(n, v)
         if lanes == 1:
