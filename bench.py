@@ -158,7 +158,7 @@ def kernel_variant_label(n):
     if v == 0:
         if n <= int(os.environ.get("PA_COOP_MAX", "2304")):
             return "coop"
-        one = int(os.environ.get("PA_PAIR_MAX", "32768")) < n <= int(os.environ.get("PA_ONE_MAX", "38912"))
+        one = int(os.environ.get("PA_PAIR_MAX", "32768")) < n <= int(os.environ.get("PA_ONE_MAX", "34048"))
         return "gen" if one else "gen2"
     return {1: "gen2", 2: "coop", 3: "gen", 4: "coop1"}.get(v, "variant%d" % v)
 

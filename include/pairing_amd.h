@@ -83,7 +83,7 @@ int pa_synchronize(void);
  *       cooperative kernels (a four-wave quad-VM workgroup per pairing,
  *       kernels_coop.hip: the verifier shape, ~1.6 ms), n <= PA_PAIR_MAX
  *       (32768) on the generated kernels with a lane pair per pairing
- *       (~8.6-9.3 ms), n <= PA_ONE_MAX (38912) on the generated
+ *       (~8.6-9.3 ms), n <= PA_ONE_MAX (34048) on the generated
  *       one-pairing-per-lane kernels (~16.1 ms), larger batches on lane
  *       pairs again, two waves per SIMD (2^16 in ~16.7 ms; tools/pgen: own
  *       register allocation, code objects lib/pa_gen_*.hsaco loaded at

@@ -216,7 +216,7 @@ def device_count():
 def set_pairing_kernel(variant):
     """Pairing kernels: 0 default by batch size (<= 2304 pairs on the
     cooperative kernels: a four-wave quad VM per pairing; <= 32768 a lane pair
-    per pairing; <= 38912 one lane per pairing; larger lane pairs), 1 lane pairs, 2
+    per pairing; <= 34048 one lane per pairing; larger lane pairs), 1 lane pairs, 2
     cooperative for every size, 3 one lane per pairing for every size, 4
     cooperative for every size on the round-2 one-wave VM.  Identical results."""
     call("pa_set_pairing_kernel", int(variant))

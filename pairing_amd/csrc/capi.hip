@@ -28,8 +28,10 @@ thread_local std::string g_last_error;
 //      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
 //   n <= pair_max() (32768): the generated kernels with a lane pair per
 //      pairing, at most one wave per SIMD: 8.6-9.3 ms whatever n;
-//   n <= one_max() (38912): one lane per pairing (one wave per SIMD at most:
-//      ~16.1 ms, where a second lane-pair wave on some SIMDs costs 16.3-17.5);
+//   n <= one_max() (34048): one lane per pairing (one wave per SIMD at most:
+//      ~16.04 ms, where a second lane-pair wave on a few SIMDs costs 16.1-17.1;
+//      with the pairing-only lane-pair Miller loop lane pairs win from ~34 000
+//      pairs, profiles/r05_regimes_after_ml2p.txt -- 38912 before it);
 //   larger: lane pairs again, two or more waves per SIMD (2^16: 16.7 ms
 //      against 17.2 ms one lane; 2^17: 33.0 vs 34.1 ms).  Round 5 gave the
 //      lane-pair final exponentiation the Karabina squarings and the
@@ -54,7 +56,7 @@ size_t pair_max() {
     return v;
 }
 size_t one_max() {
-    static const size_t v = env_size("PA_ONE_MAX", 38912);
+    static const size_t v = env_size("PA_ONE_MAX", 34048);
     return v;
 }
 bool use_coop(size_t n) {

@@ -112,7 +112,7 @@ def test_pairing_device_bit_exact_at_bench_size(gpu, oracle, variant):
     assert (got[inf] == one).all()
 
 
-@pytest.mark.parametrize("n", [2305, 32768, 32769, 38912, 38913])
+@pytest.mark.parametrize("n", [2305, 32768, 32769, 34048, 34049])
 def test_pairing_default_mid_size_batches(gpu, oracle, n):
     """The default selection's regime boundaries (PA_COOP_MAX < n <= PA_PAIR_MAX:
     lane pairs at one wave per SIMD; PA_PAIR_MAX < n <= PA_ONE_MAX: one lane per
