@@ -60,6 +60,7 @@ typedef struct { pa_fq c0, c1; } pa_fq2;
 typedef struct { pa_fq2 c0, c1, c2; } pa_fq6;
 typedef struct { pa_fq6 c0, c1; } pa_fq12;
 typedef struct { uint64_t l[4]; } pa_fr_repr;   /* canonical scalar, fr.rs:58 */
+typedef struct { uint64_t l[6]; } pa_fq_repr;   /* canonical base-field words, FqRepr fq.rs:699-700 */
 typedef struct { uint64_t l[4]; } pa_fr;        /* Montgomery form (R = 2^256), < r, fr.rs:247 */
 typedef struct { pa_fq x, y; uint8_t infinity; uint8_t _pad[7]; } pa_g1_affine;
 typedef struct { pa_fq2 x, y; uint8_t infinity; uint8_t _pad[7]; } pa_g2_affine;
@@ -120,6 +121,11 @@ int pa_fq_add_batch(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n);
 int pa_fq_sub_batch(const pa_fq *a, const pa_fq *b, pa_fq *out, size_t n);
 /* Field::inverse, fq.rs:849-902 (ok[i] = 0 for a zero input) */
 int pa_fq_inverse_batch(const pa_fq *a, pa_fq *out, uint8_t *ok, size_t n);
+/* PrimeField::from_repr, fq.rs:747-756: ok[i] = 0 = Err(NotInField) when repr >= q (out[i] = 0);
+ * otherwise out[i] = repr * R^2 (Montgomery form) */
+int pa_fq_from_repr_batch(const pa_fq_repr *repr, pa_fq *out, uint8_t *ok, size_t n);
+/* PrimeField::into_repr, fq.rs:758-775: the canonical words (mont_reduce of a) */
+int pa_fq_into_repr_batch(const pa_fq *a, pa_fq_repr *out, size_t n);
 
 /* ---- tower (fq2.rs, fq6.rs, fq12.rs) ---- */
 int pa_fq2_mul_batch(const pa_fq2 *a, const pa_fq2 *b, pa_fq2 *out, size_t n);     /* fq2.rs:123-136 */

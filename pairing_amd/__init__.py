@@ -21,7 +21,7 @@ from ._native import (W_FQ, W_FQ2, W_FQ6, W_FQ12, W_FR, W_G1A, W_G1, W_G2A, W_G2
 
 __all__ = [
     "PairingError", "version", "device_count", "set_device", "set_pairing_kernel", "set_decode_kernel",
-    "fq_mul", "fq_square", "fq_add", "fq_sub", "fq_inverse",
+    "fq_mul", "fq_square", "fq_add", "fq_sub", "fq_inverse", "fq_from_repr", "fq_into_repr",
     "fq2_mul", "fq2_square", "fq6_mul", "fq12_mul", "fq12_square", "fq12_inverse",
     "fq12_frobenius_map", "fq12_cyclotomic_square", "fq12_mul_by_014",
     "fq2_inverse", "fq2_frobenius_map", "fq6_square", "fq6_inverse", "fq6_frobenius_map", "fq_pow", "fq12_pow",
@@ -88,6 +88,20 @@ def fq_sub(a, b):
 def fq_inverse(a):
     """Fq::inverse (fq.rs:849-902): (values, ok) with ok False where the reference returns None."""
     return _inverse("pa_fq_inverse_batch", a, W_FQ)
+
+
+def fq_from_repr(repr_rows):
+    """PrimeField::from_repr (fq.rs:747-756): (values, ok), ok False = Err(NotInField) (repr >= q)."""
+    r = as_rows(repr_rows, W_FQ, "repr")
+    out = np.empty_like(r)
+    ok = np.zeros(r.shape[0], np.uint8)
+    call("pa_fq_from_repr_batch", ptr(r), ptr(out), ptr(ok), r.shape[0])
+    return out, ok.astype(bool)
+
+
+def fq_into_repr(a):
+    """PrimeField::into_repr (fq.rs:758-775): canonical FqRepr rows."""
+    return _unary("pa_fq_into_repr_batch", a, W_FQ)
 
 
 # ---- tower ----
@@ -284,6 +298,12 @@ def _wnaf_exact(group, fixed_scalar, bases, scalars, window):
     wj = W_G1 if group == 1 else W_G2
     b = as_rows(bases, wj, "base" if not fixed_scalar else "bases")
     s = as_rows(scalars, 4, "scalar" if fixed_scalar else "scalars")
+    # the fixed operand is ONE record (Wnaf::base(g, ..) / Wnaf::scalar(s)); a
+    # second row would be ignored silently, so refuse it
+    if fixed_scalar and s.shape[0] != 1:
+        raise ValueError("scalar: expected exactly one record, got %d" % s.shape[0])
+    if not fixed_scalar and b.shape[0] != 1:
+        raise ValueError("base: expected exactly one record, got %d" % b.shape[0])
     n = b.shape[0] if fixed_scalar else s.shape[0]
     out = np.empty((n, wj), np.uint64)
     w = 0 if window is None else int(window)

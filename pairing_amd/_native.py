@@ -80,6 +80,8 @@ _SIGS = {
     "pa_fq_add_batch": [_P, _P, _P, _N],
     "pa_fq_sub_batch": [_P, _P, _P, _N],
     "pa_fq_inverse_batch": [_P, _P, _P, _N],
+    "pa_fq_from_repr_batch": [_P, _P, _P, _N],
+    "pa_fq_into_repr_batch": [_P, _P, _N],
     "pa_fq2_mul_batch": [_P, _P, _P, _N],
     "pa_fq2_square_batch": [_P, _P, _N],
     "pa_fq6_mul_batch": [_P, _P, _P, _N],

@@ -31,7 +31,8 @@ thread_local std::string g_last_error;
 //   n <= one_max() (34048): one lane per pairing (one wave per SIMD at most:
 //      ~16.04 ms, where a second lane-pair wave on a few SIMDs costs 16.1-17.1;
 //      with the pairing-only lane-pair Miller loop lane pairs win from ~34 000
-//      pairs, profiles/r05_regimes_after_ml2p.txt -- 38912 before it);
+//      pairs, profiles/r05_regimes_after_ml2p.txt -- 38912 before it, and
+//      still 38912 for the Miller-loop-only entries, ml_one_max());
 //   larger: lane pairs again, two or more waves per SIMD (2^16: 16.7 ms
 //      against 17.2 ms one lane; 2^17: 33.0 vs 34.1 ms).  Round 5 gave the
 //      lane-pair final exponentiation the Karabina squarings and the
@@ -59,17 +60,26 @@ size_t one_max() {
     static const size_t v = env_size("PA_ONE_MAX", 34048);
     return v;
 }
+// the same window's upper edge for the reference-form Miller loop alone (the
+// Miller-loop entries: pa_miller_loop_fused_batch_device, pa_multi_miller_loop_affine):
+// its lane-pair kernel is slower than the pairing-only one, so one lane per pairing
+// wins up to 38912 pairs there (profiles/r05_regimes.txt)
+size_t ml_one_max() {
+    static const size_t v = env_size("PA_ML_ONE_MAX", 38912);
+    return v;
+}
 bool use_coop(size_t n) {
     const int v = pairing_variant();
     return v == 2 || v == 4 || (v == 0 && n <= coop_max());
 }
 int coop_vm() { return pairing_variant() == 4 ? 1 : 0; }
-// lanes per pairing of the generated kernels
-int gen_lanes(size_t n) {
+// lanes per pairing of the generated kernels; ml_only: the reference-form Miller
+// loop without a final exponentiation behind it (its own crossover, ml_one_max)
+int gen_lanes(size_t n, bool ml_only = false) {
     const int v = pairing_variant();
     if (v == 1) return 2;
     if (v == 3) return 1;
-    return n <= pair_max() || n > one_max() ? 2 : 1;
+    return n <= pair_max() || n > (ml_only ? ml_one_max() : one_max()) ? 2 : 1;
 }
 // multi-pairings of at most this many pairs multiply their Miller values inside
 // the cooperative final exponentiation (sequential mul12 macros); larger ones
@@ -82,7 +92,7 @@ constexpr int kMaxWnafWindow = 62;
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s, coop_vm());
-    return pa::launch_miller_loop_gen(gen_lanes(n), p, q, out, n, s);
+    return pa::launch_miller_loop_gen(gen_lanes(n, true), p, q, out, n, s);
 }
 // Miller loop of (P_i, G2Prepared_i) pairs: the generated kernel (tools/pgen
 // miller_loop_prepared_prog); PA_ML_PREPARED=hipcc selects round 4's HIP C++
@@ -100,7 +110,8 @@ hipError_t mlp_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_
 // entries themselves keep ml_launch.  PA_PAIRING_ML=ref: ml_launch (A/B).
 hipError_t pairing_ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     static const bool ref = getenv("PA_PAIRING_ML") && strcmp(getenv("PA_PAIRING_ML"), "ref") == 0;
-    if (ref || use_coop(n) || gen_lanes(n) != 2) return ml_launch(p, q, out, n, s);
+    if (use_coop(n)) return ml_launch(p, q, out, n, s);
+    if (ref || gen_lanes(n) != 2) return pa::launch_miller_loop_gen(gen_lanes(n), p, q, out, n, s);
     return pa::launch_miller_loop_pairing_gen(p, q, out, n, s);
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
@@ -364,6 +375,13 @@ int pa_fq_sub_batch(const pa_fq* a, const pa_fq* b, pa_fq* out, size_t n) {
 int pa_fq_inverse_batch(const pa_fq* a, pa_fq* out, uint8_t* ok, size_t n) {
     if (n && !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null ok");
     return host_field_op(pa::OP_FQ_INV, a, nullptr, out, ok, n, 48, 48, 0);
+}
+int pa_fq_from_repr_batch(const pa_fq_repr* repr, pa_fq* out, uint8_t* ok, size_t n) {
+    if (n && !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null ok");
+    return host_field_op(pa::OP_FQ_FROM_REPR, repr, nullptr, out, ok, n, 48, 48, 0);
+}
+int pa_fq_into_repr_batch(const pa_fq* a, pa_fq_repr* out, size_t n) {
+    return host_field_op(pa::OP_FQ_INTO_REPR, a, nullptr, out, nullptr, n, 48, 48, 0);
 }
 int pa_fq2_mul_batch(const pa_fq2* a, const pa_fq2* b, pa_fq2* out, size_t n) {
     return host_field_op(pa::OP_FQ2_MUL, a, b, out, nullptr, n, 96, 96, 0);

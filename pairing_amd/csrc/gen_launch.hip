@@ -39,7 +39,7 @@ struct Workspace {
 };
 
 struct GenDevice {
-    bool loaded = false;
+    bool loaded[kKernels] = {};
     hipModule_t mod[kKernels] = {};
     hipFunction_t fn[kKernels] = {};
     std::vector<Workspace> pool;
@@ -85,59 +85,45 @@ std::string lib_dir() {
 
 size_t wave_bytes();
 
-// Loads every code object or none: on a failure the modules already loaded
-// are unloaded and the next launch tries again.
-hipError_t load(GenDevice& d) {
-    if (d.loaded) return hipSuccess;
-    const std::string dir = lib_dir();
-    hipError_t e = hipSuccess;
-    int k = 0;
-    for (; k < kKernels; k++) {
-        const std::string path = dir + "/" + kFile[k];
-        if ((e = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess) {
-            d.mod[k] = nullptr;
-            g_detail = "generated kernel " + path;
-            break;
-        }
-        if ((e = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) {
-            g_detail = "kernel " + std::string(kName[k]) + " in " + path;
-            k++;  // this module did load
-            break;
-        }
+// Loads the one code object a launch needs, on first use.  Each object loads
+// on its own: a missing or refused file fails only the entries that launch it
+// (the others keep working), and a failed load is retried by the next launch.
+hipError_t load(GenDevice& d, int k) {
+    if (d.loaded[k]) return hipSuccess;
+    const std::string path = lib_dir() + "/" + kFile[k];
+    hipError_t e;
+    if ((e = hipModuleLoad(&d.mod[k], path.c_str())) != hipSuccess) {
+        d.mod[k] = nullptr;
+        g_detail = "generated kernel " + path;
+        return e;
+    }
+    if ((e = hipModuleGetFunction(&d.fn[k], d.mod[k], kName[k])) != hipSuccess) {
+        g_detail = "kernel " + std::string(kName[k]) + " in " + path;
+    } else {
         // the code object states its spill slots per wave: one that needs more
         // workspace than this library allocates (a stale or swapped file,
         // PA_GEN_DIR) would write past its wave's slice -- refuse it
-        {
-            hipDeviceptr_t gp = nullptr;
-            size_t gb = 0;
-            uint32_t need = 0;
-            const std::string sym = std::string(kName[k]) + "_mem_slots";
-            if ((e = hipModuleGetGlobal(&gp, &gb, d.mod[k], sym.c_str())) != hipSuccess || gb != 4 ||
-                (e = hipMemcpyDtoH(&need, gp, 4)) != hipSuccess) {
-                if (e == hipSuccess) e = hipErrorInvalidImage;
-                g_detail = "workspace size symbol " + sym + " in " + path;
-                k++;
-                break;
-            }
-            if ((size_t)need * kSlotBytes > wave_bytes()) {
-                e = hipErrorInvalidImage;
-                g_detail = path + " needs " + std::to_string(need) + " workspace slots per wave, the library allocates " +
-                           std::to_string(wave_bytes() / kSlotBytes) + " (rebuild, or PA_GEN_WS_SLOTS)";
-                k++;
-                break;
-            }
+        hipDeviceptr_t gp = nullptr;
+        size_t gb = 0;
+        uint32_t need = 0;
+        const std::string sym = std::string(kName[k]) + "_mem_slots";
+        if ((e = hipModuleGetGlobal(&gp, &gb, d.mod[k], sym.c_str())) != hipSuccess || gb != 4 ||
+            (e = hipMemcpyDtoH(&need, gp, 4)) != hipSuccess) {
+            if (e == hipSuccess) e = hipErrorInvalidImage;
+            g_detail = "workspace size symbol " + sym + " in " + path;
+        } else if ((size_t)need * kSlotBytes > wave_bytes()) {
+            e = hipErrorInvalidImage;
+            g_detail = path + " needs " + std::to_string(need) + " workspace slots per wave, the library allocates " +
+                       std::to_string(wave_bytes() / kSlotBytes) + " (rebuild, or PA_GEN_WS_SLOTS)";
         }
     }
     if (e != hipSuccess) {
-        for (int j = 0; j < k; j++)
-            if (d.mod[j]) (void)hipModuleUnload(d.mod[j]);
-        for (int j = 0; j < kKernels; j++) {
-            d.mod[j] = nullptr;
-            d.fn[j] = nullptr;
-        }
+        (void)hipModuleUnload(d.mod[k]);
+        d.mod[k] = nullptr;
+        d.fn[k] = nullptr;
         return e;
     }
-    d.loaded = true;
+    d.loaded[k] = true;
     return hipSuccess;
 }
 
@@ -211,8 +197,8 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     std::lock_guard<std::mutex> lock(g_mu);
     GenDevice& d = g_dev[dev];
-    if ((e = load(d)) != hipSuccess) {
-        if (g_detail.empty()) g_detail = "generated kernels in " + lib_dir();
+    if ((e = load(d, which)) != hipSuccess) {
+        if (g_detail.empty()) g_detail = std::string("generated kernel ") + kFile[which] + " in " + lib_dir();
         return e;
     }
     const size_t blocks = (n * kLanes[which] + 63) / 64;

@@ -10,6 +10,10 @@
 
 namespace pa {
 
+// R^2 mod q (fq.rs:33-40), Montgomery: PrimeField::from_repr's multiplier
+__constant__ const uint64_t kFqR2[6] = {0xf4df1f341c341746ULL, 0x0a76e6a609d104f1ULL, 0x8de5476c4c95b6d5ULL,
+                                        0x67eb88a9939d83c0ULL, 0x9a793e85b519952dULL, 0x11988fe592cae3aaULL};
+
 // Fq::mul_assign over a batch, fq.rs:909-960.  Grid-stride so one launch
 // covers any n with a chip-filling grid; PF = 1 software-pipelines the loop:
 // the next element's operands are loaded before the current multiply, so a
@@ -187,6 +191,33 @@ __global__ void __launch_bounds__(64) k_field_op(const uint64_t* __restrict__ a,
             ok[i] = k ? 1 : 0;
         }
         fq_store(out + 6 * i, z);
+    } else if constexpr (OP == OP_FQ_FROM_REPR || OP == OP_FQ_INTO_REPR) {
+        Fq x, z;
+        fq_load(x, a + 6 * i);
+        if constexpr (OP == OP_FQ_FROM_REPR) {
+            // PrimeField::from_repr, fq.rs:747-756: a repr < q (is_valid), times R^2
+            int c = 0;
+#pragma unroll
+            for (int k = 11; k >= 0; k--)
+                if (c == 0 && x.w[k] != q_word(k)) c = x.w[k] < q_word(k) ? -1 : 1;
+            const bool valid = c < 0;
+            Fq r2;
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                r2.w[2 * k] = (uint32_t)kFqR2[k];
+                r2.w[2 * k + 1] = (uint32_t)(kFqR2[k] >> 32);
+            }
+            if (valid) fq_mul(z, x, r2);
+            else fq_zero(z);
+            ok[i] = valid ? 1 : 0;
+        } else {
+            // PrimeField::into_repr, fq.rs:758-775: mont_reduce of the words, a * 1 * R^-1
+            Fq one_raw;
+            fq_zero(one_raw);
+            one_raw.w[0] = 1;
+            fq_mul(z, x, one_raw);
+        }
+        fq_store(out + 6 * i, z);
     } else if constexpr (OP == OP_FQ_POW) {
         Fq x, z;
         fq_load(x, a + 6 * i);
@@ -324,6 +355,8 @@ hipError_t launch_field_op(int op, const uint64_t* a, const uint64_t* b, uint64_
         PA_CASE(OP_FQ_ADD)
         PA_CASE(OP_FQ_SUB)
         PA_CASE(OP_FQ_INV)
+        PA_CASE(OP_FQ_FROM_REPR)
+        PA_CASE(OP_FQ_INTO_REPR)
         PA_CASE(OP_FQ2_MUL)
         PA_CASE(OP_FQ2_SQR)
         PA_CASE(OP_FQ6_MUL)

@@ -1377,8 +1377,13 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
             }
         return v;
     }();
+    // the override is taken whole or not at all: exactly parts - 1 bounds, strictly
+    // descending, each in (0, W) -- otherwise windows would be summed twice or skipped
+    bool use_env = wlo_env.size() + 1 == parts;
+    for (size_t k = 0; use_env && k < wlo_env.size(); k++)
+        use_env = wlo_env[k] > 0 && wlo_env[k] < p.W && (k == 0 || wlo_env[k] < wlo_env[k - 1]);
     auto wlo = [&](uint32_t q) {
-        if (wlo_env.size() + 1 == parts && q + 1 < parts && wlo_env[q] < p.W) return wlo_env[q];
+        if (use_env && q + 1 < parts) return wlo_env[q];
         return q + 1 == parts ? 0u : (uint32_t)(((uint64_t)p.W * (parts - 1 - q)) / parts);
     };
     for (uint32_t q = 0; q < parts && err == hipSuccess; q++) {

@@ -299,6 +299,9 @@ def wnaf_fixed_base_exact(group, base, scalars, out, window, workspace, stream=N
     jw = W_G1 if group == 1 else W_G2
     n = scalars.shape[0]
     _rows(out, n, "out")
+    _rows(base, 1, "base")
+    if base.shape[0] != 1:
+        raise ValueError("base: expected exactly one record, got %d" % base.shape[0])
     call("pa_g%d_wnaf_fixed_base_exact_device" % group, _dptr(base, jw, "base"), _dptr(scalars, 4, "scalars"),
          _dptr(out, jw, "out"), n, int(window), ctypes.c_void_p(workspace.data_ptr()), workspace.numel(),
          _stream_ptr(stream))
@@ -310,6 +313,9 @@ def wnaf_fixed_scalar_exact(group, bases, scalar, out, window, workspace, stream
     jw = W_G1 if group == 1 else W_G2
     n = bases.shape[0]
     _rows(out, n, "out")
+    _rows(scalar, 1, "scalar")
+    if scalar.shape[0] != 1:
+        raise ValueError("scalar: expected exactly one record, got %d" % scalar.shape[0])
     call("pa_g%d_wnaf_fixed_scalar_exact_device" % group, _dptr(bases, jw, "bases"), n,
          _dptr(scalar, 4, "scalar"), _dptr(out, jw, "out"), int(window), ctypes.c_void_p(workspace.data_ptr()),
          workspace.numel(), _stream_ptr(stream))

@@ -15,7 +15,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"pa_gen_final_exp": "final_exponentiation", "pa_gen_miller_loop": "miller_loop_fused",
-        "pa_gen_final_exp2": "final_exponentiation_lane_pairs", "pa_gen_miller_loop2": "miller_loop_fused_lane_pairs"}
+        "pa_gen_final_exp2": "final_exponentiation_lane_pairs", "pa_gen_miller_loop2": "miller_loop_fused_lane_pairs",
+        "pa_gen_miller_loop2p": "miller_loop_fused_lane_pairs_pairing_only"}
 
 
 def load(path, counter):
