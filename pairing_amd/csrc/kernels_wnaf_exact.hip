@@ -28,9 +28,20 @@
 //   a point of small order: B outside G1) raises a flag in the workspace and
 //   k_wx_serial replays the reference's chain on one lane instead; both
 //   paths are stream-ordered, no host round trip.
-//   k_wx_fixed_base_mul  per scalar: wnaf_form into a digit-major scratch
-//                        column, then wnaf_exp over the table.
+//   k_wx_table_fl        the finished table converted once to the lazy
+//                        28-bit core's limbs (fl.h: 14 x u32 per Fq, R = 2^392)
+//   k_wx_fixed_base_mul_fl  per scalar: wnaf_form's nonzero digits into a
+//                        packed digit-major column, then wnaf_exp on the lazy
+//                        core (curve_fl.h / curve_fl2.h: dbl-2009-l and
+//                        add-2007-bl with the reference's field-value
+//                        sequence), the coordinates canonical at the store --
+//                        the same Jacobian words as the 12-word kernel
+//                        (k_wx_fixed_base_mul, PA_WX_MUL=word12 for A/B)
+#include <cstring>
+
 #include "curve.h"
+#include "curve_fl2.h"
+#include "dec_quad.h"
 #include "launch.h"
 #include "wnaf_exact_consts.h"
 
@@ -92,6 +103,49 @@ PA_DEV int wnaf_digits(const uint64_t* s, int window, int32_t* d, size_t stride)
     return len;
 }
 
+// wnaf_form as above, keeping only the nonzero digits, in increasing position
+// order, each packed as (digit << 9) | position (positions < kWxMaxDigits <
+// 512, |digit| < 2^20): at most wx_max_nonzero(window) entries at d[k stride]
+PA_DEV int wnaf_nonzero(const uint64_t* s, int window, int32_t* d, size_t stride) {
+    uint64_t c0 = s[0], c1 = s[1], c2 = s[2], c3 = s[3];
+    const uint64_t mod_mask = (1ull << (window + 1)) - 1;
+    const int64_t half = (int64_t)1 << window;
+    int pos = 0, cnt = 0;
+    while ((c0 | c1 | c2 | c3) != 0) {
+        if (c0 & 1) {
+            int64_t u = (int64_t)(c0 & mod_mask);
+            if (u > half) u -= (int64_t)1 << (window + 1);
+            if (u > 0) {
+                const uint64_t t = (uint64_t)u;
+                const uint64_t b0 = c0 < t;
+                c0 -= t;
+                const uint64_t b1 = c1 < b0;
+                c1 -= b0;
+                const uint64_t b2 = c2 < b1;
+                c2 -= b1;
+                c3 -= b2;
+            } else {
+                const uint64_t t = (uint64_t)(-u);
+                c0 += t;
+                const uint64_t k0 = c0 < t;
+                c1 += k0;
+                const uint64_t k1 = k0 && c1 == 0;
+                c2 += k1;
+                const uint64_t k2 = k1 && c2 == 0;
+                c3 += k2;
+            }
+            d[(size_t)cnt * stride] = (int32_t)(((uint32_t)(int32_t)u << 9) | (uint32_t)pos);
+            cnt++;
+        }
+        pos++;
+        c0 = (c0 >> 1) | (c1 << 63);
+        c1 = (c1 >> 1) | (c2 << 63);
+        c2 = (c2 >> 1) | (c3 << 63);
+        c3 >>= 1;
+    }
+    return cnt;
+}
+
 // wnaf_exp (wnaf.rs:45-71): entry e of the table at table + 3W estride e (u64),
 // digit j at d[j dstride]
 template <int G>
@@ -115,6 +169,48 @@ PA_DEV void wnaf_exp(Jac<typename Wx<G>::F>& r, const uint64_t* table, size_t es
         }
     }
 }
+
+// ---------------- lazy-core helpers (G1: curve_fl.h, G2: curve_fl2.h) ----------------
+// table entry layout of k_wx_table_fl: x, y, z as lazy limbs, padded to 16-byte
+// pieces (G1: 42 -> 48 u32, G2: 84 -> 96 u32)
+template <int G> struct WxL;
+template <> struct WxL<1> {
+    using J = FlJac;
+    static constexpr int EW = 48;
+};
+template <> struct WxL<2> {
+    using J = FlJac2;
+    static constexpr int EW = 96;
+};
+
+PA_DEV void wl_put(uint32_t* e, const F<1>& a) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) e[i] = a.w[i];
+}
+PA_DEV void wl_put(uint32_t* e, const F2<1>& a) {
+    wl_put(e, a.c0);
+    wl_put(e + 14, a.c1);
+}
+PA_DEV void wl_get(F<1>& a, const uint32_t* e) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) a.w[i] = e[i];
+}
+PA_DEV void wl_get(F2<1>& a, const uint32_t* e) {
+    wl_get(a.c0, e);
+    wl_get(a.c1, e + 14);
+}
+PA_DEV void wl_load(F<1>& a, const uint64_t* p) { a = fl_load(p); }
+PA_DEV void wl_load(F2<1>& a, const uint64_t* p) { a = fl2_load(p); }
+PA_DEV bool wl_zero_test(const F<1>& a) { return fl_is_zero(a); }
+PA_DEV bool wl_zero_test(const F2<1>& a) { return f2_is_zero(a); }
+PA_DEV void wl_double(FlJac& p) { fl_jac_double(p); }
+PA_DEV void wl_double(FlJac2& p) { fl2_jac_double(p); }
+PA_DEV void wl_add(FlJac& s, const FlJac& o) { fl_jac_add(s, o); }
+PA_DEV void wl_add(FlJac2& s, const FlJac2& o) { fl2_jac_add(s, o); }
+PA_DEV void wl_store(uint64_t* p, const FlJac& a) { fl_store_jac(p, a); }
+PA_DEV void wl_store(uint64_t* p, const FlJac2& a) { fl2_store_jac(p, a); }
+PA_DEV void wl_set_zero(FlJac& r) { r = {fl_zero(), fl_one(), fl_zero()}; }   // ec.rs:224-230
+PA_DEV void wl_set_zero(FlJac2& r) { r = fl2_jac_zero(); }
 
 // ---------------- fixed scalar ----------------
 __global__ void __launch_bounds__(64) k_wx_scalar_digits(const uint64_t* __restrict__ scalar, int window,
@@ -200,6 +296,50 @@ __global__ void __launch_bounds__(64) k_wx_affine(const uint64_t* __restrict__ b
     store(aff + (size_t)2 * W * k + W, a.y);
 }
 
+// the same affine multiples on the lazy core (curve_fl.h / curve_fl2.h), the
+// inversion of z by the 12-word binary GCD (bgcd.h); the affine values do not
+// depend on the chain, so any exact group law gives the same words
+PA_DEV bool wl_inverse(F<1>& r, const F<1>& a) {
+    Fq t;
+    const bool ok = fq_inv(t, fl_to_abi(a));
+    r = fl_from_abi(t);
+    return ok;
+}
+PA_DEV bool wl_inverse(F2<1>& r, const F2<1>& a) {   // fq2.rs:138-155
+    F<1> t;
+    const bool ok = wl_inverse(t, sop(a.c0, a.c0, a.c1, a.c1));
+    r = {mul(a.c0, t), mul(red(neg(a.c1)), t)};
+    return ok;
+}
+PA_DEV void wl_store1(uint64_t* p, const F<1>& a) { fl_store(p, a); }
+PA_DEV void wl_store1(uint64_t* p, const F2<1>& a) { fl2_store(p, a); }
+PA_DEV FlJac wl_load_jac(const uint64_t* p, FlJac*) { return fl_load_jac(p); }
+PA_DEV FlJac2 wl_load_jac(const uint64_t* p, FlJac2*) { return fl2_load_jac(p); }
+
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_affine_fl(const uint64_t* __restrict__ base, size_t N,
+                                                     uint64_t* __restrict__ aff, uint64_t* __restrict__ meta) {
+    constexpr int W = Wx<G>::W;
+    using J = typename WxL<G>::J;
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N || meta[5 * W]) return;   // a zero B or D: the serial chain runs instead
+    const J b = wl_load_jac(base, (J*)nullptr);
+    J r = b;
+    const uint64_t m = 2 * (uint64_t)k + 1;
+    for (int bit = 62 - __builtin_clzll(m); bit >= 0; bit--) {
+        if (!wl_zero_test(r.z)) wl_double(r);
+        if ((m >> bit) & 1) wl_add(r, b);
+    }
+    decltype(r.z) zi;
+    if (!wl_inverse(zi, r.z)) {   // (2k + 1) B = 0: B has small order
+        meta[5 * W] = 1;
+        return;
+    }
+    const auto zi2 = sqr(zi);
+    wl_store1(aff + (size_t)2 * W * k, mul(r.x, zi2));
+    wl_store1(aff + (size_t)2 * W * k + W, mul(r.y, mul(zi2, zi)));
+}
+
 template <int G>
 __global__ void __launch_bounds__(64) k_wx_coef(const uint64_t* __restrict__ base, const uint64_t* __restrict__ aff,
                                                 size_t N, uint64_t* __restrict__ coef, uint64_t* __restrict__ meta) {
@@ -276,6 +416,58 @@ __global__ void __launch_bounds__(64) k_wx_scan(const uint64_t* __restrict__ cin
     store(cout + (size_t)W * i, v);
 }
 
+// The scan step on the lazy core.  G1: one element per lane QUAD, its
+// exponentiation spread over the quad (dec_quad.h: a dependent product is ~0.6
+// us instead of ~1.6 us on the 12-word core), a 4-bit sliding window over the
+// same exponent, so the same field value v * p^(3^(2^s)).
+__global__ void __launch_bounds__(256) k_wx_scan_q1(const uint64_t* __restrict__ cin, uint64_t* __restrict__ cout,
+                                                    size_t N, size_t off, int s, const uint64_t* __restrict__ meta) {
+    const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    if (i >= N || meta[5 * 6]) return;   // whole quads leave together
+    const int lane = threadIdx.x & 63;
+    Fq v;
+    load(v, cin + 6 * i);
+    if (i >= off) {
+        const dq::Lc l = dq::lctx(lane, 1);
+        Fq p;
+        load(p, cin + 6 * (i - off));
+        const uint64_t* e = PA_WX_E1[s];
+        const dq::Q<1> t = dq::pow_fixed(dq::from_abi(p, l), e, top_bit(e), l);
+        v = dq::to_abi(dq::mul(dq::from_abi(v, l), t, l));
+    }
+    if ((lane & 3) == 0) store(cout + 6 * i, v);
+}
+
+// G2: one element per lane on the lazy core's Fq2 (tower_fl.h), z^(e0 + e1 q)
+// = z^e0 conj(z)^e1 over one run of squarings, as pow3 above
+__global__ void __launch_bounds__(64) k_wx_scan_fl2(const uint64_t* __restrict__ cin, uint64_t* __restrict__ cout,
+                                                    size_t N, size_t off, int s, const uint64_t* __restrict__ meta) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N || meta[5 * 12]) return;
+    if (i < off) {
+        for (int j = 0; j < 12; j++) cout[12 * i + j] = cin[12 * i + j];
+        return;
+    }
+    const F2<1> z = fl2_load(cin + 12 * (i - off));
+    const F2<1> zc = red(conj(z));
+    const F2<1> zz = mul(z, zc);
+    const uint64_t* e0 = PA_WX_E2[s][0];
+    const uint64_t* e1 = PA_WX_E2[s][1];
+    const int t0 = top_bit(e0), t1 = top_bit(e1);
+    F2<1> r = f2_one();
+    bool started = false;
+    for (int b = t0 > t1 ? t0 : t1; b >= 0; b--) {
+        if (started) r = sqr(r);
+        const bool x0 = (e0[b >> 6] >> (b & 63)) & 1, x1 = (e1[b >> 6] >> (b & 63)) & 1;
+        if (x0 || x1) {
+            const F2<1>& f = x0 && x1 ? zz : (x0 ? z : zc);
+            r = started ? mul(r, f) : f;
+            started = true;
+        }
+    }
+    fl2_store(cout + 12 * i, mul(fl2_load(cin + 12 * i), r));
+}
+
 template <int G>
 __global__ void __launch_bounds__(64) k_wx_finish(const uint64_t* __restrict__ base, const uint64_t* __restrict__ aff,
                                                   const uint64_t* __restrict__ zs, size_t N,
@@ -334,6 +526,91 @@ __global__ void __launch_bounds__(64) k_wx_fixed_base_mul(const uint64_t* __rest
     store_jac(out + (size_t)JW * i, r);
 }
 
+
+// ---------------- fixed base: the multiply on the lazy core ----------------
+template <int G>
+__global__ void __launch_bounds__(64) k_wx_table_fl(const uint64_t* __restrict__ table, size_t N,
+                                                    uint32_t* __restrict__ tfl) {
+    constexpr int W = Wx<G>::W, EW = WxL<G>::EW, L = 14 * (W / 6);
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    typename WxL<G>::J t;
+    wl_load(t.x, table + (size_t)3 * W * k);
+    wl_load(t.y, table + (size_t)3 * W * k + W);
+    wl_load(t.z, table + (size_t)3 * W * k + 2 * W);
+    uint32_t e[EW];
+    wl_put(e, t.x);
+    wl_put(e + L, t.y);
+    wl_put(e + 2 * L, t.z);
+#pragma unroll
+    for (int j = 3 * L; j < EW; j++) e[j] = 0;
+    uint4* dst = reinterpret_cast<uint4*>(tfl + (size_t)EW * k);
+#pragma unroll
+    for (int j = 0; j < EW / 4; j++) dst[j] = make_uint4(e[4 * j], e[4 * j + 1], e[4 * j + 2], e[4 * j + 3]);
+}
+
+template <int G>
+PA_DEV typename WxL<G>::J wl_entry(const uint32_t* __restrict__ tfl, int e) {
+    constexpr int EW = WxL<G>::EW, L = 14 * G;
+    const uint4* src = reinterpret_cast<const uint4*>(tfl + (size_t)EW * e);
+    uint32_t v[EW];
+#pragma unroll
+    for (int j = 0; j < EW / 4; j++) {
+        const uint4 x = src[j];
+        v[4 * j] = x.x;
+        v[4 * j + 1] = x.y;
+        v[4 * j + 2] = x.z;
+        v[4 * j + 3] = x.w;
+    }
+    typename WxL<G>::J t;
+    wl_get(t.x, v);
+    wl_get(t.y, v + L);
+    wl_get(t.z, v + 2 * L);
+    return t;
+}
+
+// wnaf_exp (wnaf.rs:45-71) over the packed nonzero digits: the reference's
+// loop doubles once per digit position below the first nonzero one and adds
+// (or subtracts, sub_assign = add of the negation, ec.rs:528-532) the entry of
+// each nonzero digit.  double() and negate() leave a zero point's words as they
+// are (ec.rs:298-300, 556-560): tested on z, as is_zero does.
+// G1: at most 256 registers (VGPR + AGPR), so two waves share a SIMD
+template <int G>
+__global__ void __launch_bounds__(64, G == 1 ? 2 : 1) k_wx_fixed_base_mul_fl(const uint32_t* __restrict__ tfl,
+                                                             const uint64_t* __restrict__ scalars, size_t n,
+                                                             int window, int32_t* __restrict__ digits,
+                                                             uint64_t* __restrict__ out) {
+    constexpr int JW = 3 * Wx<G>::W;
+    using J = typename WxL<G>::J;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t* d = digits + i;
+    const int cnt = wnaf_nonzero(scalars + 4 * i, window, d, n);
+    J r;
+    wl_set_zero(r);
+    int prev = -1;
+    for (int k = cnt - 1; k >= 0; k--) {
+        const int32_t pk = d[(size_t)k * n];
+        const int pos = pk & 511, v = pk >> 9;
+        for (int j = prev - pos; prev >= 0 && j > 0; j--)
+            if (!wl_zero_test(r.z)) wl_double(r);
+        J t = wl_entry<G>(tfl, (v > 0 ? v : -v) >> 1);
+        if (v < 0 && !wl_zero_test(t.z)) t.y = red(neg(t.y));
+        wl_add(r, t);
+        prev = pos;
+    }
+    for (int j = prev; j > 0; j--)
+        if (!wl_zero_test(r.z)) wl_double(r);
+    wl_store(out + (size_t)JW * i, r);
+}
+
+// PA_WX_MUL=word12: the round-5 multiply on the 12-word core (A/B); its
+// dense digit column needs the larger workspace (wx_layout)
+bool wx_mul_word12() {
+    static const bool v = getenv("PA_WX_MUL") && strcmp(getenv("PA_WX_MUL"), "word12") == 0;
+    return v;
+}
+
 template <int G>
 hipError_t wx_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t* out, size_t n, int window,
                          void* workspace, hipStream_t stream) {
@@ -349,19 +626,36 @@ hipError_t wx_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t
     int32_t* digits = reinterpret_cast<int32_t*>(ws + L.digits);
     const unsigned gb = blocks_for(N, 64);
     hipLaunchKernelGGL(k_wx_prep<G>, dim3(1), dim3(64), 0, stream, base, meta);
-    hipLaunchKernelGGL(k_wx_affine<G>, dim3(gb), dim3(64), 0, stream, base, N, aff, meta);
+    if (wx_mul_word12())
+        hipLaunchKernelGGL(k_wx_affine<G>, dim3(gb), dim3(64), 0, stream, base, N, aff, meta);
+    else
+        hipLaunchKernelGGL(k_wx_affine_fl<G>, dim3(gb), dim3(64), 0, stream, base, N, aff, meta);
     hipLaunchKernelGGL(k_wx_coef<G>, dim3(gb), dim3(64), 0, stream, base, aff, N, c0, meta);
     int s = 0;
     for (size_t off = 1; off < N; off <<= 1, s++) {
-        hipLaunchKernelGGL(k_wx_scan<G>, dim3(gb), dim3(64), 0, stream, c0, c1, N, off, s, meta);
+        if (wx_mul_word12())
+            hipLaunchKernelGGL(k_wx_scan<G>, dim3(gb), dim3(64), 0, stream, c0, c1, N, off, s, meta);
+        else if constexpr (G == 1)
+            hipLaunchKernelGGL(k_wx_scan_q1, dim3(blocks_for(4 * N, 256)), dim3(256), 0, stream, c0, c1, N, off, s,
+                               meta);
+        else
+            hipLaunchKernelGGL(k_wx_scan_fl2, dim3(gb), dim3(64), 0, stream, c0, c1, N, off, s, meta);
         uint64_t* t = c0;
         c0 = c1;
         c1 = t;
     }
     hipLaunchKernelGGL(k_wx_finish<G>, dim3(gb), dim3(64), 0, stream, base, aff, c0, N, table, meta);
     hipLaunchKernelGGL(k_wx_serial<G>, dim3(1), dim3(64), 0, stream, base, N, table, meta);
-    if (n) hipLaunchKernelGGL(k_wx_fixed_base_mul<G>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table, scalars, n,
-                              window, digits, out);
+    if (n == 0) return hipGetLastError();
+    if (wx_mul_word12()) {
+        hipLaunchKernelGGL(k_wx_fixed_base_mul<G>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, table, scalars, n,
+                           window, digits, out);
+    } else {
+        uint32_t* tfl = reinterpret_cast<uint32_t*>(ws + L.tfl);
+        hipLaunchKernelGGL(k_wx_table_fl<G>, dim3(gb), dim3(64), 0, stream, table, N, tfl);
+        hipLaunchKernelGGL(k_wx_fixed_base_mul_fl<G>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, tfl, scalars, n,
+                           window, digits, out);
+    }
     (void)W;
     return hipGetLastError();
 }
@@ -402,7 +696,9 @@ WxLayout wx_layout(int group, size_t n, int window) {
     L.c1 = at;
     at = align256(at + 8 * W * N);
     L.digits = at;
-    at = align256(at + 4 * (size_t)kWxMaxDigits * n);
+    at = align256(at + 4 * (size_t)(wx_mul_word12() ? kWxMaxDigits : wx_max_nonzero(window)) * n);
+    L.tfl = at;
+    at = align256(at + (wx_mul_word12() ? 0 : 4 * (size_t)(group == 1 ? WxL<1>::EW : WxL<2>::EW) * N));
     L.bytes = at;
     return L;
 }

@@ -30,6 +30,8 @@ enum FieldOp : int {
     OP_FQ6_FROB,
     OP_FQ_POW,     // b = exponent words (device), param = their count
     OP_FQ12_POW,
+    OP_FQ_FROM_REPR,   // ok = 0 (Err(NotInField)) and out = 0 for a repr >= q
+    OP_FQ_INTO_REPR,
 };
 
 // Generic elementwise field op: out[i] = op(a[i], b[i]); `ok` (may be null)
@@ -199,8 +201,11 @@ constexpr int kWxMaxWindow = 20;         // fixed base: 2^19 table entries, int3
 constexpr int kWxMaxScalarWindow = 12;   // fixed scalar: a table per base
 constexpr int kWxMaxDigits = 260;        // wnaf_form of a 256-bit repr: at most 257 digits
 struct WxLayout {
-    size_t meta, table, aff, c0, c1, digits, bytes;
+    size_t meta, table, aff, c0, c1, digits, tfl, bytes;
 };
+// nonzero wNAF digits of one scalar at window w: nonzero digits sit at least
+// w + 1 positions apart among the < kWxMaxDigits positions
+constexpr int wx_max_nonzero(int w) { return kWxMaxDigits / (w + 1) + 1; }
 WxLayout wx_layout(int group, size_t n, int window);
 WxLayout wx_scalar_layout(int group, size_t n, int window);
 hipError_t launch_wnaf_exact_fixed_base(int group, const uint64_t* base, const uint64_t* scalars, uint64_t* out,
