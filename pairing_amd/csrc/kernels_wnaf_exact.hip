@@ -247,7 +247,34 @@ __global__ void __launch_bounds__(64) k_wx_fixed_scalar(const uint64_t* __restri
 }
 
 // ---------------- fixed base: the table ----------------
-// meta (u64): [0, 3W) D, [3W, 4W) x_D, [4W, 5W) 2 Z_D^3, [5W] special-step flag
+// Y^2 == X^3 + b Z^6 (b = 4, ec.rs:885-887; G2: 4 (u + 1), ec.rs:1557-1562)
+PA_DEV void times_b(Fq& r, const Fq& a) {
+    dbl(r, a);
+    dbl(r, r);
+}
+PA_DEV void times_b(Fq2& r, const Fq2& a) {
+    mul_by_nonresidue(r, a);
+    dbl(r, r);
+    dbl(r, r);
+}
+template <class F>
+PA_DEV bool jac_on_curve(const Jac<F>& p) {
+    F y2, x3, z6, t;
+    sqr(y2, p.y);
+    sqr(x3, p.x);
+    mul(x3, x3, p.x);
+    sqr(z6, p.z);
+    sqr(t, z6);
+    mul(z6, t, z6);
+    times_b(t, z6);
+    add(x3, x3, t);
+    return eq(y2, x3);
+}
+
+// meta (u64): [0, 3W) D, [3W, 4W) x_D, [4W, 5W) 2 Z_D^3, [5W] special-step flag,
+// [5W + 1] B is a nonzero point on the curve: E(Fq) and E'(Fq2) have odd order
+// (cofactor times r), so no point of the chain has order 2 and a doubling of a
+// nonzero point is nonzero -- the multiply then tests for zero only after adds
 template <int G>
 __global__ void __launch_bounds__(64) k_wx_prep(const uint64_t* __restrict__ base, uint64_t* __restrict__ meta) {
     using F = typename Wx<G>::F;
@@ -270,6 +297,7 @@ __global__ void __launch_bounds__(64) k_wx_prep(const uint64_t* __restrict__ bas
         store(meta + 4 * W, k2);
     }
     meta[5 * W] = flag;
+    meta[5 * W + 1] = !jac_is_zero(b) && jac_on_curve(b) ? 1 : 0;
 }
 
 // affine (2k + 1) B for k < N (a plain double-and-add: affine values do not
@@ -438,6 +466,183 @@ __global__ void __launch_bounds__(256) k_wx_scan_q1(const uint64_t* __restrict__
     if ((lane & 3) == 0) store(cout + 6 * i, v);
 }
 
+// Two scan steps s, s + 1 in one launch (radix 4), for the steps whose
+// exponents are reduced modulo q - 1 (full size): with a = 2^s,
+//   C_i <- C_i C_(i-a)^(E_s) C_(i-2a)^(E_(s+1)) C_(i-3a)^(E_s E_(s+1))
+// (a term whose index is negative is absent), the same value the two
+// Hillis-Steele steps give; the three powers share one run of squarings
+// (Straus, a 4-bit sliding window per exponent): ~630 products against ~930.
+PA_DEV int ebit(const uint64_t* e, int b) { return (int)((e[b >> 6] >> (b & 63)) & 1); }
+PA_DEV dq::Q<1> pick8(const dq::Q<1> (&t)[8], int k) {
+    switch (k) {
+        case 0: return t[0];
+        case 1: return t[1];
+        case 2: return t[2];
+        case 3: return t[3];
+        case 4: return t[4];
+        case 5: return t[5];
+        case 6: return t[6];
+        default: return t[7];
+    }
+}
+PA_DEV void odd_powers(dq::Q<1> (&t)[8], const dq::Q<1>& x, const dq::Lc& l) {
+    t[0] = x;
+    const dq::Q<1> x2 = dq::sqr(x, l);
+#pragma unroll
+    for (int k = 1; k < 8; k++) t[k] = dq::mul(t[k - 1], x2, l);
+}
+// a 4-bit window of e opens at bit b (e's bit b set): its low end and value
+PA_DEV void open_window(const uint64_t* e, int b, int& lo, int& v) {
+    int L = b - 3 < 0 ? 0 : b - 3;
+    while (!ebit(e, L)) L++;
+    int val = 0;
+    for (int c = b; c >= L; c--) val = 2 * val + ebit(e, c);
+    lo = L;
+    v = val;
+}
+PA_DEV dq::Q<1> pow_multi3(const dq::Q<1>& x0, const dq::Q<1>& x1, const dq::Q<1>& x2, const uint64_t* e0,
+                           const uint64_t* e1, const uint64_t* e2, const dq::Lc& l) {
+    dq::Q<1> t0[8], t1[8], t2[8];
+    odd_powers(t0, x0, l);
+    odd_powers(t1, x1, l);
+    odd_powers(t2, x2, l);
+    int top = top_bit(e0);
+    top = top_bit(e1) > top ? top_bit(e1) : top;
+    top = top_bit(e2) > top ? top_bit(e2) : top;
+    int lo0 = -1, lo1 = -1, lo2 = -1, v0 = 0, v1 = 0, v2 = 0;
+    bool started = false;
+    dq::Q<1> acc = x0;
+    auto close = [&](const dq::Q<1> (&t)[8], int v) {
+        const dq::Q<1> f = pick8(t, v >> 1);
+        acc = started ? dq::mul(acc, f, l) : f;
+        started = true;
+    };
+#pragma unroll 1
+    for (int b = top; b >= 0; b--) {
+        if (lo0 < 0 && ebit(e0, b)) open_window(e0, b, lo0, v0);
+        if (lo1 < 0 && ebit(e1, b)) open_window(e1, b, lo1, v1);
+        if (lo2 < 0 && ebit(e2, b)) open_window(e2, b, lo2, v2);
+        if (started) acc = dq::sqr(acc, l);
+        if (lo0 == b) {
+            close(t0, v0);
+            lo0 = -1;
+        }
+        if (lo1 == b) {
+            close(t1, v1);
+            lo1 = -1;
+        }
+        if (lo2 == b) {
+            close(t2, v2);
+            lo2 = -1;
+        }
+    }
+    return acc;
+}
+
+__global__ void __launch_bounds__(256) k_wx_scan4_q1(const uint64_t* __restrict__ cin, uint64_t* __restrict__ cout,
+                                                     size_t N, size_t a, int s, const uint64_t* __restrict__ meta) {
+    const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    if (i >= N || meta[5 * 6]) return;   // whole quads leave together
+    const int lane = threadIdx.x & 63;
+    Fq v;
+    load(v, cin + 6 * i);
+    if (i >= a) {
+        const dq::Lc l = dq::lctx(lane, 1);
+        const dq::Q<1> one = dq::qconst(FL_ONE, l);
+        Fq p;
+        load(p, cin + 6 * (i - a));
+        const dq::Q<1> x0 = dq::from_abi(p, l);
+        dq::Q<1> x1 = one, x2 = one;
+        if (i >= 2 * a) {
+            load(p, cin + 6 * (i - 2 * a));
+            x1 = dq::from_abi(p, l);
+        }
+        if (i >= 3 * a) {
+            load(p, cin + 6 * (i - 3 * a));
+            x2 = dq::from_abi(p, l);
+        }
+        const dq::Q<1> t = pow_multi3(x0, x1, x2, PA_WX_E1[s], PA_WX_E1[s + 1], PA_WX_E1T[s], l);
+        v = dq::to_abi(dq::mul(dq::from_abi(v, l), t, l));
+    }
+    if ((lane & 3) == 0) store(cout + 6 * i, v);
+}
+
+// The radix-4 step one element per LANE on the lazy core's one-lane leaves:
+// 512 waves for 2^15 entries leave half the SIMDs idle and a lone wave's
+// product is ~1.1 us, but a quad product costs 2.5x the issue slots and the
+// quad form of these steps is issue-bound at two waves per SIMD
+// (PA_WX_SCAN4=quad selects it for A/B)
+PA_DEV F<1> pick8(const F<1> (&t)[8], int k) {
+    switch (k) {
+        case 0: return t[0];
+        case 1: return t[1];
+        case 2: return t[2];
+        case 3: return t[3];
+        case 4: return t[4];
+        case 5: return t[5];
+        case 6: return t[6];
+        default: return t[7];
+    }
+}
+PA_DEV void odd_powers(F<1> (&t)[8], const F<1>& x) {
+    t[0] = x;
+    const F<1> x2 = sqr(x);
+#pragma unroll
+    for (int k = 1; k < 8; k++) t[k] = mul(t[k - 1], x2);
+}
+PA_DEV F<1> pow_multi3(const F<1>& x0, const F<1>& x1, const F<1>& x2, const uint64_t* e0, const uint64_t* e1,
+                       const uint64_t* e2) {
+    F<1> t0[8], t1[8], t2[8];
+    odd_powers(t0, x0);
+    odd_powers(t1, x1);
+    odd_powers(t2, x2);
+    int top = top_bit(e0);
+    top = top_bit(e1) > top ? top_bit(e1) : top;
+    top = top_bit(e2) > top ? top_bit(e2) : top;
+    int lo0 = -1, lo1 = -1, lo2 = -1, v0 = 0, v1 = 0, v2 = 0;
+    bool started = false;
+    F<1> acc = x0;
+    auto close = [&](const F<1> (&t)[8], int v) {
+        const F<1> f = pick8(t, v >> 1);
+        acc = started ? mul(acc, f) : f;
+        started = true;
+    };
+#pragma unroll 1
+    for (int b = top; b >= 0; b--) {
+        if (lo0 < 0 && ebit(e0, b)) open_window(e0, b, lo0, v0);
+        if (lo1 < 0 && ebit(e1, b)) open_window(e1, b, lo1, v1);
+        if (lo2 < 0 && ebit(e2, b)) open_window(e2, b, lo2, v2);
+        if (started) acc = sqr(acc);
+        if (lo0 == b) {
+            close(t0, v0);
+            lo0 = -1;
+        }
+        if (lo1 == b) {
+            close(t1, v1);
+            lo1 = -1;
+        }
+        if (lo2 == b) {
+            close(t2, v2);
+            lo2 = -1;
+        }
+    }
+    return acc;
+}
+__global__ void __launch_bounds__(64) k_wx_scan4_fl1(const uint64_t* __restrict__ cin, uint64_t* __restrict__ cout,
+                                                     size_t N, size_t a, int s, const uint64_t* __restrict__ meta) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N || meta[5 * 6]) return;
+    if (i < a) {
+        for (int j = 0; j < 6; j++) cout[6 * i + j] = cin[6 * i + j];
+        return;
+    }
+    const F<1> x0 = fl_load(cin + 6 * (i - a));
+    const F<1> x1 = i >= 2 * a ? fl_load(cin + 6 * (i - 2 * a)) : fl_one();
+    const F<1> x2 = i >= 3 * a ? fl_load(cin + 6 * (i - 3 * a)) : fl_one();
+    const F<1> t = pow_multi3(x0, x1, x2, PA_WX_E1[s], PA_WX_E1[s + 1], PA_WX_E1T[s]);
+    fl_store(cout + 6 * i, mul(fl_load(cin + 6 * i), t));
+}
+
 // G2: one element per lane on the lazy core's Fq2 (tower_fl.h), z^(e0 + e1 q)
 // = z^e0 conj(z)^e1 over one run of squarings, as pow3 above
 __global__ void __launch_bounds__(64) k_wx_scan_fl2(const uint64_t* __restrict__ cin, uint64_t* __restrict__ cout,
@@ -579,28 +784,39 @@ template <int G>
 __global__ void __launch_bounds__(64, G == 1 ? 2 : 1) k_wx_fixed_base_mul_fl(const uint32_t* __restrict__ tfl,
                                                              const uint64_t* __restrict__ scalars, size_t n,
                                                              int window, int32_t* __restrict__ digits,
+                                                             const uint64_t* __restrict__ meta,
                                                              uint64_t* __restrict__ out) {
-    constexpr int JW = 3 * Wx<G>::W;
+    constexpr int W = Wx<G>::W, JW = 3 * W;
     using J = typename WxL<G>::J;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const bool on_curve = meta[5 * W + 1] != 0;
     int32_t* d = digits + i;
     const int cnt = wnaf_nonzero(scalars + 4 * i, window, d, n);
     J r;
     wl_set_zero(r);
+    bool rz = true;   // r is zero (z == 0)
+    auto doublings = [&](int m) {
+        if (on_curve) {
+            if (!rz)
+                for (int j = m; j > 0; j--) wl_double(r);
+        } else {
+            for (int j = m; j > 0; j--)
+                if (!wl_zero_test(r.z)) wl_double(r);
+        }
+    };
     int prev = -1;
     for (int k = cnt - 1; k >= 0; k--) {
         const int32_t pk = d[(size_t)k * n];
         const int pos = pk & 511, v = pk >> 9;
-        for (int j = prev - pos; prev >= 0 && j > 0; j--)
-            if (!wl_zero_test(r.z)) wl_double(r);
+        if (prev >= 0) doublings(prev - pos);
         J t = wl_entry<G>(tfl, (v > 0 ? v : -v) >> 1);
         if (v < 0 && !wl_zero_test(t.z)) t.y = red(neg(t.y));
         wl_add(r, t);
+        rz = wl_zero_test(r.z);
         prev = pos;
     }
-    for (int j = prev; j > 0; j--)
-        if (!wl_zero_test(r.z)) wl_double(r);
+    if (prev > 0) doublings(prev);
     wl_store(out + (size_t)JW * i, r);
 }
 
@@ -608,6 +824,16 @@ __global__ void __launch_bounds__(64, G == 1 ? 2 : 1) k_wx_fixed_base_mul_fl(con
 // dense digit column needs the larger workspace (wx_layout)
 bool wx_mul_word12() {
     static const bool v = getenv("PA_WX_MUL") && strcmp(getenv("PA_WX_MUL"), "word12") == 0;
+    return v;
+}
+
+bool wx_scan4_quad() {
+    static const bool v = getenv("PA_WX_SCAN4") && strcmp(getenv("PA_WX_SCAN4"), "quad") == 0;
+    return v;
+}
+// PA_WX_RADIX4=0: radix-2 steps only (A/B)
+bool wx_radix4() {
+    static const bool v = !(getenv("PA_WX_RADIX4") && atoi(getenv("PA_WX_RADIX4")) == 0);
     return v;
 }
 
@@ -633,6 +859,22 @@ hipError_t wx_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t
     hipLaunchKernelGGL(k_wx_coef<G>, dim3(gb), dim3(64), 0, stream, base, aff, N, c0, meta);
     int s = 0;
     for (size_t off = 1; off < N; off <<= 1, s++) {
+        if constexpr (G == 1) {
+            // radix 4 where both steps' exponents are full size (3^(2^s) > q)
+            if (!wx_mul_word12() && wx_radix4() && s >= 8 && 2 * off < N) {
+                if (wx_scan4_quad())
+                    hipLaunchKernelGGL(k_wx_scan4_q1, dim3(blocks_for(4 * N, 256)), dim3(256), 0, stream, c0, c1, N,
+                                       off, s, meta);
+                else
+                    hipLaunchKernelGGL(k_wx_scan4_fl1, dim3(gb), dim3(64), 0, stream, c0, c1, N, off, s, meta);
+                uint64_t* t = c0;
+                c0 = c1;
+                c1 = t;
+                off <<= 1;
+                s++;
+                continue;
+            }
+        }
         if (wx_mul_word12())
             hipLaunchKernelGGL(k_wx_scan<G>, dim3(gb), dim3(64), 0, stream, c0, c1, N, off, s, meta);
         else if constexpr (G == 1)
@@ -654,7 +896,7 @@ hipError_t wx_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t
         uint32_t* tfl = reinterpret_cast<uint32_t*>(ws + L.tfl);
         hipLaunchKernelGGL(k_wx_table_fl<G>, dim3(gb), dim3(64), 0, stream, table, N, tfl);
         hipLaunchKernelGGL(k_wx_fixed_base_mul_fl<G>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, tfl, scalars, n,
-                           window, digits, out);
+                           window, digits, meta, out);
     }
     (void)W;
     return hipGetLastError();
@@ -686,7 +928,7 @@ WxLayout wx_layout(int group, size_t n, int window) {
     WxLayout L;
     size_t at = 0;
     L.meta = at;
-    at = align256(at + 8 * (5 * W + 1));
+    at = align256(at + 8 * (5 * W + 2));
     L.table = at;
     at = align256(at + 8 * 3 * W * N);
     L.aff = at;
