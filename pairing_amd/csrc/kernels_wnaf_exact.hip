@@ -285,7 +285,11 @@ __global__ void __launch_bounds__(64) k_wx_prep(const uint64_t* __restrict__ bas
     d = b;
     jac_double(d);
     store_jac(meta, d);
-    uint64_t flag = jac_is_zero(b) || jac_is_zero(d) ? 1 : 0;
+    // the closed form recombines (2k + 1) B from another addition chain, which
+    // gives the serial chain's values only where the group law holds: a base off
+    // the curve takes the serial chain too
+    const bool on_curve = !jac_is_zero(b) && jac_on_curve(b);
+    uint64_t flag = jac_is_zero(b) || jac_is_zero(d) || !on_curve ? 1 : 0;
     if (!flag) {
         Aff<F> a;
         jac_to_affine(a, d);
@@ -297,7 +301,7 @@ __global__ void __launch_bounds__(64) k_wx_prep(const uint64_t* __restrict__ bas
         store(meta + 4 * W, k2);
     }
     meta[5 * W] = flag;
-    meta[5 * W + 1] = !jac_is_zero(b) && jac_on_curve(b) ? 1 : 0;
+    meta[5 * W + 1] = on_curve ? 1 : 0;
 }
 
 // affine (2k + 1) B for k < N (a plain double-and-add: affine values do not

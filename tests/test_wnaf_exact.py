@@ -11,7 +11,7 @@ and the add_nocarry wrap (wnaf.rs:30-35) at every window tested."""
 import numpy as np
 import pytest
 
-from helpers import RMONT, R_ORDER, limbs, random_scalars, rng
+from helpers import RMONT, R_ORDER, limbs, random_fq, random_scalars, rng
 
 NT = 8
 
@@ -100,6 +100,20 @@ def test_fixed_base_exact_special_bases(gpu, oracle, group):
     for b in cases:
         for w in (2, 5):
             _check_fixed_base(gpu, oracle, group, np.ascontiguousarray(b), s, w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", [1, 2])
+def test_fixed_base_exact_off_curve_bases(gpu, oracle, group):
+    """Jacobian words that are not a curve point (the reference computes its
+    chain on them all the same): the serial chain, and the multiply with a zero
+    test before every doubling"""
+    g = rng(355 + group)
+    s = _edge_scalars(g, 40)
+    jw = 18 if group == 1 else 36
+    base = random_fq(g, jw // 6).reshape(1, jw)
+    for w in (1, 3, 6):
+        _check_fixed_base(gpu, oracle, group, np.ascontiguousarray(base), s, w)
 
 
 @pytest.mark.gpu
