@@ -331,6 +331,22 @@ class Prog:
         assert self.lanes == 2
         return self._cse("sel", [a, b], max(a.u, b.u), vb=max(a.vb, b.vb))
 
+    def bcast(self, a, r):
+        """lane r's value of a in both lanes of the pair (one v_mov_b32_dpp per
+        limb, quad_perm [r, r, r + 2, r + 2])"""
+        assert self.lanes == 2 and r in (0, 1)
+        return self._cse("bcast", [a], a.u, imm=r, vb=a.vb)
+
+    def pairz(self, a):
+        """lane 0: -(lane 1's a) (C - a1, C the subtraction constant of a's
+        bound), lane 1: its own a -- sel(neg(swap(a)), a) as one op: a v_sub_u32
+        and a v_cndmask_b32_dpp (quad_perm swap, VCC = the odd-lane mask) per limb"""
+        assert self.lanes == 2
+        self._full(a)
+        key = self.sub_key(a)
+        cu, cv = self.sub_bounds(key)
+        return self._cse("pairz", [a], max(cu, a.u), imm=key, vb=max(cv, a.vb) if self.use_norm else None)
+
     def const(self, x):
         """field element x (plain integer) as a canonical Fl constant"""
         return self._op("const", [], 1, imm=to_mont_limbs(x % Q))
@@ -782,6 +798,11 @@ def evaluate(prog, inputs, stats=None, trace=None):
             r = [s[0][1 - ln] for ln in range(L)]
         elif k == "sel":
             r = [s[ln][ln] for ln in range(L)]
+        elif k == "bcast":
+            r = [s[0][op.imm] for ln in range(L)]
+        elif k == "pairz":
+            c = SUBC[op.imm]
+            r = [tuple(ci - b for ci, b in zip(c, s[0][1])), s[0][1]]
         elif k == "dppadd":
             r = [tuple(x + y for x, y in zip(s[0][op.imm[ln]], s[1][ln])) for ln in range(L)]
         elif k in ("wsop", "wnorm"):

@@ -644,6 +644,35 @@ class Emitter:
         for i in range(NL):
             self.i("v_add_u32_dpp", d + i, a + i, b + i, perm)
 
+    def emit_bcast(self, a, d, r):
+        self.i("s_nop", 1)   # VALU write -> DPP read of the same VGPR: 2 wait states
+        for i in range(NL):
+            self.i("v_mov_b32_dpp_bcast", d + i, a + i, r)
+
+    def emit_pairz(self, a, d, key):
+        """d = C - a (every lane), then d = VCC ? a : d of the partner lane
+        (v_cndmask_b32_dpp, VCC = the odd lanes): lane 0 gets C - a1, lane 1
+        its a.  The cndmask of limb i comes three instructions after the sub
+        that writes limb i (a DPP read needs two wait states after the VALU
+        write) and the cndmasks alternate with the subs (back-to-back VOP2
+        cndmasks reading VCC issue at ~19 clk on a lone wave,
+        profiles/r03_issue_probe.txt).  d must not alias a."""
+        c = SUBC[key]
+        self.i("s_mov_b64", VCC, S(S_ODD))
+        seq = [("s", 0), ("s", 1), ("s", 2)]
+        for i in range(NL):
+            seq.append(("c", i))
+            if i + 3 < NL:
+                seq.append(("s", i + 3))
+        at = {}
+        for n, (kind, i) in enumerate(seq):
+            if kind == "s":
+                self.i("v_sub_u32", d + i, K(c[i]), a + i)
+                at[i] = n
+            else:
+                assert n - at[i] - 1 >= 2
+                self.i("v_cndmask_b32_dpp_swap", d + i, d + i, a + i)
+
     def emit_sel(self, a, b, d):
         for i in range(NL):
             self.i("v_cndmask_b32_e64", d + i, a + i, b + i, S(S_ODD))
@@ -1167,7 +1196,7 @@ class Emitter:
             # in place over a dying source (safe for every op kind below)
             dk = None
             for vs, kk in zip(srcs, sk):
-                if (vs in dying and self.vslot[kk] is vs and k not in ("swap", "dppadd")
+                if (vs in dying and self.vslot[kk] is vs and k not in ("swap", "dppadd", "bcast", "pairz")
                         and not (k in ("sub", "csub") and op.srcs[0].id == op.srcs[1].id)):
                     dk = kk
                     break
@@ -1227,6 +1256,10 @@ class Emitter:
             self.emit_swap(base[0], d)
         elif k == "sel":
             self.emit_sel(base[0], base[1], d)
+        elif k == "bcast":
+            self.emit_bcast(base[0], d, op.imm)
+        elif k == "pairz":
+            self.emit_pairz(base[0], d, op.imm)
         elif k == "dppadd":
             self.emit_dppadd(base[0], base[1], d, op.imm)
         elif k == "selz":
@@ -1288,7 +1321,7 @@ class Emitter:
 
     # ---------------- prefetch ----------------
     COST = {"sop": None, "sqr": 460, "red": 62, "norm": 39, "add": 14, "add3": 14, "shladd": 14, "shl": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
-            "sel": 14, "dppadd": 15, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14, "tload": 7, "tnext": 2,
+            "sel": 14, "dppadd": 15, "bcast": 15, "pairz": 29, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14, "tload": 7, "tnext": 2,
             "selz": 80, "binv": 33000}
     # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
     AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}

@@ -101,6 +101,13 @@ class Renderer:
                 o[0], o[1], o[2], q[0], q[1], q[0] + 2, q[1] + 2)]
         if m == "v_mov_b32_dpp_swap":
             return ["v_mov_b32_dpp %s, %s quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" % (o[0], o[1])]
+        if m == "v_mov_b32_dpp_bcast":
+            r = a[2]
+            return ["v_mov_b32_dpp %s, %s quad_perm:[%d,%d,%d,%d] row_mask:0xf bank_mask:0xf" % (
+                o[0], o[1], r, r, r + 2, r + 2)]
+        if m == "v_cndmask_b32_dpp_swap":
+            return ["v_cndmask_b32_dpp %s, %s, %s, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" % (
+                o[0], o[1], o[2])]
         if m == "ds_write_b64":
             return ["ds_write_b64 %s, %s offset:%d" % (o[0], o[1], a[2])]
         if m == "ds_read_b64":

@@ -50,7 +50,7 @@ class Sim:
     # gfx950: a VALU read of an SGPR (mask, carry-in or operand) must come two
     # wait states after a VALU instruction wrote it (LLVM inserts s_nop 1 there)
     VALU_SW = {"v_mad_u64_u32": "vcc", "v_mad_i64_i32": "vcc", "v_sub_co_u32": "vcc", "v_subb_co_u32": "vcc"}
-    VALU_SR = {"v_cndmask_b32": "vcc", "v_subb_co_u32": "vcc"}
+    VALU_SR = {"v_cndmask_b32": "vcc", "v_subb_co_u32": "vcc", "v_cndmask_b32_dpp_swap": "vcc"}
 
     def hazard(self, t):
         m, a = t[0], t[1:]
@@ -201,6 +201,19 @@ class Sim:
                     src = {ln: self.vf[ln][t[2]] for ln in self.lanes}
                     for ln in self.lanes:
                         self.vf[ln][t[1]] = src[ln ^ 1] if (ln ^ 1) in src else 0
+                    nxt = None
+                elif m == "v_mov_b32_dpp_bcast":
+                    src = {ln: self.vf[ln][t[2]] for ln in self.lanes}
+                    for ln in self.lanes:
+                        self.vf[ln][t[1]] = src[(ln & ~1) | t[3]]
+                    nxt = None
+                elif m == "v_cndmask_b32_dpp_swap":
+                    # lane ln: VCC ? its own src1 : src0 of its partner lane
+                    src = {ln: self.vf[ln][t[2]] for ln in self.lanes}
+                    val = {ln: self.vf[ln][t[3]] if self.vcc_of(ln) else (src[ln ^ 1] if (ln ^ 1) in src else 0)
+                           for ln in self.lanes}
+                    for ln in self.lanes:
+                        self.vf[ln][t[1]] = val[ln]
                     nxt = None
                 elif m == "v_add_u32_dpp":
                     # lane ln reads src0 from lane (ln & ~1) | perm[ln & 1] of its pair

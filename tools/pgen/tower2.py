@@ -18,6 +18,9 @@ PREP_REUSE = os.environ.get("PGEN_PREP_REUSE", "1") == "1"
 DPP_ADD = os.environ.get("PGEN_DPP_ADD", "1") == "1"
 SQR_NORM = os.environ.get("PGEN_SQR_NORM", "1") == "1"
 PAIR_SUM = os.environ.get("PGEN_PAIR_SUM", "0") == "1"   # measured: more live pairs, more spills
+# mul2's operand pair by a DPP broadcast and a fused negate + DPP select (42
+# instructions) instead of swap, negate and two selects (56)
+PAIR_DPP = os.environ.get("PGEN_PAIR_DPP", "1") == "1"
 MUL2_USES = {}       # value id -> mul2 operand uses, from a first build (two_pass)
 MUL2_COUNT = None
 SWAPPED = set()      # value ids whose partner swap a first build formed (outside xi)
@@ -100,10 +103,13 @@ class Tower2(Tower):
     def _prepped(self, a):
         """a's operand pair (x, z) of mul2 is already formed in this block"""
         memo = self.p.cur.__dict__.get("memo", {})
-        return ("swap", (a.id,), None) in memo or (id(self.p.cur), a.id) in self.pairs
+        return (not PAIR_DPP and ("swap", (a.id,), None) in memo) or (id(self.p.cur), a.id) in self.pairs
 
     def _pair_direct(self, a):
         p = self.p
+        if PAIR_DPP:
+            # a0 on both lanes (one DPP broadcast); -a1 | a1 (a sub and a DPP select)
+            return p.bcast(a, 0), p.pairz(a)
         oa = p.swap(a)
         return p.sel(a, oa), p.sel(p.neg(oa), a)     # a0 on both lanes; -a1 | a1
 
@@ -117,7 +123,7 @@ class Tower2(Tower):
     def _pair_cost(self, a):
         if self._prepped(a):
             return 0
-        return 28 if self._summed(a) is not None else 56
+        return 28 if self._summed(a) is not None else (42 if PAIR_DPP else 56)
 
     def _pair_fits(self, x, z, b):
         p = self.p
@@ -160,7 +166,7 @@ class Tower2(Tower):
         p = self.p
         if SUBCU[a.u] * b.u > a.u * SUBCU[b.u]:
             a, b = b, a
-        # the (x, z) pair costs 56 instructions, the partner swap of b 14: let
+        # the (x, z) pair costs 42 (56) instructions, the partner swap of b 14: let
         # the operand whose pair is already formed be a -- or, neither being
         # formed, the one more products will use (MUL2_USES, a first build's
         # count) -- if the bounds allow
