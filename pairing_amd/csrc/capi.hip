@@ -106,13 +106,14 @@ hipError_t mlp_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_
 // pa_multi_pairing_device): on lane pairs the pairing-only kernel, whose Miller
 // values differ from the reference's by Fq2 factors that the final
 // exponentiation removes ((q^12 - 1) / r is a multiple of q^2 - 1) -- 3.5 %
-// fewer instructions (tools/pgen/kernels.py doubling_step_h).  The Miller-loop
-// entries themselves keep ml_launch.  PA_PAIRING_ML=ref: ml_launch (A/B).
+// fewer instructions (tools/pgen/kernels.py doubling_step_h); round 6: one lane
+// per pairing too (pa_gen_miller_loop1p).  The Miller-loop entries themselves
+// keep ml_launch.  PA_PAIRING_ML=ref: the reference-form kernels (A/B).
 hipError_t pairing_ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     static const bool ref = getenv("PA_PAIRING_ML") && strcmp(getenv("PA_PAIRING_ML"), "ref") == 0;
     if (use_coop(n)) return ml_launch(p, q, out, n, s);
-    if (ref || gen_lanes(n) != 2) return pa::launch_miller_loop_gen(gen_lanes(n), p, q, out, n, s);
-    return pa::launch_miller_loop_pairing_gen(p, q, out, n, s);
+    if (ref) return pa::launch_miller_loop_gen(gen_lanes(n), p, q, out, n, s);
+    return pa::launch_miller_loop_pairing_gen(gen_lanes(n), p, q, out, n, s);
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s, coop_vm());

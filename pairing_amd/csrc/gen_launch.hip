@@ -28,7 +28,7 @@
 namespace pa {
 namespace {
 
-constexpr int kKernels = 7;
+constexpr int kKernels = 8;
 constexpr size_t kSlotBytes = 3584;  // one 14-limb spill slot for a 64-lane wave
 
 struct Workspace {
@@ -53,21 +53,23 @@ thread_local std::string g_detail;   // the code object that failed to load, for
 // loop of a batch against one shared G2Prepared (a line table in place of a1);
 // 5: the Miller loop of (P_i, G2Prepared_i) pairs, a1 = the prepared records;
 // 6: the pairing-only lane-pair Miller loop (e(P, Q) paths: its Miller values
-// differ from the reference's by Fq2 factors the final exponentiation removes)
+// differ from the reference's by Fq2 factors the final exponentiation removes);
+// 7: the same one lane per pairing
 const char* const kFile[kKernels] = {"pa_gen_miller_loop.hsaco", "pa_gen_final_exp.hsaco",
                                      "pa_gen_miller_loop2.hsaco", "pa_gen_final_exp2.hsaco",
                                      "pa_gen_miller_loop_shared.hsaco", "pa_gen_miller_loop_prepared.hsaco",
-                                     "pa_gen_miller_loop2p.hsaco"};
+                                     "pa_gen_miller_loop2p.hsaco", "pa_gen_miller_loop1p.hsaco"};
 const char* const kName[kKernels] = {"pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2",
                                      "pa_gen_final_exp2", "pa_gen_miller_loop_shared",
-                                     "pa_gen_miller_loop_prepared", "pa_gen_miller_loop2p"};
+                                     "pa_gen_miller_loop_prepared", "pa_gen_miller_loop2p", "pa_gen_miller_loop1p"};
 const size_t kWaveBytes[kKernels] = {PA_GEN_MILLER_LOOP_MEM_SLOTS * kSlotBytes, PA_GEN_FINAL_EXP_MEM_SLOTS * kSlotBytes,
                                      PA_GEN_MILLER_LOOP2_MEM_SLOTS * kSlotBytes,
                                      PA_GEN_FINAL_EXP2_MEM_SLOTS * kSlotBytes,
                                      PA_GEN_MILLER_LOOP_SHARED_MEM_SLOTS * kSlotBytes,
                                      PA_GEN_MILLER_LOOP_PREPARED_MEM_SLOTS * kSlotBytes,
-                                     PA_GEN_MILLER_LOOP2P_MEM_SLOTS * kSlotBytes};
-const int kLanes[kKernels] = {1, 1, 2, 2, 1, 1, 2};
+                                     PA_GEN_MILLER_LOOP2P_MEM_SLOTS * kSlotBytes,
+                                     PA_GEN_MILLER_LOOP1P_MEM_SLOTS * kSlotBytes};
+const int kLanes[kKernels] = {1, 1, 2, 2, 1, 1, 2, 1};
 
 // PA_GEN_DIR (A/B experiments with alternative generated code objects) overrides
 // the directory of libpairing_amd.so; PA_GEN_WS_SLOTS raises the workspace size
@@ -250,9 +252,9 @@ hipError_t launch_miller_loop_shared_gen(const uint64_t* p_aff, const uint64_t* 
                                          hipStream_t stream) {
     return launch(4, p_aff, prepared, out, n, stream);
 }
-hipError_t launch_miller_loop_pairing_gen(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
-                                          hipStream_t stream) {
-    return launch(6, p_aff, q_aff, out, n, stream);
+hipError_t launch_miller_loop_pairing_gen(int lanes, const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out,
+                                          size_t n, hipStream_t stream) {
+    return launch(lanes == 2 ? 6 : 7, p_aff, q_aff, out, n, stream);
 }
 hipError_t launch_miller_loop_prepared_gen(const uint64_t* p_aff, const uint64_t* prepared, uint64_t* out,
                                            size_t n, hipStream_t stream) {

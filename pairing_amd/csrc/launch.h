@@ -84,7 +84,7 @@ hipError_t launch_miller_loop_shared_gen(const uint64_t* p_aff, const uint64_t* 
 // the pairing-only lane-pair Miller loop (homogeneous G2 steps, own line
 // scaling): for e(P, Q) paths only -- its values equal the reference's Miller
 // values up to Fq2 factors, which the final exponentiation removes
-hipError_t launch_miller_loop_pairing_gen(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
+hipError_t launch_miller_loop_pairing_gen(int lanes, const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                           hipStream_t stream);
 // the generated Miller loop of (P_i, G2Prepared_i) pairs (tools/pgen
 // MillerLoopPreparedCfg): each lane reads its own record's lines

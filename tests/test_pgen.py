@@ -59,6 +59,15 @@ def test_dsl_final_exp_matches_oracle(ref_pair, lanes, lazy):
     assert [out[k] for k in range(12)] == fe
 
 
+def test_dsl_pairing_only_miller_loop_one_lane_gives_the_pairing(ref_pair):
+    """the same on one lane per pairing (pa_gen_miller_loop1p)"""
+    ins, ml, fe = ref_pair
+    f = dsl.evaluate(kernels.miller_loop_prog(pairing_only=True), ins)
+    assert [f[k] for k in range(12)] != ml
+    out = dsl.evaluate(kernels.final_exp_prog(), {k: f[k] for k in range(12)})
+    assert [out[k] for k in range(12)] == fe
+
+
 def test_wide_values_exact():
     """wide products / normalisation / reduction of the lazy tower equal
     their integer meaning (tower.TowerLazy, dsl.wsop/wnorm/wred)"""
@@ -123,7 +132,7 @@ def test_dsl_pairing_only_miller_loop_gives_the_pairing(ref_pair):
     assert [out[k] for k in range(12)] == fe
 
 
-@pytest.mark.parametrize("which", ["ml", "ml2", "ml2p", pytest.param("mlz", marks=_ab_only)])
+@pytest.mark.parametrize("which", ["ml", "ml2", "ml2p", "ml1p", pytest.param("mlz", marks=_ab_only)])
 def test_sim_miller_loop_kernel(which):
     assert sim_check.check(which, debug=True)
 

@@ -98,6 +98,8 @@ PROGRAMS = {
     "ml2p": _mk(__import__("tower2").two_pass(lambda: kernels.miller_loop_prog(lanes=2, pairing_only=True),
                                                xi_dpp=False),
                 kcfg.MillerLoopCfg2p, "pa_gen_miller_loop2p"),
+    # the same on one lane per pairing (the default in (PA_PAIR_MAX, PA_ONE_MAX], variant 3)
+    "ml1p": _mk(lambda: kernels.miller_loop_prog(pairing_only=True), kcfg.MillerLoopCfg1p, "pa_gen_miller_loop1p"),
     # one G2Prepared shared by the whole batch: the line table in place of G2 arithmetic
     "mls": _mk(kernels.miller_loop_shared_prog, kcfg.MillerLoopSharedCfg, "pa_gen_miller_loop_shared"),
     # a G2Prepared per pairing (the north-star call): the lines read from each lane's record
@@ -116,7 +118,7 @@ PROGRAMS = {
 FILES = {"small": "pa_gen_small.hsaco", "cyc": "pa_gen_cyc.hsaco", "ml": "pa_gen_miller_loop.hsaco", "fe": "pa_gen_final_exp.hsaco",
          "mls": "pa_gen_miller_loop_shared.hsaco", "mlp": "pa_gen_miller_loop_prepared.hsaco",
          "fen": "pa_gen_fe_norm.hsaco", "fei": "pa_gen_fe_inv.hsaco",
-         "ml2": "pa_gen_miller_loop2.hsaco", "ml2p": "pa_gen_miller_loop2p.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
+         "ml2": "pa_gen_miller_loop2.hsaco", "ml2p": "pa_gen_miller_loop2p.hsaco", "ml1p": "pa_gen_miller_loop1p.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
          "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco",
          "tdec": "test/pa_gen_tdec.hsaco", "tunit": "test/pa_gen_tunit.hsaco", "tdec2": "test/pa_gen_tdec2.hsaco"}
 
@@ -165,8 +167,9 @@ def write_work_json(outdir):
                            ("fei", "fe_inv", 13), ("mls", "miller_loop_shared", 2),
                            ("mlp", "miller_loop_prepared", 2),
                            ("ml2", "miller_loop_lane_pairs", 6), ("fe2", "final_exp_lane_pairs", 12),
-                           ("ml2p", "miller_loop_lane_pairs_pairing_only", 6)):
-        if key in ("fen", "fei", "mls", "mlp", "ml2", "fe2", "ml2p") and not PROGRAMS[key].cache:
+                           ("ml2p", "miller_loop_lane_pairs_pairing_only", 6),
+                           ("ml1p", "miller_loop_pairing_only", 6)):
+        if key in ("fen", "fei", "mls", "mlp", "ml2", "fe2", "ml2p", "ml1p") and not PROGRAMS[key].cache:
             continue
         prog = PROGRAMS[key]()[0]
         st = dsl.Stats()
@@ -196,20 +199,20 @@ def main():
         del args[i:i + 2]
     os.makedirs(outdir, exist_ok=True)
     meta = {}
-    for w in args or ["ml", "fe", "ml2", "fe2", "mls", "mlp", "ml2p"]:
+    for w in args or ["ml", "fe", "ml2", "fe2", "mls", "mlp", "ml2p", "ml1p"]:
         build(w, outdir)
         meta[w] = PROGRAMS[w].cache["r"][3]
     if "ml" in meta and "fe" in meta or "ml2" in meta and "fe2" in meta:
-        for k in ("ml", "fe", "ml2", "fe2", "mls", "mlp", "ml2p"):
+        for k in ("ml", "fe", "ml2", "fe2", "mls", "mlp", "ml2p", "ml1p"):
             PROGRAMS[k]()   # every program the work file describes
         write_work_json(outdir)
-    if all(k in meta for k in ("ml", "fe", "ml2", "fe2", "mls", "mlp", "ml2p")):
+    if all(k in meta for k in ("ml", "fe", "ml2", "fe2", "mls", "mlp", "ml2p", "ml1p")):
         hdr = os.path.join(ROOT, "pairing_amd", "csrc", "pa_gen_meta.h")
         with open(hdr, "w") as f:
             f.write("// GENERATED by tools/pgen/build_gen.py -- spill workspace per wave (M slots)\n#pragma once\n")
             for k, name in (("ml", "MILLER_LOOP"), ("fe", "FINAL_EXP"), ("ml2", "MILLER_LOOP2"), ("fe2", "FINAL_EXP2"),
                             ("mls", "MILLER_LOOP_SHARED"), ("mlp", "MILLER_LOOP_PREPARED"),
-                            ("ml2p", "MILLER_LOOP2P")):
+                            ("ml2p", "MILLER_LOOP2P"), ("ml1p", "MILLER_LOOP1P")):
                 f.write("#define PA_GEN_%s_MEM_SLOTS %d\n" % (name, meta[k]))
 
 

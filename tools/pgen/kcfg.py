@@ -412,6 +412,12 @@ class MillerLoopCfg2p(MillerLoopCfg2):
     name = "pa_gen_miller_loop2p"
 
 
+class MillerLoopCfg1p(MillerLoopCfg):
+    """the pairing-only one-lane Miller loop (kernels.miller_loop_prog(pairing_only=True)):
+    same records, masks and output slots as MillerLoopCfg"""
+    name = "pa_gen_miller_loop1p"
+
+
 class FinalExpCfg2(FinalExpCfg):
     name = "pa_gen_final_exp2"
     lanes = 2

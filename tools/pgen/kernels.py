@@ -177,8 +177,7 @@ def miller_loop_prog(homes=None, lanes=1, lazy=False, pairing_only=False):
             px, py = p.get("px"), p.get("py")
         else:   # replicate P's coordinates from the packed (px | py) slot
             pk = p.get("px")
-            o = p.swap(pk)
-            px, py = p.sel(pk, o), p.sel(o, pk)
+            px, py = p.bcast(pk, 0), p.bcast(pk, 1)
         V.set12("f", ell(T, V.get12("f"), c, px, py))
 
     with p.loop(62) as L:
