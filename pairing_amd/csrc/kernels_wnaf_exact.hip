@@ -39,6 +39,8 @@
 //                        (k_wx_fixed_base_mul, PA_WX_MUL=word12 for A/B)
 #include <cstring>
 
+#include <hipcub/hipcub.hpp>
+
 #include "curve.h"
 #include "curve_fl2.h"
 #include "dec_quad.h"
@@ -789,14 +791,19 @@ __global__ void __launch_bounds__(64, G == 1 ? 2 : 1) k_wx_fixed_base_mul_fl(con
                                                              const uint64_t* __restrict__ scalars, size_t n,
                                                              int window, int32_t* __restrict__ digits,
                                                              const uint64_t* __restrict__ meta,
+                                                             const uint32_t* __restrict__ perm,
+                                                             const int32_t* __restrict__ cnts,
                                                              uint64_t* __restrict__ out) {
     constexpr int W = Wx<G>::W, JW = 3 * W;
     using J = typename WxL<G>::J;
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const size_t t_ = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t_ >= n) return;
     const bool on_curve = meta[5 * W + 1] != 0;
+    // perm: the scalar this lane takes (k_wx_digit_keys + sort: its digits are
+    // in place already); none: the lane's own scalar, digits formed here
+    const size_t i = perm ? perm[t_] : t_;
     int32_t* d = digits + i;
-    const int cnt = wnaf_nonzero(scalars + 4 * i, window, d, n);
+    const int cnt = perm ? cnts[i] : wnaf_nonzero(scalars + 4 * i, window, d, n);
     J r;
     wl_set_zero(r);
     bool rz = true;   // r is zero (z == 0)
@@ -822,6 +829,34 @@ __global__ void __launch_bounds__(64, G == 1 ? 2 : 1) k_wx_fixed_base_mul_fl(con
     }
     if (prev > 0) doublings(prev);
     wl_store(out + (size_t)JW * i, r);
+}
+
+// Lanes of a wave run the wnaf_exp rounds of their scalars in lockstep: each
+// round costs the wave its longest gap of doublings, ~30 % more doublings than
+// a lane needs for random scalars.  Scalars whose nonzero digits sit at similar
+// positions waste less, so the multiply takes them in the order of a key --
+// the nonzero-digit count, then the positions of the six highest nonzero
+// digits -- sorted by a radix sort (the words of each result are unchanged:
+// out[i] is still scalar i's).  Simulated on random scalars: 353 -> 327
+// doubling-equivalents per lane.
+__global__ void __launch_bounds__(64) k_wx_digit_keys(const uint64_t* __restrict__ scalars, size_t n, int window,
+                                                      int32_t* __restrict__ digits, int32_t* __restrict__ cnts,
+                                                      uint64_t* __restrict__ keys, uint32_t* __restrict__ idx) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t* d = digits + i;
+    const int cnt = wnaf_nonzero(scalars + 4 * i, window, d, n);
+    uint64_t key = (uint64_t)cnt << 54;
+    for (int k = 0; k < 6 && k < cnt; k++) key |= (uint64_t)(d[(size_t)(cnt - 1 - k) * n] & 511) << (45 - 9 * k);
+    cnts[i] = cnt;
+    keys[i] = key;
+    idx[i] = (uint32_t)i;
+}
+
+// PA_WX_SORT=0: the scalars in their own order (A/B)
+bool wx_sort() {
+    static const bool v = !(getenv("PA_WX_SORT") && atoi(getenv("PA_WX_SORT")) == 0);
+    return v;
 }
 
 // PA_WX_MUL=word12: the round-5 multiply on the 12-word core (A/B); its
@@ -899,8 +934,22 @@ hipError_t wx_fixed_base(const uint64_t* base, const uint64_t* scalars, uint64_t
     } else {
         uint32_t* tfl = reinterpret_cast<uint32_t*>(ws + L.tfl);
         hipLaunchKernelGGL(k_wx_table_fl<G>, dim3(gb), dim3(64), 0, stream, table, N, tfl);
+        const uint32_t* perm = nullptr;
+        int32_t* cnts = nullptr;
+        if (wx_sort() && n <= 0x7fffffff) {
+            uint64_t* keys = reinterpret_cast<uint64_t*>(ws + L.keys);
+            uint32_t* idx = reinterpret_cast<uint32_t*>(ws + L.perm);
+            cnts = reinterpret_cast<int32_t*>(ws + L.cnts);
+            hipLaunchKernelGGL(k_wx_digit_keys, dim3(blocks_for(n, 64)), dim3(64), 0, stream, scalars, n, window,
+                               digits, cnts, keys, idx);
+            size_t tmp_bytes = L.sort_tmp_bytes;
+            hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + L.sort_tmp, tmp_bytes, keys, keys + n, idx,
+                                                              idx + n, (int)n, 0, 64, stream);
+            if (e != hipSuccess) return e;
+            perm = idx + n;
+        }
         hipLaunchKernelGGL(k_wx_fixed_base_mul_fl<G>, dim3(blocks_for(n, 64)), dim3(64), 0, stream, tfl, scalars, n,
-                           window, digits, meta, out);
+                           window, digits, meta, perm, cnts, out);
     }
     (void)W;
     return hipGetLastError();
@@ -945,6 +994,19 @@ WxLayout wx_layout(int group, size_t n, int window) {
     at = align256(at + 4 * (size_t)(wx_mul_word12() ? kWxMaxDigits : wx_max_nonzero(window)) * n);
     L.tfl = at;
     at = align256(at + (wx_mul_word12() ? 0 : 4 * (size_t)(group == 1 ? WxL<1>::EW : WxL<2>::EW) * N));
+    // the scalar order of the multiply: keys and indices in and out of the sort
+    L.keys = at;
+    at = align256(at + 2 * 8 * n);
+    L.perm = at;
+    at = align256(at + 2 * 4 * n);
+    L.cnts = at;
+    at = align256(at + 4 * n);
+    L.sort_tmp = at;
+    L.sort_tmp_bytes = 0;
+    if (n && n <= 0x7fffffff)
+        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, L.sort_tmp_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                 (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 64);
+    at = align256(at + L.sort_tmp_bytes);
     L.bytes = at;
     return L;
 }

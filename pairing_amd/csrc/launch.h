@@ -201,7 +201,7 @@ constexpr int kWxMaxWindow = 20;         // fixed base: 2^19 table entries, int3
 constexpr int kWxMaxScalarWindow = 12;   // fixed scalar: a table per base
 constexpr int kWxMaxDigits = 260;        // wnaf_form of a 256-bit repr: at most 257 digits
 struct WxLayout {
-    size_t meta, table, aff, c0, c1, digits, tfl, bytes;
+    size_t meta, table, aff, c0, c1, digits, tfl, keys, perm, cnts, sort_tmp, sort_tmp_bytes, bytes;
 };
 // nonzero wNAF digits of one scalar at window w: nonzero digits sit at least
 // w + 1 positions apart among the < kWxMaxDigits positions
