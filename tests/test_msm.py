@@ -174,13 +174,17 @@ def test_multiexp_crowded_buckets(gpu, oracle, group, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("parts,chunk", [("1", "32"), ("3", "8"), ("8", "16"), ("2", "512")])
-def test_multiexp_window_parts(gpu, oracle, parts, chunk):
+@pytest.mark.parametrize("parts,chunk,wlo", [("1", "32", None), ("3", "8", None), ("8", "16", None), ("2", "512", None),
+                                             ("3", "64", "12,5"), ("2", "64", "3,40"), ("3", "64", "5,10"),
+                                             ("2", "64", "40"), ("2", "64", "0")])
+def test_multiexp_window_parts(gpu, oracle, parts, chunk, wlo):
     """The MSM's launch structure (kernels_msm.hip msm_run): the windows in
     PA_MSM_PARTS parts on side streams, PA_MSM_CHUNK sorted items per lane
     (read once per process, hence a subprocess): small chunks put most buckets
     across several chunks (the continuation pieces), many parts cut chunks at
-    window boundaries; the sum stays the same point (ec.rs:45-85)"""
+    window boundaries; the sum stays the same point (ec.rs:45-85).  PA_MSM_WLO
+    (unequal parts, A/B) is taken whole or not at all: a malformed list (wrong
+    length, not descending, a bound of 0 or >= W) falls back to the even split"""
     import os
     import subprocess
     import sys
@@ -203,6 +207,8 @@ def test_multiexp_window_parts(gpu, oracle, parts, chunk):
         for name, a in (("p1", p1), ("s1", s1), ("p2", p2), ("s2", s2)):
             np.save(os.path.join(d, name + ".npy"), a)
         env = dict(os.environ, PA_MSM_PARTS=parts, PA_MSM_CHUNK=chunk)
+        if wlo is not None:
+            env["PA_MSM_WLO"] = wlo
         r = subprocess.run([sys.executable, "-c", code, d], env=env, capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-3000:]
         o1, o2 = np.load(os.path.join(d, "o1.npy")), np.load(os.path.join(d, "o2.npy"))

@@ -132,7 +132,7 @@ def test_dsl_pairing_only_miller_loop_gives_the_pairing(ref_pair):
     assert [out[k] for k in range(12)] == fe
 
 
-@pytest.mark.parametrize("which", ["ml", "ml2", "ml2p", "ml1p", pytest.param("mlz", marks=_ab_only)])
+@pytest.mark.parametrize("which", ["ml", "ml2", "ml2p", "ml1p", "ml2ps", pytest.param("mlz", marks=_ab_only)])
 def test_sim_miller_loop_kernel(which):
     assert sim_check.check(which, debug=True)
 

@@ -62,6 +62,18 @@ def cyc_probe_prog(iters=None):
     return p
 
 
+def _with(mod, name, value, progf):
+    """progf() with mod.name = value while it builds"""
+    def f():
+        old = getattr(mod, name)
+        setattr(mod, name, value)
+        try:
+            return progf()
+        finally:
+            setattr(mod, name, old)
+    return f
+
+
 def _mk(progf, cfgc, kname):
     cache = {}
 
@@ -98,6 +110,10 @@ PROGRAMS = {
     "ml2p": _mk(__import__("tower2").two_pass(lambda: kernels.miller_loop_prog(lanes=2, pairing_only=True),
                                                xi_dpp=False),
                 kcfg.MillerLoopCfg2p, "pa_gen_miller_loop2p"),
+    # A/B only: ml2p with the signed-operand Fq2 squaring (tower2.SQR_SIGNED)
+    "ml2ps": _mk(_with(__import__("tower2"), "SQR_SIGNED", True, __import__("tower2").two_pass(
+        lambda: kernels.miller_loop_prog(lanes=2, pairing_only=True), xi_dpp=False)),
+        kcfg.MillerLoopCfg2p, "pa_gen_miller_loop2p"),
     # the same on one lane per pairing (the default in (PA_PAIR_MAX, PA_ONE_MAX], variant 3)
     "ml1p": _mk(lambda: kernels.miller_loop_prog(pairing_only=True), kcfg.MillerLoopCfg1p, "pa_gen_miller_loop1p"),
     # one G2Prepared shared by the whole batch: the line table in place of G2 arithmetic
@@ -118,7 +134,7 @@ PROGRAMS = {
 FILES = {"small": "pa_gen_small.hsaco", "cyc": "pa_gen_cyc.hsaco", "ml": "pa_gen_miller_loop.hsaco", "fe": "pa_gen_final_exp.hsaco",
          "mls": "pa_gen_miller_loop_shared.hsaco", "mlp": "pa_gen_miller_loop_prepared.hsaco",
          "fen": "pa_gen_fe_norm.hsaco", "fei": "pa_gen_fe_inv.hsaco",
-         "ml2": "pa_gen_miller_loop2.hsaco", "ml2p": "pa_gen_miller_loop2p.hsaco", "ml1p": "pa_gen_miller_loop1p.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
+         "ml2": "pa_gen_miller_loop2.hsaco", "ml2p": "pa_gen_miller_loop2p.hsaco", "ml1p": "pa_gen_miller_loop1p.hsaco", "ml2ps": "pa_gen_miller_loop2p.hsaco", "fe2": "pa_gen_final_exp2.hsaco",
          "mlz": "pa_gen_miller_loop_lazy.hsaco", "fez": "pa_gen_final_exp_lazy.hsaco",
          "tdec": "test/pa_gen_tdec.hsaco", "tunit": "test/pa_gen_tunit.hsaco", "tdec2": "test/pa_gen_tdec2.hsaco"}
 

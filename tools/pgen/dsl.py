@@ -80,11 +80,14 @@ class Val:
     double-width unreduced product ("wide" value, see Prog.wsop): only its
     limb bound u is tracked here, the value bound of the pair is tracked by
     the code that builds it (tower.py Wide)."""
-    __slots__ = ("id", "u", "half", "vb")
+    __slots__ = ("id", "u", "half", "vb", "sgn")
 
     def __init__(self, id_, u, half=False, vb=None):
         self.id, self.u, self.half = id_, u, half
         self.vb = u if vb is None else vb     # value < vb 2q (full values)
+        # signed (Prog.pdiff): limbs in (-u MASK, u MASK], |value| < vb 2q; only
+        # the second operand of a product may be signed (Prog.mul -> "ssop")
+        self.sgn = False
 
     def __repr__(self):
         return "v%d/u%d%s%s" % (self.id, self.u, "" if self.vb == self.u else "/vb%d" % self.vb,
@@ -158,13 +161,32 @@ class Prog:
     @staticmethod
     def _full(*vals):
         assert not any(v.half for v in vals), "field op on a wide half"
+        assert not any(v.sgn for v in vals), "a signed value is only a product's second operand"
 
     # ---- field ops ----
     def mul(self, a, b):
+        if b.sgn:
+            return self._ssop(a, b)
         self._full(a, b)
         assert a.u * b.u <= COL_BOUND, "mul bound %d*%d" % (a.u, b.u)
         assert a.vb * b.vb <= VB_PROD, "mul value bound %d*%d" % (a.vb, b.vb)
         return self._op("sop", [a, b], 1)
+
+    def _ssop(self, a, b):
+        """a b with b signed (pdiff): the leaf's products by v_mad_i64_i32 into a
+        signed accumulator, arithmetic carries, and q added by the last
+        Montgomery digit (m_13 + 2^28: + R q before the division), so the
+        result (s + m q) / R + q is positive: value in (q - e, 2q + e) for the
+        bounds below -- u = 1, vb = 2 (emit.Emitter.emit_sop signed=True;
+        exact limbs: mont_sop_signed)"""
+        self._full(a)
+        assert not b.half
+        assert a.u * b.u <= 8, "signed product bound %d*%d (the accumulator has 63 bits)" % (a.u, b.u)
+        assert a.u <= 8, "a's limbs must read as signed 32-bit"
+        # |a b| / R < 4 a.vb b.vb q^2 / R ~ 0.0016 a.vb b.vb q: the result stays in
+        # (0, 4q) while a.vb b.vb < 629
+        assert a.vb * b.vb <= VB_PROD, "signed product value bound %d*%d" % (a.vb, b.vb)
+        return self._op("ssop", [a, b], 1, vb=2)
 
     def sop(self, a, b, c, d):
         self._full(a, b, c, d)
@@ -330,6 +352,17 @@ class Prog:
         """lane 0 takes a, lane 1 takes b"""
         assert self.lanes == 2
         return self._cse("sel", [a, b], max(a.u, b.u), vb=max(a.vb, b.vb))
+
+    def pdiff(self, a):
+        """lane 0: a0 - a1 (its own a minus the partner's), lane 1: a0 (the
+        partner's) -- SIGNED limbs, the second operand of an Fq2 squaring's
+        product (tower2.Tower2.sqr2): a v_cndmask_b32_dpp (partner's a | 0) and
+        a v_sub_u32_dpp (a0 - that) per limb"""
+        assert self.lanes == 2
+        self._full(a)
+        v = self._cse("pdiff", [a], a.u, vb=a.vb)
+        v.sgn = True
+        return v
 
     def bcast(self, a, r):
         """lane r's value of a in both lanes of the pair (one v_mov_b32_dpp per
@@ -609,6 +642,34 @@ def mont_sop(pairs):
     return tuple(gen_fl.limbs(out))
 
 
+def val_of_signed(limbs):
+    return sum(int(x) << (28 * i) for i, x in enumerate(limbs))
+
+
+def mont_sop_signed(a, b):
+    """exact limbs of emit_sop(signed=True): (s + m q) / R + q for s = a b with
+    b's limbs signed, m = -s q^-1 mod R (the digits the leaf takes) plus R from
+    the last digit's 2^28 -- every column of the signed 64-bit accumulator checked"""
+    cols = [0] * (2 * NL)
+    for i in range(NL):
+        for j in range(NL):
+            cols[i + j] += a[i] * b[j]
+    s = val_of(a) * val_of_signed(b)
+    m = (-s * pow(Q, -1, R)) % R
+    ml = gen_fl.limbs(m)
+    ml[NL - 1] += 1 << 28
+    t = s + (m + R) * Q
+    assert t % R == 0
+    acc = 0
+    for k in range(2 * NL - 1):
+        acc += cols[k] + sum(ml[i] * QL[k - i] for i in range(max(0, k - NL + 1), min(k, NL - 1) + 1))
+        assert -(1 << 63) <= acc < (1 << 63), "signed column %d overflows" % k
+        acc >>= 28
+    out = t // R
+    assert 0 <= out < R
+    return tuple(gen_fl.limbs(out))
+
+
 def norm_limbs(x):
     """the emitted carry pass: limbs 0..12 below 2^28, the value unchanged"""
     r, c = [], 0
@@ -729,6 +790,8 @@ def evaluate(prog, inputs, stats=None, trace=None):
             return mont_sop(list(zip(s[0::2], s[1::2])))
         if k == "sqr":
             return mont_sop([(s[0], s[0])])
+        if k == "ssop":
+            return mont_sop_signed(s[0], s[1])
         if k == "add":
             return tuple(a + b for a, b in zip(*s))
         if k == "add3":
@@ -803,6 +866,15 @@ def evaluate(prog, inputs, stats=None, trace=None):
         elif k == "pairz":
             c = SUBC[op.imm]
             r = [tuple(ci - b for ci, b in zip(c, s[0][1])), s[0][1]]
+        elif k == "pdiff":
+            r = [tuple(x - y for x, y in zip(s[0][0], s[0][1])), s[0][0]]
+            for ln in range(L):
+                assert all(-op.dst.u * MASK < x <= op.dst.u * MASK for x in r[ln]), "pdiff limb bound"
+                assert abs(val_of_signed(r[ln])) < op.dst.vb * 2 * Q, "pdiff value bound"
+            env[op.dst.id] = r
+            if trace is not None:
+                trace.append((op.dst.id, tuple(r), op))
+            return
         elif k == "dppadd":
             r = [tuple(x + y for x, y in zip(s[0][op.imm[ln]], s[1][ln])) for ln in range(L)]
         elif k in ("wsop", "wnorm"):

@@ -476,25 +476,46 @@ class Emitter:
         return k
 
     # ---------------- ops ----------------
-    def emit_sop(self, pairs, d):
+    def emit_sop(self, pairs, d, signed=False):
+        """signed (dsl.Prog._ssop, one pair, b's limbs signed): the products by
+        v_mad_i64_i32 into a signed accumulator, arithmetic shifts between
+        columns, and the last Montgomery digit + 2^28 (the result + q, so it
+        stays positive); the reduction's products are unsigned either way"""
         first = True
         acc = (ACC, ACC + 1)
+        mad = "v_mad_i64_i32" if signed else "v_mad_u64_u32"
         for k in range(2 * NL - 1):
             for a, b in pairs:
                 for i in range(max(0, k - NL + 1), min(k, NL - 1) + 1):
-                    self.i("v_mad_u64_u32", ACC, a + i, b + k - i, K(0) if first else ACC)
+                    self.i(mad, ACC, a + i, b + k - i, K(0) if first else ACC)
                     first = False
             for i in range(max(0, k - NL + 1), min(k - 1, NL - 1) + 1):
                 self.i("v_mad_u64_u32", ACC, M0 + i, S(SQ + k - i), ACC)
             if k < NL:
                 self.i("v_mul_lo_u32", M0 + k, ACC, S(SQINV))
                 self.i("v_and_b32", M0 + k, K(MASK), M0 + k)
+                if signed and k == NL - 1:
+                    self.i("v_or_b32", M0 + k, K(1 << 28), M0 + k)
                 self.i("v_mad_u64_u32", ACC, M0 + k, S(SQ), ACC)
             else:
                 self.i("v_and_b32", d + k - NL, K(MASK), ACC)
-            self.i("v_lshrrev_b64", ACC, K(28), ACC)
+            self.i("v_ashrrev_i64" if signed else "v_lshrrev_b64", ACC, K(28), ACC)
         self.i("v_mov_b32", d + NL - 1, ACC)
         del acc
+
+    def emit_pdiff(self, a, d):
+        """d = (a0 - a1 | a0), signed limbs: w = VCC ? 0 : partner's a (v15 = 0,
+        VCC = the odd lanes), then d = a of lane 0 (DPP broadcast) - w.  w lives in
+        d; the cndmasks alternate with the subs (back-to-back VOP2 cndmasks issue
+        slowly).  d must not alias a."""
+        self.i("s_mov_b64", VCC, S(S_ODD))
+        self.i("v_mov_b32", 15, K(0))
+        self.i("s_nop", 1)   # VALU write -> DPP read of the same VGPR: 2 wait states
+        for i in range(NL):
+            self.i("v_cndmask_b32_dpp_swap", d + i, a + i, 15)
+            if i:
+                self.i("v_sub_u32_dpp_bcast0", d + i - 1, a + i - 1, d + i - 1)
+        self.i("v_sub_u32_dpp_bcast0", d + NL - 1, a + NL - 1, d + NL - 1)
 
     def emit_red(self, x, d):
         self.i("v_mad_u64_u32", ACC, x + 12, S(SKQ), K(0))
@@ -1196,7 +1217,7 @@ class Emitter:
             # in place over a dying source (safe for every op kind below)
             dk = None
             for vs, kk in zip(srcs, sk):
-                if (vs in dying and self.vslot[kk] is vs and k not in ("swap", "dppadd", "bcast", "pairz")
+                if (vs in dying and self.vslot[kk] is vs and k not in ("swap", "dppadd", "bcast", "pairz", "pdiff")
                         and not (k in ("sub", "csub") and op.srcs[0].id == op.srcs[1].id)):
                     dk = kk
                     break
@@ -1223,6 +1244,10 @@ class Emitter:
             self.emit_sop(list(zip(base[0::2], base[1::2])), d)
         elif k == "sqr":
             self.emit_sop([(base[0], base[0])], d)
+        elif k == "ssop":
+            self.emit_sop([(base[0], base[1])], d, signed=True)
+        elif k == "pdiff":
+            self.emit_pdiff(base[0], d)
         elif k == "red":
             self.emit_red(base[0], d)
         elif k == "norm":
@@ -1321,13 +1346,15 @@ class Emitter:
 
     # ---------------- prefetch ----------------
     COST = {"sop": None, "sqr": 460, "red": 62, "norm": 39, "add": 14, "add3": 14, "shladd": 14, "shl": 14, "sub": 28, "neg": 14, "const": 14, "swap": 15,
-            "sel": 14, "dppadd": 15, "bcast": 15, "pairz": 29, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14, "tload": 7, "tnext": 2,
+            "sel": 14, "dppadd": 15, "bcast": 15, "pairz": 29, "pdiff": 31, "load_raw": 60, "store_raw": 200, "getvar": 0, "setvar": 14, "tload": 7, "tnext": 2,
             "selz": 80, "binv": 33000}
     # instructions of other work that hide the load latency (PGEN_AHEAD_L/_M: experiments)
     AHEAD = {"L": int(os.environ.get("PGEN_AHEAD_L", 40)), "M": int(os.environ.get("PGEN_AHEAD_M", 500))}
     WINDOW = int(os.environ.get("PGEN_WINDOW", 2500))
 
     def op_cost(self, op):
+        if op.kind == "ssop":
+            return 196 * 2 + 71
         if op.kind == "sop":
             return 196 * (len(op.srcs) // 2 + 1) + 70
         if op.kind == "wsop":

@@ -105,6 +105,8 @@ class Renderer:
             r = a[2]
             return ["v_mov_b32_dpp %s, %s quad_perm:[%d,%d,%d,%d] row_mask:0xf bank_mask:0xf" % (
                 o[0], o[1], r, r, r + 2, r + 2)]
+        if m == "v_sub_u32_dpp_bcast0":
+            return ["v_sub_u32_dpp %s, %s, %s quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf" % (o[0], o[1], o[2])]
         if m == "v_cndmask_b32_dpp_swap":
             return ["v_cndmask_b32_dpp %s, %s, %s, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" % (
                 o[0], o[1], o[2])]

@@ -207,6 +207,13 @@ class Sim:
                     for ln in self.lanes:
                         self.vf[ln][t[1]] = src[(ln & ~1) | t[3]]
                     nxt = None
+                elif m == "v_sub_u32_dpp_bcast0":
+                    # lane ln: src0 of the pair's lane 0 minus its own src1
+                    src = {ln: self.vf[ln][t[2]] for ln in self.lanes}
+                    val = {ln: (src[ln & ~1] - self.vf[ln][t[3]]) & 0xffffffff for ln in self.lanes}
+                    for ln in self.lanes:
+                        self.vf[ln][t[1]] = val[ln]
+                    nxt = None
                 elif m == "v_cndmask_b32_dpp_swap":
                     # lane ln: VCC ? its own src1 : src0 of its partner lane
                     src = {ln: self.vf[ln][t[2]] for ln in self.lanes}
@@ -476,7 +483,7 @@ class Sim:
                 if len(self.lanes) == 2:
                     limbs = limbs[self.lanes.index(self.lane)]
                 got = tuple(self.v[a[1] + i] for i in range(14))
-                if got != tuple(limbs):
+                if got != tuple(x & 0xffffffff for x in limbs):   # signed limbs (pdiff) as u32
                     raise AssertionError("first divergence at %r (instr %d): got %s want %s" % (
                         op, self.count, got, tuple(limbs)))
         elif m == "s_waitcnt_lgkm0":

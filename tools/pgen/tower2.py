@@ -21,6 +21,12 @@ PAIR_SUM = os.environ.get("PGEN_PAIR_SUM", "0") == "1"   # measured: more live p
 # mul2's operand pair by a DPP broadcast and a fused negate + DPP select (42
 # instructions) instead of swap, negate and two selects (56)
 PAIR_DPP = os.environ.get("PGEN_PAIR_DPP", "1") == "1"
+# sqr2 with a signed second operand (a0 - a1 | a0): three exchange ops instead
+# of four (dsl.Prog.pdiff / _ssop).  Measured off: the product adds q to stay
+# positive, so its value bound is 2 and the sums after it need full reductions
+# where carry passes did (FE2 +0.1 % instructions, ML2p -0.14 %); built for
+# A/B as build_gen "ml2ps"
+SQR_SIGNED = os.environ.get("PGEN_SQR_SIGNED", "0") == "1"
 MUL2_USES = {}       # value id -> mul2 operand uses, from a first build (two_pass)
 MUL2_COUNT = None
 SWAPPED = set()      # value ids whose partner swap a first build formed (outside xi)
@@ -191,6 +197,11 @@ class Tower2(Tower):
                 a = p.norm_only(a)
             else:
                 a = p.red(a)
+        if SQR_SIGNED:
+            # lane 0: (a1 + a0)(a0 - a1), lane 1: (2 a1) a0; the product adds q
+            # (signed operand), so its value bound is 2
+            x = p.dppadd(a, a, (1, 1))    # a1 + a0 | 2 a1
+            return p.mul(x, p.pdiff(a))
         o = p.swap(a)
         if DPP_ADD:
             x = p.dppadd(a, o, (0, 0))    # o + a0: a0 + a1 | 2 a0, one v_add_u32_dpp per limb
