@@ -85,10 +85,13 @@ int pa_synchronize(void);
  *       kernels_coop.hip: the verifier shape, ~1.6 ms), n <= PA_PAIR_MAX
  *       (32768) on the generated kernels with a lane pair per pairing
  *       (~8.6-9.3 ms), n <= PA_ONE_MAX (34048) on the generated
- *       one-pairing-per-lane kernels (~16.1 ms), larger batches on lane
- *       pairs again, two waves per SIMD (2^16 in ~16.7 ms; tools/pgen: own
- *       register allocation, code objects lib/pa_gen_*.hsaco loaded at
- *       first use)
+ *       one-pairing-per-lane kernels (~15.7 ms), larger batches on lane
+ *       pairs again, two waves per SIMD (2^16 in ~15.7 ms; tools/pgen: own
+ *       register allocation, code objects lib/pa_gen_*.hsaco, each loaded
+ *       at its first use).  e(P, Q) entries (pa_pairing_batch, multi_pairing)
+ *       run the pairing-only Miller loops (lane pairs and, round 6, one lane
+ *       per pairing); the Miller-loop entries keep the reference's values and
+ *       switch from one lane to lane pairs above 38912 (PA_ML_ONE_MAX)
  *   1 = generated kernels with a lane pair per pairing, every size (A/B)
  *   2 = cooperative kernels for every size (A/B, tests)
  *   3 = generated one-pairing-per-lane kernels for every size (A/B, tests)
