@@ -14,7 +14,17 @@ from elfsym import read_u32, symbol_offset
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "pairing_amd", "lib")
-KERNELS = ["pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2", "pa_gen_final_exp2"]
+# every code object the library loads (gen_launch.hip kFile)
+KERNELS = ["pa_gen_miller_loop", "pa_gen_final_exp", "pa_gen_miller_loop2", "pa_gen_final_exp2",
+           "pa_gen_miller_loop_shared", "pa_gen_miller_loop_prepared", "pa_gen_miller_loop2p",
+           "pa_gen_miller_loop1p"]
+
+
+def test_kernel_list_matches_the_loader():
+    with open(os.path.join(ROOT, "pairing_amd", "csrc", "gen_launch.hip")) as f:
+        src = f.read()
+    files = re.search(r"kFile\[kKernels\] = \{(.*?)\};", src, re.S).group(1)
+    assert re.findall(r'"(pa_gen_\w+)\.hsaco"', files) == KERNELS
 
 
 def meta_slots():
