@@ -84,8 +84,11 @@ int pa_synchronize(void);
  *       cooperative kernels (a four-wave quad-VM workgroup per pairing,
  *       kernels_coop.hip: the verifier shape, ~1.6 ms), n <= PA_PAIR_MAX
  *       (32768) on the generated kernels with a lane pair per pairing
- *       (~8.6-9.3 ms), n <= PA_ONE_MAX (34048) on the generated
- *       one-pairing-per-lane kernels (~15.7 ms), larger batches on lane
+ *       (~8.6-9.3 ms), n <= PA_PAIR_MAX + PA_TAIL_MAX (34048; round 6)
+ *       as the first 32768 on lane pairs and the tail on the cooperative
+ *       kernels on a stream forked from the caller's (32769 pairs in
+ *       ~10.8 ms; not under stream capture, where the one-pairing-per-lane
+ *       kernels run the window, ~15.7 ms), larger batches on lane
  *       pairs again, two waves per SIMD (2^16 in ~15.7 ms; tools/pgen: own
  *       register allocation, code objects lib/pa_gen_*.hsaco, each loaded
  *       at its first use).  e(P, Q) entries (pa_pairing_batch, multi_pairing)

@@ -28,11 +28,15 @@ thread_local std::string g_last_error;
 //      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
 //   n <= pair_max() (32768): the generated kernels with a lane pair per
 //      pairing, at most one wave per SIMD: 8.6-9.3 ms whatever n;
+//   n <= pair_max() + tail_max() (34048; round 6): the first 32768 on lane
+//      pairs and the tail on the cooperative kernels on a forked stream
+//      (split_head below; 32769: 10.8 ms instead of 15.7);
 //   n <= one_max() (34048): one lane per pairing (one wave per SIMD at most:
-//      ~16.04 ms, where a second lane-pair wave on a few SIMDs costs 16.1-17.1;
+//      ~15.7 ms, where a second lane-pair wave on a few SIMDs costs 15.6-16.7;
 //      with the pairing-only lane-pair Miller loop lane pairs win from ~34 000
 //      pairs, profiles/r05_regimes_after_ml2p.txt -- 38912 before it, and
-//      still 38912 for the Miller-loop-only entries, ml_one_max());
+//      still 38912 for the Miller-loop-only entries, ml_one_max(), which the
+//      tail split leaves alone);
 //   larger: lane pairs again, two or more waves per SIMD (2^16: 16.7 ms
 //      against 17.2 ms one lane; 2^17: 33.0 vs 34.1 ms).  Round 5 gave the
 //      lane-pair final exponentiation the Karabina squarings and the
@@ -90,6 +94,93 @@ constexpr size_t kCoopProductMax = 16;
 // a digit mod 2^(w+1) in a u64)
 constexpr int kMaxWnafWindow = 62;
 
+// Batches just above pair_max(): n <= pair_max() + tail_max() pairings run as
+// the first pair_max() on lane pairs (one wave per SIMD, ~9.3 ms) and the tail
+// on the cooperative kernels (a workgroup per pairing, latency-bound), the tail
+// on a second stream forked from and joined back into the caller's, so its
+// workgroups run beside the lane-pair waves -- instead of a second lane-pair
+// wave on a few SIMDs (~15.7 ms whatever the tail).  Values are the same
+// whichever kernels run a pairing (final exponentiation output; the
+// pairing-only Miller values differ from the cooperative Miller loop's by Fq2
+// factors, as pa_pairing_miller_loop_batch_device documents).  Not under
+// stream capture (the side stream would join the graph); PA_TAIL_MAX=0 turns
+// it off, PA_TAIL_SERIAL=1 runs the tail on the caller's stream (A/B).
+size_t tail_max() {
+    // profiles/r06_tail/: the forked cooperative tail beats a second lane-pair wave
+    // (15.6-15.7 ms) up to ~1300 pairs: 32769 10.8 ms, 33024 10.6, 33792 13.1,
+    // 34048 14.4, 34816 17.1 (serial tail 10.7 / 10.5 / 19.5 / 20.7 / 23.1)
+    static const size_t v = env_size("PA_TAIL_MAX", 1280);
+    return v;
+}
+struct TailFork {
+    int dev = -1;
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+// a process-wide pool: a call takes a fork, enqueues the fork wait, the tail and
+// the join wait, and gives it back (a wait holds the event's state at the time it
+// is enqueued, so the next call may record the events again)
+std::mutex g_tail_mu;
+std::vector<TailFork*> g_tail_free;
+size_t split_head(size_t n, hipStream_t s) {
+    if (pairing_variant() != 0 || n <= pair_max() || n - pair_max() > tail_max()) return 0;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return 0;
+    return pair_max();
+}
+// a fork whose side stream is ordered after everything enqueued on s (nullptr
+// with PA_TAIL_SERIAL: the tail runs on s)
+hipError_t tail_begin(hipStream_t s, TailFork** out) {
+    static const bool serial = getenv("PA_TAIL_SERIAL") && atoi(getenv("PA_TAIL_SERIAL")) != 0;
+    *out = nullptr;
+    if (serial) return hipSuccess;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    TailFork* f = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_tail_mu);
+        for (size_t i = 0; i < g_tail_free.size(); i++)
+            if (g_tail_free[i]->dev == dev) {
+                f = g_tail_free[i];
+                g_tail_free.erase(g_tail_free.begin() + i);
+                break;
+            }
+    }
+    if (!f) {
+        f = new TailFork;
+        f->dev = dev;
+        if ((e = hipStreamCreateWithFlags(&f->side, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&f->fork, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&f->join, hipEventDisableTiming)) != hipSuccess) {
+            if (f->join) (void)hipEventDestroy(f->join);
+            if (f->fork) (void)hipEventDestroy(f->fork);
+            if (f->side) (void)hipStreamDestroy(f->side);
+            delete f;
+            return e;
+        }
+    }
+    if ((e = hipEventRecord(f->fork, s)) == hipSuccess) e = hipStreamWaitEvent(f->side, f->fork, 0);
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lock(g_tail_mu);
+        g_tail_free.push_back(f);
+        return e;
+    }
+    *out = f;
+    return hipSuccess;
+}
+// s waits for the tail; the fork goes back to the pool
+hipError_t tail_end(hipStream_t s, TailFork* f) {
+    if (!f) return hipSuccess;
+    hipError_t e = hipEventRecord(f->join, f->side);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, f->join, 0);
+    std::lock_guard<std::mutex> lock(g_tail_mu);
+    g_tail_free.push_back(f);
+    return e;
+}
+constexpr size_t kG1Words = sizeof(pa_g1_affine) / 8, kG2Words = sizeof(pa_g2_affine) / 8,
+                 kF12Words = sizeof(pa_fq12) / 8;
+
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s, coop_vm());
     return pa::launch_miller_loop_gen(gen_lanes(n, true), p, q, out, n, s);
@@ -112,11 +203,31 @@ hipError_t mlp_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_
 hipError_t pairing_ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     static const bool ref = getenv("PA_PAIRING_ML") && strcmp(getenv("PA_PAIRING_ML"), "ref") == 0;
     if (use_coop(n)) return ml_launch(p, q, out, n, s);
+    if (const size_t h = split_head(n, s)) {
+        TailFork* f = nullptr;
+        hipError_t e = pa::launch_miller_loop_pairing_gen(2, p, q, out, h, s);
+        if (e == hipSuccess) e = tail_begin(s, &f);
+        if (e == hipSuccess)
+            e = pa::launch_coop_miller_loop(p + h * kG1Words, q + h * kG2Words, out + h * kF12Words, n - h,
+                                            f ? f->side : s, coop_vm());
+        const hipError_t j = tail_end(s, f);
+        return e != hipSuccess ? e : j;
+    }
     if (ref) return pa::launch_miller_loop_gen(gen_lanes(n), p, q, out, n, s);
     return pa::launch_miller_loop_pairing_gen(gen_lanes(n), p, q, out, n, s);
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
     if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s, coop_vm());
+    if (const size_t h = split_head(n, s)) {
+        TailFork* f = nullptr;
+        hipError_t e = pa::launch_final_exp_gen(2, in, out, ok, h, s);
+        if (e == hipSuccess) e = tail_begin(s, &f);
+        if (e == hipSuccess)
+            e = pa::launch_coop_final_exp(in + h * kF12Words, out + h * kF12Words, ok ? ok + h : nullptr, n - h,
+                                          f ? f->side : s, coop_vm());
+        const hipError_t j = tail_end(s, f);
+        return e != hipSuccess ? e : j;
+    }
     return pa::launch_final_exp_gen(gen_lanes(n), in, out, ok, n, s);
 }
 

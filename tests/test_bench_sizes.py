@@ -112,12 +112,13 @@ def test_pairing_device_bit_exact_at_bench_size(gpu, oracle, variant):
     assert (got[inf] == one).all()
 
 
-@pytest.mark.parametrize("n", [2305, 32768, 32769, 34048, 34049])
+@pytest.mark.parametrize("n", [2305, 32768, 32769, 33792, 34048, 34049])
 def test_pairing_default_mid_size_batches(gpu, oracle, n):
     """The default selection's regime boundaries (PA_COOP_MAX < n <= PA_PAIR_MAX:
-    lane pairs at one wave per SIMD; PA_PAIR_MAX < n <= PA_ONE_MAX: one lane per
-    pairing; above: lane pairs at two waves per SIMD) on both sides, every
-    pairing against the oracle"""
+    lane pairs at one wave per SIMD; PA_PAIR_MAX < n <= PA_PAIR_MAX + PA_TAIL_MAX
+    (34048): the first PA_PAIR_MAX on lane pairs and the tail on the cooperative
+    kernels, on a forked stream; above: lane pairs at two waves per SIMD) on
+    both sides, every pairing against the oracle"""
     import torch
     import bench
     import pairing_amd.device as pdev
@@ -127,6 +128,42 @@ def test_pairing_default_mid_size_batches(gpu, oracle, n):
     pdev.pairing(_dev(p_np), _dev(q_np), out, scratch)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_host(out), oracle.pairing(p_np, q_np, _threads()))
+
+
+def test_split_batch_stages_with_zeros_and_infinity(gpu, oracle):
+    """A batch just above PA_PAIR_MAX through the two stages apart: the Miller
+    loop stage (lane pairs for the head, the cooperative kernel on the forked
+    stream for the tail) then the final exponentiation (split the same way) ==
+    the oracle's pairing, with infinity Q on both sides of the split; and the
+    final exponentiation alone over such a batch with zero Miller values in the
+    head and in the tail: ok = 0 / zero output exactly there, in place too"""
+    import torch
+    import bench
+    import pairing_amd.device as pdev
+    n = 32768 + 300
+    p_np, q_np = bench.make_pairs(n, 0, seed=31)
+    for k in (7, 32768 + 3, n - 1):
+        q_np[k, :24] = 0
+        q_np[k, 12:18] = limbs(pow(2, 384, Q))
+        q_np[k, 24] = 1
+    f = pdev.empty_records(n, 72, "cuda:0")
+    out = pdev.empty_records(n, 72, "cuda:0")
+    pdev.pairing_miller_loop(_dev(p_np), _dev(q_np), f)
+    pdev.final_exponentiation(f, out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(out), oracle.pairing(p_np, q_np, _threads()))
+    fv = _host(f)
+    zeros = [11, 32768, 32768 + 299]
+    fv[zeros] = 0
+    exp, ok_exp = oracle.final_exponentiation(fv, _threads())
+    d = _dev(fv)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    pdev.final_exponentiation(d, d, ok)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_host(d), exp)
+    okh = ok.cpu().numpy()
+    np.testing.assert_array_equal(okh, np.asarray(ok_exp, np.uint8))
+    assert (okh[zeros] == 0).all() and okh.sum() == n - len(zeros)
 
 
 def test_pairing_two_streams_concurrently(gpu, oracle):
