@@ -292,6 +292,18 @@ int pa_g1_decode_batch(const uint8_t *enc, size_t n, int compressed, int checked
                        uint8_t *status);
 int pa_g2_decode_batch(const uint8_t *enc, size_t n, int compressed, int checked, pa_g2_affine *out,
                        uint8_t *status);
+/* is_in_correct_subgroup_assuming_on_curve (ec.rs:142-144, r * P == 0) for
+ * affine points: ok[i] = 1 in the subgroup (infinity included), 0 not.
+ * into_affine = into_affine_unchecked + is_on_curve + this check (ec.rs:676-684,
+ * 786-793, 1323-1331, 1449-1457); for compressed encodings the unchecked
+ * decode already rejects points off the curve, so decode(checked) ==
+ * decode(unchecked) followed by this check (a failing point: status
+ * PA_DECODE_NOT_IN_SUBGROUP, output the point at infinity).  Apart, a verifier
+ * can start its pairing on the unchecked points while the check runs beside it
+ * (bench.py --workload verify --decode).  Points off the curve: unspecified
+ * (the reference's "assuming on curve"). */
+int pa_g1_subgroup_check_batch(const pa_g1_affine *p, size_t n, uint8_t *ok);
+int pa_g2_subgroup_check_batch(const pa_g2_affine *p, size_t n, uint8_t *ok);
 /* EncodedPoint::from_affine (ec.rs:737-752, 839-867, 1398-1415, 1510-1539) */
 int pa_g1_encode_batch(const pa_g1_affine *in, size_t n, int compressed, uint8_t *enc);
 int pa_g2_encode_batch(const pa_g2_affine *in, size_t n, int compressed, uint8_t *enc);
@@ -360,6 +372,8 @@ int pa_g1_decode_batch_device(const uint8_t *enc, size_t n, int compressed, int 
                               uint8_t *status, void *stream);
 int pa_g2_decode_batch_device(const uint8_t *enc, size_t n, int compressed, int checked, pa_g2_affine *out,
                               uint8_t *status, void *stream);
+int pa_g1_subgroup_check_batch_device(const pa_g1_affine *p, size_t n, uint8_t *ok, void *stream);
+int pa_g2_subgroup_check_batch_device(const pa_g2_affine *p, size_t n, uint8_t *ok, void *stream);
 int pa_g1_batch_normalization_device(pa_g1 *v, size_t n, void *stream);
 /* u64 words of the fixed-base table and of the scratch used to build it.  The
  * multiply stages below give the reference's wNAF point for the window

@@ -353,6 +353,12 @@ using G2 = Projective<2>;
     }                                                                                              \
     /* CurveAffine::into_projective, ec.rs:570-582 */                                              \
     inline PROJ into_projective() const;                                                           \
+    /* is_in_correct_subgroup_assuming_on_curve, ec.rs:142-144 (the endomorphism test) */          \
+    bool is_in_correct_subgroup_assuming_on_curve() const {                                        \
+        uint8_t ok = 0;                                                                            \
+        check(pa_g##G##_subgroup_check_batch(&v, 1, &ok), "is_in_correct_subgroup_assuming_on_curve"); \
+        return ok != 0;                                                                            \
+    }                                                                                              \
     /* CurveAffine::mul, ec.rs:174-177: the reference's double-and-add, bit-exact Jacobian words */ \
     inline PROJ mul(const FrRepr& s) const;                                                        \
     static inline std::vector<PROJ> mul_batch(const std::vector<A>& p, const std::vector<FrRepr>& s);

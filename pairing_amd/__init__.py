@@ -29,6 +29,7 @@ __all__ = [
     "g2_prepare", "miller_loop_batch", "miller_loop_shared_prepared", "multi_miller_loop", "final_exponentiation", "pairing",
     "multi_miller_loop_affine", "multi_pairing", "pairing_multi_gpu",
     "fq_sqrt", "fq2_sqrt", "g1_decode", "g2_decode", "g1_encode", "g2_encode", "DECODE_STATUS",
+    "g1_subgroup_check", "g2_subgroup_check",
     "fr_mul", "fr_square", "fr_add", "fr_sub", "fr_double", "fr_negate", "fr_inverse",
     "fr_from_repr", "fr_into_repr", "fr_pow", "fr_legendre", "fr_sqrt",
     "g1_affine_mul", "g2_affine_mul", "g1_mul_assign", "g2_mul_assign", "g1_multiexp", "g2_multiexp",
@@ -419,6 +420,24 @@ def g1_decode(enc, compressed, checked=True):
 def g2_decode(enc, compressed, checked=True):
     """G2Uncompressed / G2Compressed ::into_affine[_unchecked] (ec.rs:1322-1509)."""
     return _decode(2, enc, compressed, checked)
+
+
+def _subgroup(group, pts):
+    pts = as_rows(pts, W_G1A if group == 1 else W_G2A, "points")
+    ok = np.zeros(pts.shape[0], np.uint8)
+    call("pa_g%d_subgroup_check_batch" % group, ptr(pts), pts.shape[0], ptr(ok))
+    return ok.astype(bool)
+
+
+def g1_subgroup_check(pts):
+    """is_in_correct_subgroup_assuming_on_curve (ec.rs:142-144) for (n, 13) affine
+    rows: True where r * P == 0 (infinity included); unspecified off the curve."""
+    return _subgroup(1, pts)
+
+
+def g2_subgroup_check(pts):
+    """is_in_correct_subgroup_assuming_on_curve for (n, 25) G2 affine rows."""
+    return _subgroup(2, pts)
 
 
 def _encode(group, pts, compressed):

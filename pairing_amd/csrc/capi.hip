@@ -958,6 +958,18 @@ int host_decode(int group, const uint8_t* enc, size_t n, int compressed, int che
     if ((rc = download(out, dout, rec * n))) return rc;
     return download(status, dst, n);
 }
+int host_subgroup(int group, const void* pts, size_t n, uint8_t* ok) {
+    if (n == 0) return PA_OK;
+    if (!pts || !ok) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    const size_t rec = group == 1 ? sizeof(pa_g1_affine) : sizeof(pa_g2_affine);
+    DevBuf dp, dok;
+    int rc;
+    if ((rc = upload(dp, pts, rec * n))) return rc;
+    PA_TRY(dok.alloc(n), "device scratch");
+    PA_TRY(pa::launch_subgroup_check(group, dp.as<uint64_t>(), n, dok.as<uint8_t>(), call_stream()), "kernel launch");
+    PA_TRY(call_sync(), "kernel execution");
+    return download(ok, dok, n);
+}
 int host_encode(int group, const void* in, size_t n, int compressed, uint8_t* enc) {
     if (n == 0) return PA_OK;
     if (!in || !enc) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
@@ -995,6 +1007,8 @@ int pa_g2_decode_batch(const uint8_t* enc, size_t n, int compressed, int checked
                        uint8_t* status) {
     return host_decode(2, enc, n, compressed != 0, checked != 0, out, status);
 }
+int pa_g1_subgroup_check_batch(const pa_g1_affine* p, size_t n, uint8_t* ok) { return host_subgroup(1, p, n, ok); }
+int pa_g2_subgroup_check_batch(const pa_g2_affine* p, size_t n, uint8_t* ok) { return host_subgroup(2, p, n, ok); }
 int pa_g1_encode_batch(const pa_g1_affine* in, size_t n, int compressed, uint8_t* enc) {
     return host_encode(1, in, n, compressed != 0, enc);
 }
@@ -1139,6 +1153,16 @@ int pa_g2_wnaf_fixed_scalar_exact_device(const pa_g2* bases, size_t n, const pa_
 }
 
 // ---- device-resident variants ----
+int pa_g1_subgroup_check_batch_device(const pa_g1_affine* p, size_t n, uint8_t* ok, void* stream) {
+    if (n && (!p || !ok)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_subgroup_check(1, (const uint64_t*)p, n, ok, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
+int pa_g2_subgroup_check_batch_device(const pa_g2_affine* p, size_t n, uint8_t* ok, void* stream) {
+    if (n && (!p || !ok)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");
+    PA_TRY(pa::launch_subgroup_check(2, (const uint64_t*)p, n, ok, (hipStream_t)stream), "kernel launch");
+    return PA_OK;
+}
 int pa_g1_decode_batch_device(const uint8_t* enc, size_t n, int compressed, int checked, pa_g1_affine* out,
                               uint8_t* status, void* stream) {
     if (n && (!enc || !out || !status)) return fail(PA_ERR_INVALID_ARGUMENT, "null pointer");

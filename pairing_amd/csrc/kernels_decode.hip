@@ -783,6 +783,53 @@ __global__ void __launch_bounds__(64) k_decode_quad(const uint8_t* __restrict__ 
     }
 }
 
+// is_in_correct_subgroup_assuming_on_curve (ec.rs:142-144) over affine points
+// in HBM, apart from a decode: EncodedPoint::into_affine is
+// into_affine_unchecked + this check (ec.rs:676-684, 786-793), so a verifier
+// can start its pairing on the unchecked points while the check runs beside it
+// (bench.py --workload verify --decode).  The same endomorphism identities as
+// the decode's checked path (in_subgroup / qdec::in_g1, in_g2); infinity is in
+// the subgroup.  For a point off the curve the answer is unspecified, as the
+// reference's name says.  One record per group of quads (latency form) ...
+template <int G>
+__global__ void __launch_bounds__(64) k_subgroup_quad(const uint64_t* __restrict__ pts, size_t n,
+                                                      uint8_t* __restrict__ ok) {
+    constexpr int NQ = G == 1 ? 4 : 8, L = 4 * NQ, PER = 64 / L;
+    constexpr int RW = G == 1 ? 13 : 25;
+    const int lane = threadIdx.x;
+    const size_t i = (size_t)blockIdx.x * PER + lane / L;
+    if (i >= n) return;   // whole groups leave together
+    const dq::Lc l = dq::lctx(lane, NQ);
+    const uint64_t* r = pts + (size_t)RW * i;
+    bool in = true;
+    if ((r[RW - 1] & 0xff) == 0) {   // the infinity byte (pa_g1_affine / pa_g2_affine)
+        if constexpr (G == 1) {
+            Fq x, y;
+            fq_load(x, r);
+            fq_load(y, r + 6);
+            in = qdec::in_g1<NQ>(dq::from_abi(x, l), dq::from_abi(y, l), l);
+        } else {
+            Fq v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) fq_load(v[k], r + 6 * k);
+            in = qdec::in_g2<NQ>(dq::Q2<1>{dq::from_abi(v[0], l), dq::from_abi(v[1], l)},
+                                 dq::Q2<1>{dq::from_abi(v[2], l), dq::from_abi(v[3], l)}, l);
+        }
+    }
+    if (lane % L == 0) ok[i] = in ? 1 : 0;
+}
+// ... or one lane per record (throughput form, large batches)
+template <int G>
+__global__ void __launch_bounds__(64) k_subgroup(const uint64_t* __restrict__ pts, size_t n, uint8_t* __restrict__ ok) {
+    using F = typename std::conditional<G == 1, Fq, Fq2>::type;
+    constexpr int W = FieldWords<F>::n;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Aff<F> a;
+    load_aff(a, pts + (size_t)(2 * W + 1) * i);
+    ok[i] = in_subgroup(a) ? 1 : 0;
+}
+
 // EncodedPoint::from_affine
 template <int G, bool COMPRESSED>
 __global__ void __launch_bounds__(64) k_encode(const uint64_t* __restrict__ in, size_t n, uint8_t* __restrict__ enc) {
@@ -880,6 +927,22 @@ hipError_t launch_decode(int group, int compressed, int checked, const uint8_t* 
     else if (group == 1) k_decode<1, false><<<b, 64, 0, stream>>>(enc, n, checked, out, status);
     else if (compressed) k_decode<2, true><<<b, 64, 0, stream>>>(enc, n, checked, out, status);
     else k_decode<2, false><<<b, 64, 0, stream>>>(enc, n, checked, out, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_subgroup_check(int group, const uint64_t* pts, size_t n, uint8_t* ok, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const int dv = g_decode_variant.load(std::memory_order_relaxed);
+    if (dv == 2 || (dv == 0 && n <= decode_quad_max())) {
+        const unsigned per = group == 1 ? 4 : 2;   // records per 64-lane block
+        const unsigned bq = (unsigned)((n + per - 1) / per);
+        if (group == 1) k_subgroup_quad<1><<<bq, 64, 0, stream>>>(pts, n, ok);
+        else k_subgroup_quad<2><<<bq, 64, 0, stream>>>(pts, n, ok);
+        return hipGetLastError();
+    }
+    const unsigned b = blocks_for(n);
+    if (group == 1) k_subgroup<1><<<b, 64, 0, stream>>>(pts, n, ok);
+    else k_subgroup<2><<<b, 64, 0, stream>>>(pts, n, ok);
     return hipGetLastError();
 }
 

@@ -120,6 +120,8 @@ hipError_t launch_fq12_product(uint64_t* work, size_t n, uint64_t* out, hipStrea
 
 // point decoding / encoding (group 1 or 2; records in the wire format) and
 // square roots (degree 1: Fq, 2: Fq2), kernels_decode.hip
+// is_in_correct_subgroup_assuming_on_curve (ec.rs:142-144) over affine records: ok = 1 / 0
+hipError_t launch_subgroup_check(int group, const uint64_t* pts, size_t n, uint8_t* ok, hipStream_t stream);
 hipError_t launch_decode(int group, int compressed, int checked, const uint8_t* enc, size_t n, uint64_t* out,
                          uint8_t* status, hipStream_t stream);
 // 0: by batch size (<= PA_DECODE_QUAD_MAX records: the quad-group latency

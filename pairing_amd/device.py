@@ -247,6 +247,14 @@ def group_add(group, a, b, out, stream=None):
     call("pa_g%d_add_batch_device" % group, *args, a.shape[0], _stream_ptr(stream))
 
 
+def subgroup_check(group, pts, ok, stream=None):
+    """is_in_correct_subgroup_assuming_on_curve (ec.rs:142-144) over affine rows in HBM
+    (n, 13|25) int64: ok (n,) uint8 = 1 in the subgroup (infinity included), 0 not."""
+    n = pts.shape[0]
+    args = (_dptr(pts, W_G1A if group == 1 else W_G2A, "pts"),)
+    call("pa_g%d_subgroup_check_batch_device" % group, *args, n, _flags(ok, n), _stream_ptr(stream))
+
+
 def decode(group, enc, compressed, checked, out, status, stream=None):
     """EncodedPoint::into_affine[_unchecked] over records resident in HBM:
     enc (n, 48|96|192) uint8, out (n, 13|25) int64 affine records, status (n,) uint8."""

@@ -164,6 +164,26 @@ static void encoding_tests(const Data& d) {
     EXPECT(decode_error([&] { u.into_affine(); }) == GroupDecodingError::NotOnCurve);
     EXPECT(u.into_affine_unchecked().v.infinity == 0);   // unchecked skips the curve check
 
+    // is_in_correct_subgroup_assuming_on_curve (ec.rs:142-144): the generators and zero are in the
+    // groups; the first small x whose compressed encoding decodes unchecked is a point on E(Fq)
+    // outside G1 (cofactor ~2^126), which into_affine rejects
+    EXPECT(G1Affine::one().is_in_correct_subgroup_assuming_on_curve());
+    EXPECT(G2Affine::one().is_in_correct_subgroup_assuming_on_curve());
+    EXPECT(G1Affine::zero().is_in_correct_subgroup_assuming_on_curve());
+    EXPECT(G2Affine::zero().is_in_correct_subgroup_assuming_on_curve());
+    bool found = false;
+    for (int x = 1; x < 64 && !found; x++) {
+        auto e = G1Affine::one().into_compressed();
+        std::memset(e.as_mut(), 0, 48);
+        e.as_mut()[0] = 0x80;
+        e.as_mut()[47] = (uint8_t)x;
+        if (decode_error([&] { e.into_affine_unchecked(); }) != -1) continue;
+        found = true;
+        EXPECT(!e.into_affine_unchecked().is_in_correct_subgroup_assuming_on_curve());
+        EXPECT(decode_error([&] { e.into_affine(); }) == GroupDecodingError::NotInSubgroup);
+    }
+    EXPECT(found);
+
     // batched: the aP encode and decode back
     auto enc = G1Compressed::from_affine_batch(d.a_p);
     std::vector<uint8_t> st;

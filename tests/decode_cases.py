@@ -292,6 +292,21 @@ def subgroup_points(group, seed, n=6):
     return pts, truth
 
 
+def aff_record(group, P):
+    """the ABI affine record (pa_g1_affine 13 / pa_g2_affine 25 u64, Montgomery
+    coordinates, infinity word last) of a point P = (x, y), or of None (infinity)"""
+    from helpers import mont
+    w = 13 if group == 1 else 25
+    if P is None:
+        r = [0] * w
+        r[-1] = 1
+        return r
+    x, y = P
+    if group == 1:
+        return mont(x) + mont(y) + [0]
+    return mont(x[0]) + mont(x[1]) + mont(y[0]) + mont(y[1]) + [0]
+
+
 def subgroup_records(group, seed, n=6):
     pts, truth = subgroup_points(group, seed, n)
     enc = enc_g1 if group == 1 else enc_g2

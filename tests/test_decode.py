@@ -203,6 +203,46 @@ def test_gpu_subgroup_check_matches_oracle(gpu, oracle, decode_kernel, subgroup_
 
 
 @pytest.mark.gpu
+def test_gpu_subgroup_check_entry(gpu, oracle, decode_kernel, subgroup_case):
+    """pa_g{1,2}_subgroup_check_batch (is_in_correct_subgroup_assuming_on_curve,
+    ec.rs:142-144) on the unchecked decode's points == r * P == 0, infinity in;
+    and decode(checked) == decode(unchecked) + this check (into_affine,
+    ec.rs:1322-1332: the uncompressed points here are all on the curve)"""
+    group, enc, truth = subgroup_case
+    dec = gpu.g1_decode if group == 1 else gpu.g2_decode
+    chk = gpu.g1_subgroup_check if group == 1 else gpu.g2_subgroup_check
+    pts, st = dec(enc, False, False)
+    assert (st == D.OK).all()
+    ok = chk(pts)
+    assert ok.tolist() == list(truth)
+    want_pts, want_st = oracle.decode(group, enc, False, checked=True, nthreads=4)
+    assert want_st.tolist() == [D.OK if t else D.NOT_IN_SUBGROUP for t in ok]
+    assert np.array_equal(pts[ok], want_pts[ok])
+    # infinity rows (from zero encodings) are in the subgroup
+    zero = np.zeros_like(pts[:2])
+    zero[:, -1] = 1
+    assert chk(np.concatenate([zero, pts[:2]])).tolist() == [True, True] + list(truth[:2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", [1, 2])
+def test_gpu_subgroup_check_device_large_batch(gpu, group):
+    """the device entry over more points than the latency form takes (one lane
+    per record): the generator's multiples in, each one's image under a point
+    of small order (off the subgroup) out, in a seeded interleaving"""
+    import torch
+    import pairing_amd.device as pdev
+    pts, truth = D.subgroup_points(group, seed=90 + group, n=2)
+    base = np.array([D.aff_record(group, P) for P in pts], np.uint64)
+    idx = np.random.default_rng(3).integers(0, len(pts), size=9001)
+    rows = np.ascontiguousarray(base[idx])
+    ok = torch.empty(len(rows), dtype=torch.uint8, device="cuda:0")
+    pdev.subgroup_check(group, torch.from_numpy(rows.view(np.int64)).cuda(), ok)
+    torch.cuda.synchronize()
+    assert ok.cpu().numpy().astype(bool).tolist() == [bool(truth[k]) for k in idx]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("group", [1, 2])
 def test_gpu_subgroup_check_compressed(gpu, oracle, decode_kernel, group):
     """the same points (in and outside the subgroup, small-order components
