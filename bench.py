@@ -156,11 +156,13 @@ def kernel_variant_label(n):
     generated one lane, else lane pairs again; 1 lane pairs, 2 quad VM, 3 one lane, 4 one-wave VM)"""
     v = int(os.environ.get("PA_PAIRING_KERNEL", "0"))
     if v == 0:
+        if int(os.environ.get("PA_PQ_MIN", "1024")) < n <= int(os.environ.get("PA_PQ_MAX", "2048")):
+            return "lane_groups"
         if n <= int(os.environ.get("PA_COOP_MAX", "2304")):
             return "coop"
         one = int(os.environ.get("PA_PAIR_MAX", "32768")) < n <= int(os.environ.get("PA_ONE_MAX", "34048"))
         return "gen" if one else "gen2"
-    return {1: "gen2", 2: "coop", 3: "gen", 4: "coop1"}.get(v, "variant%d" % v)
+    return {1: "gen2", 2: "coop", 3: "gen", 4: "coop1", 5: "lane_groups"}.get(v, "variant%d" % v)
 
 
 def host_threads():

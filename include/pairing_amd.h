@@ -82,7 +82,10 @@ int pa_synchronize(void);
  * (identical results):
  *   0 = default, by batch size n: n <= PA_COOP_MAX (2304) on the
  *       cooperative kernels (a four-wave quad-VM workgroup per pairing,
- *       kernels_coop.hip: the verifier shape, ~1.6 ms), n <= PA_PAIR_MAX
+ *       kernels_coop.hip: the verifier shape, ~1.6 ms) except n in
+ *       (PA_PQ_MIN, PA_PQ_MAX] = (1024, 2048] on the lane-group kernels
+ *       (round 6, kernels_pair_quad.hip: one pairing per 32 lanes, ~4.5 ms
+ *       for up to 2048 pairings), n <= PA_PAIR_MAX
  *       (32768) on the generated kernels with a lane pair per pairing
  *       (~8.6-9.3 ms), n <= PA_PAIR_MAX + PA_TAIL_MAX (34048; round 6)
  *       as the first 32768 on lane pairs and the tail on the cooperative
@@ -101,6 +104,9 @@ int pa_synchronize(void);
  *   4 = cooperative kernels for every size on the round-2 one-wave VM
  *       (A/B, tests; added in round 3 -- 0 and 2 now run batches of up to
  *       PA_COOP_QUAD_MAX items on the four-wave quad VM, same results)
+ *   5 = lane-group kernels for every size (round 6: one pairing per 32
+ *       lanes, the tower's products batched into levels over 8 lane quads,
+ *       kernels_pair_quad.hip; the Miller values are the reference's)
  * Process-wide; not part of the reference interface.
  * Behavior change in round 2: the numbering was 0 = hipcc lazy core,
  * 1 / 2 = hipcc 32-bit word kernels (one lane / two lanes), 3 = generated,

@@ -25,7 +25,9 @@ thread_local std::string g_last_error;
 // Pairing kernel selection (pa_set_pairing_kernel).  0 (default) by batch
 // size, each where it is fastest (round 5, profiles/r05_regimes.txt):
 //   n <= coop_max() (2304): the cooperative kernels (kernels_coop.hip, a
-//      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
+//      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms), except
+//      (pq_min(), pq_max()] = (1024, 2048] on the lane-group kernels (round 6,
+//      kernels_pair_quad.hip: one pairing per 32 lanes, ~4.5 ms);
 //   n <= pair_max() (32768): the generated kernels with a lane pair per
 //      pairing, at most one wave per SIMD: 8.6-9.3 ms whatever n;
 //   n <= pair_max() + tail_max() (34048; round 6): the first 32768 on lane
@@ -75,6 +77,24 @@ size_t ml_one_max() {
 bool use_coop(size_t n) {
     const int v = pairing_variant();
     return v == 2 || v == 4 || (v == 0 && n <= coop_max());
+}
+// the lane-group kernels (kernels_pair_quad.hip, one pairing per 32 lanes):
+// variant 5 every size; the default in (PA_PQ_MIN, PA_PQ_MAX] = (1024, 2048],
+// inside the cooperative range, where one round of them (~4.5 ms, at most
+// 2048 pairings at one wave per SIMD) beats the quad VM's ~270 k pairings/s
+// (1153: 4.43 vs 4.97 ms, 2048: 4.49 vs 7.63 -- the quad VM steps up after
+// 1024 pairings, its rounds of workgroups; profiles/r06_lane_groups.txt)
+size_t pq_min() {
+    static const size_t v = env_size("PA_PQ_MIN", 1024);
+    return v;
+}
+size_t pq_max() {
+    static const size_t v = env_size("PA_PQ_MAX", 2048);
+    return v;
+}
+bool use_pq(size_t n) {
+    const int v = pairing_variant();
+    return v == 5 || (v == 0 && n > pq_min() && n <= pq_max());
 }
 int coop_vm() { return pairing_variant() == 4 ? 1 : 0; }
 // lanes per pairing of the generated kernels; ml_only: the reference-form Miller
@@ -182,6 +202,7 @@ constexpr size_t kG1Words = sizeof(pa_g1_affine) / 8, kG2Words = sizeof(pa_g2_af
                  kF12Words = sizeof(pa_fq12) / 8;
 
 hipError_t ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
+    if (use_pq(n)) return pa::launch_pq_miller_loop(p, q, out, n, s);
     if (use_coop(n)) return pa::launch_coop_miller_loop(p, q, out, n, s, coop_vm());
     return pa::launch_miller_loop_gen(gen_lanes(n, true), p, q, out, n, s);
 }
@@ -202,7 +223,7 @@ hipError_t mlp_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_
 // keep ml_launch.  PA_PAIRING_ML=ref: the reference-form kernels (A/B).
 hipError_t pairing_ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
     static const bool ref = getenv("PA_PAIRING_ML") && strcmp(getenv("PA_PAIRING_ML"), "ref") == 0;
-    if (use_coop(n)) return ml_launch(p, q, out, n, s);
+    if (use_coop(n) || use_pq(n)) return ml_launch(p, q, out, n, s);
     if (const size_t h = split_head(n, s)) {
         TailFork* f = nullptr;
         hipError_t e = pa::launch_miller_loop_pairing_gen(2, p, q, out, h, s);
@@ -217,6 +238,7 @@ hipError_t pairing_ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out
     return pa::launch_miller_loop_pairing_gen(gen_lanes(n), p, q, out, n, s);
 }
 hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
+    if (use_pq(n)) return pa::launch_pq_final_exp(in, out, ok, n, s);
     if (use_coop(n)) return pa::launch_coop_final_exp(in, out, ok, n, s, coop_vm());
     if (const size_t h = split_head(n, s)) {
         TailFork* f = nullptr;
@@ -458,7 +480,7 @@ int pa_set_device(int device) {
     return PA_OK;
 }
 int pa_set_pairing_kernel(int variant) {
-    if (variant < 0 || variant > 4) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..4");
+    if (variant < 0 || variant > 5) return fail(PA_ERR_INVALID_ARGUMENT, "kernel variant must be 0..5");
     g_pairing_variant.store(variant, std::memory_order_relaxed);
     return PA_OK;
 }

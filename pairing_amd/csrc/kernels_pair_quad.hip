@@ -1,0 +1,64 @@
+// Pairing kernels on lane groups (pair_quad.h): one pairing per 32 lanes,
+// two per 64-lane block.  The latency form for mid-size batches; values as
+// the reference's (the Miller values bit for bit, the final exponentiation's
+// result being unique).
+#include "launch.h"
+#include "pair_quad.h"
+
+namespace pa {
+namespace {
+
+// out[i] = miller_loop([(p[i], q[i].prepare())]) (mod.rs:40-102); a pair with
+// an infinity side gives one (mod.rs:50-54)
+__global__ void __launch_bounds__(64) k_pq_miller_loop(const uint64_t* __restrict__ p_aff,
+                                                       const uint64_t* __restrict__ q_aff,
+                                                       uint64_t* __restrict__ out, size_t n) {
+    const int lane = threadIdx.x;
+    const size_t i = (size_t)blockIdx.x * 2 + (lane >> 5);
+    if (i >= n) return;   // whole groups leave together
+    const dq::Lc l = dq::lctx(lane, pq::NQ);
+    const uint64_t* p = p_aff + 13 * i;
+    const uint64_t* q = q_aff + 25 * i;
+    pq::E12 f;
+    if (((p[12] | q[24]) & 0xff) != 0) {
+        f = pq::e12_one(l);
+    } else {
+        const dq::Q<1> px = pq::load_q(p, l), py = pq::load_q(p + 6, l);
+        const pq::E2 qx = {pq::load_q(q, l), pq::load_q(q + 6, l)};
+        const pq::E2 qy = {pq::load_q(q + 12, l), pq::load_q(q + 18, l)};
+        f = pq::miller_loop(px, py, qx, qy, l);
+    }
+    pq::store12(out + 72 * i, f, false, lane & 31);
+}
+
+// out[i] = final_exponentiation(in[i]) (mod.rs:104-160); ok[i] = 0 and a zero
+// output iff in[i] == 0 (mod.rs:108); in place allowed (the group reads its
+// record before it writes)
+__global__ void __launch_bounds__(64) k_pq_final_exp(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n) {
+    const int lane = threadIdx.x;
+    const size_t i = (size_t)blockIdx.x * 2 + (lane >> 5);
+    if (i >= n) return;
+    const dq::Lc l = dq::lctx(lane, pq::NQ);
+    const pq::E12 f = pq::load12(in + 72 * i, l);
+    bool good = true;
+    const pq::E12 r = pq::final_exp(f, good, l);
+    pq::store12(out + 72 * i, r, !good, lane & 31);
+    if (ok && (lane & 31) == 0) ok[i] = good ? 1 : 0;
+}
+
+}  // namespace
+
+hipError_t launch_pq_miller_loop(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (n > 0x1fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pq_miller_loop, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, s, p, q, out, n);
+    return hipGetLastError();
+}
+hipError_t launch_pq_final_exp(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (n > 0x1fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pq_final_exp, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, s, in, out, ok, n);
+    return hipGetLastError();
+}
+
+}  // namespace pa

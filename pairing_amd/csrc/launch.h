@@ -106,6 +106,11 @@ hipError_t launch_final_exp_gen(int lanes, const uint64_t* in, uint64_t* out, ui
 // results as the one-lane kernels at a fraction of their latency.  vm: 0 =
 // by batch size (the four-wave quad VM up to PA_COOP_QUAD_MAX items, else the
 // one-wave VM; PA_COOP_VM=1 / 4 overrides), 1 = one-wave VM, 4 = quad VM
+// pairings on lane groups (kernels_pair_quad.hip, pair_quad.h): one pairing per
+// 32 lanes; the Miller values are the reference's, the final exponentiation
+// gives ok = 0 / zero for in == 0
+hipError_t launch_pq_miller_loop(const uint64_t* p, const uint64_t* q, uint64_t* out, size_t n, hipStream_t s);
+hipError_t launch_pq_final_exp(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, hipStream_t s);
 hipError_t launch_coop_miller_loop(const uint64_t* p_aff, const uint64_t* q_aff, uint64_t* out, size_t n,
                                    hipStream_t stream, int vm = 0);
 // nin > 1 (with n = 1): the final exponentiation of in[0] * ... * in[nin - 1]

@@ -35,7 +35,7 @@ def timed(fn, reps=5):
 sizes = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 16, 64, 256, 1024, 2048, 4096]
 VARIANTS = ((2, "coop4"), (4, "coop1"), (3, "one-lane"))
 if os.environ.get("COOP_LAT_VARIANTS"):   # e.g. "1,3": lane pairs vs one lane for mid-size batches
-    names = {0: "default", 1: "lane-pair", 2: "coop4", 3: "one-lane", 4: "coop1"}
+    names = {0: "default", 1: "lane-pair", 2: "coop4", 3: "one-lane", 4: "coop1", 5: "lane-group"}
     VARIANTS = tuple((int(v), names[int(v)]) for v in os.environ["COOP_LAT_VARIANTS"].split(","))
 for variant, name in VARIANTS:
     pairing_amd.set_pairing_kernel(variant)
