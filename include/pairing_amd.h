@@ -84,7 +84,7 @@ int pa_synchronize(void);
  *       cooperative kernels (a four-wave quad-VM workgroup per pairing,
  *       kernels_coop.hip: the verifier shape, ~1.6 ms) except n in
  *       (PA_PQ_MIN, PA_PQ_MAX] = (1024, 2048] on the lane-group kernels
- *       (round 6, kernels_pair_quad.hip: one pairing per 32 lanes, ~4.5 ms
+ *       (round 6, kernels_pair_quad.hip: one pairing per 32 lanes, ~3.8 ms
  *       for up to 2048 pairings), n <= PA_PAIR_MAX
  *       (32768) on the generated kernels with a lane pair per pairing
  *       (~8.6-9.3 ms), n <= PA_PAIR_MAX + PA_TAIL_MAX (34048; round 6)

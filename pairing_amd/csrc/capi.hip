@@ -81,9 +81,9 @@ bool use_coop(size_t n) {
 // the lane-group kernels (kernels_pair_quad.hip, one pairing per 32 lanes):
 // variant 5 every size; the default in (PA_PQ_MIN, PA_PQ_MAX] = (1024, 2048],
 // inside the cooperative range, where one round of them (~4.5 ms, at most
-// 2048 pairings at one wave per SIMD) beats the quad VM's ~270 k pairings/s
-// (1153: 4.43 vs 4.97 ms, 2048: 4.49 vs 7.63 -- the quad VM steps up after
-// 1024 pairings, its rounds of workgroups; profiles/r06_lane_groups.txt)
+// 2048 pairings at one wave per SIMD, ~3.8 ms) beats the quad VM's ~270 k
+// pairings/s (1024: 3.72 vs 3.96 ms, 2048: 3.78 vs 7.63; the quad VM steps up
+// after 1024 pairings, its rounds of workgroups; profiles/r06_lane_groups.txt)
 size_t pq_min() {
     static const size_t v = env_size("PA_PQ_MIN", 1024);
     return v;

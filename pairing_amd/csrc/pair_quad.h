@@ -131,10 +131,21 @@ PA_DEV Q6<cmax(U + subcu(U), 2 * U)> mul_v(const Q6<U>& a, const Lc& l) {
 }
 PA_DEV E6 e6_zero() { return {e2_zero(), e2_zero(), e2_zero()}; }
 
+template <int K>
+PA_DEV void mul6s_raw(Q6<10> (&o)[K], const Q6<2> (&a)[K], const Q6<2> (&b)[K], const Lc& l);
 // K Fq6 products a[k] b[k] (fq6.rs:199-248, Karatsuba: 6 Fq2 products each),
 // all 6 K Fq2 products in one batch
 template <int K>
 PA_DEV void mul6s(E6 (&o)[K], const Q6<2> (&a)[K], const Q6<2> (&b)[K], const Lc& l) {
+    Q6<10> u[K];
+    mul6s_raw<K>(u, a, b, l);
+#pragma unroll
+    for (int k = 0; k < K; k++) o[k] = red6(u[k], l);
+}
+// the same, the Karatsuba combinations left unreduced (bound 10), for
+// callers whose next sums stay within the reduction's bound
+template <int K>
+PA_DEV void mul6s_raw(Q6<10> (&o)[K], const Q6<2> (&a)[K], const Q6<2> (&b)[K], const Lc& l) {
     E2 p[6 * K];
     prods_g<6 * K>(p, [&](int k, Q2<2>& x, Q2<2>& y) {
         const Q6<2>& u = a[k / 6];
@@ -152,9 +163,9 @@ PA_DEV void mul6s(E6 (&o)[K], const Q6<2> (&a)[K], const Q6<2> (&b)[K], const Lc
     for (int k = 0; k < K; k++) {
         const E2 v0 = p[6 * k], v1 = p[6 * k + 1], v2 = p[6 * k + 2];
         const E2 t0 = p[6 * k + 3], t1 = p[6 * k + 4], t2 = p[6 * k + 5];
-        o[k].c0 = red(add(xi(sub(t0, add(v1, v2), l), l), v0), l);
-        o[k].c1 = red(add(sub(t1, add(v0, v1), l), xi(v2, l)), l);
-        o[k].c2 = red(add(sub(t2, add(v0, v2), l), v1), l);
+        o[k].c0 = relax<10>(add(xi(sub(t0, add(v1, v2), l), l), v0));
+        o[k].c1 = relax<10>(add(sub(t1, add(v0, v1), l), xi(v2, l)));
+        o[k].c2 = relax<10>(add(sub(t2, add(v0, v2), l), v1));
     }
 }
 
@@ -195,11 +206,11 @@ PA_DEV E12 e12_one(const Lc& l) { return {{one_e<Q2>(l), e2_zero(), e2_zero()}, 
 PA_DEV E12 mul12(const E12& a, const E12& b, const Lc& l) {
     const Q6<2> as[3] = {w6(a.c0, l), w6(a.c1, l), w6(add6(a.c0, a.c1), l)};
     const Q6<2> bs[3] = {w6(b.c0, l), w6(b.c1, l), w6(add6(b.c0, b.c1), l)};
-    E6 p[3];
-    mul6s<3>(p, as, bs, l);
-    const E6 aa = p[0], bb = p[1], cross = p[2];
+    Q6<10> p[3];
+    mul6s_raw<3>(p, as, bs, l);
+    const E6 aa = red6(p[0], l), bb = red6(p[1], l);
     E12 r;
-    r.c1 = red6(sub6(cross, add6(aa, bb), l), l);
+    r.c1 = red6(sub6(p[2], add6(aa, bb), l), l);   // cross unreduced: 10 + subcu(2) <= 16
     r.c0 = red6(add6(mul_v(bb, l), aa), l);
     return r;
 }
@@ -207,11 +218,11 @@ PA_DEV E12 mul12(const E12& a, const E12& b, const Lc& l) {
 PA_DEV E12 sqr12(const E12& a, const Lc& l) {
     const Q6<2> as[2] = {w6(a.c0, l), w6(red6(add6(mul_v(a.c1, l), a.c0), l), l)};
     const Q6<2> bs[2] = {w6(a.c1, l), w6(add6(a.c0, a.c1), l)};
-    E6 p[2];
-    mul6s<2>(p, as, bs, l);
-    const E6 ab = p[0], t = p[1];
+    Q6<10> p[2];
+    mul6s_raw<2>(p, as, bs, l);
+    const E6 ab = red6(p[0], l);
     E12 r;
-    r.c0 = red6(sub6(t, red6(add6(ab, mul_v(ab, l)), l), l), l);
+    r.c0 = red6(sub6(p[1], add6(ab, mul_v(ab, l)), l), l);   // t unreduced: 10 + subcu(4) <= 16
     r.c1 = red6(add6(ab, ab), l);
     return r;
 }
@@ -229,11 +240,24 @@ PA_DEV E12 mul_by_014(const E12& a, const E2& c0, const E2& c1, const E2& c4, co
     y[12] = w2(c4, l);
     E2 p[13];
     prods<13>(p, x, y, l);
-    const E6 aa = by01_fin(p, 0, l), s = by01_fin(p, 5, l);
+    // mul_by_01's combinations (by01_fin) left unreduced where the final sums'
+    // bounds allow -- aa.c0 (bound 8) is the only one reduced
+    auto fin = [&](int k, auto& c0, auto& c1, auto& c2) {
+        const E2 a_a = p[k], b_b = p[k + 1], t1 = p[k + 2], t3 = p[k + 3], t2 = p[k + 4];
+        c0 = add(xi(sub(t1, b_b, l), l), a_a);
+        c1 = relax<4>(sub(t2, add(a_a, b_b), l));
+        c2 = relax<4>(add(sub(t3, a_a, l), b_b));
+    };
+    Q2<8> a0, s0;
+    Q2<4> a1, a2, s1, s2;
+    fin(0, a0, a1, a2);
+    fin(5, s0, s1, s2);
+    const E2 aa0 = red(a0, l);
     const E6 bb = {p[10], p[11], p[12]};
     E12 r;
-    r.c1 = red6(sub6(s, add6(aa, bb), l), l);
-    r.c0 = red6(add6(mul_v(bb, l), aa), l);
+    r.c1 = {red(sub(s0, add(aa0, bb.c0), l), l), red(sub(s1, add(a1, bb.c1), l), l),
+            red(sub(s2, add(a2, bb.c2), l), l)};
+    r.c0 = {red(add(xi(bb.c2, l), aa0), l), red(add(bb.c0, a1), l), red(add(bb.c1, a2), l)};
     return r;
 }
 // Fq12::frobenius_map, fq12.rs:90-97 (fq6.rs:157-164 on both halves): 2 levels
@@ -269,11 +293,14 @@ PA_DEV E12 cyc_sqr(const E12& f, const Lc& l) {
     }
     E2 s[9];
     prods<9>(s, x, x, l);
-    E2 t[6];   // fq4_sqr: r0 = xi b^2 + a^2, r1 = (a + b)^2 - a^2 - b^2
+    // fq4_sqr: r0 = xi b^2 + a^2, r1 = (a + b)^2 - a^2 - b^2, left unreduced
+    // (bound 4): 3 t -+ 2 a stays within the reduction's bound 16 (the Fq
+    // reductions are half of a level's time, so 12 fewer per squaring count)
+    Q2<4> t[6];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        t[2 * k] = red(add(xi(s[3 * k + 1], l), s[3 * k]), l);
-        t[2 * k + 1] = red(sub(s[3 * k + 2], add(s[3 * k], s[3 * k + 1]), l), l);
+        t[2 * k] = add(xi(s[3 * k + 1], l), s[3 * k]);
+        t[2 * k + 1] = relax<4>(sub(s[3 * k + 2], add(s[3 * k], s[3 * k + 1]), l));
     }
     E12 r;
     r.c0.c0 = red(add(dbl(sub(t[0], f.c0.c0, l)), t[0]), l);
@@ -403,7 +430,7 @@ PA_DEV Line dbl_step(G2J& r, const Lc& l) {
     const E2 t2 = b[0], t5 = b[2];
     const E2 t3 = red(dbl(sub(b[1], add(t0, t2), l)), l);
     Line c;
-    c.c2 = red(sub(b[3], red(add(add(t0, t5), dbl(dbl(t1))), l), l), l);
+    c.c2 = red(sub(b[3], add(add(t0, t5), dbl(dbl(t1))), l), l);
     const E2 x = red(sub(t5, dbl(t3), l), l);
     const E2 z = red(sub(zy2, add(t1, zz), l), l);
     E2 d[3];
@@ -412,7 +439,7 @@ PA_DEV Line dbl_step(G2J& r, const Lc& l) {
         const Q2<2> ys[3] = {relax<2>(t4), relax<2>(zz), relax<2>(zz)};
         prods<3>(d, xs, ys, l);
     }
-    r.y = red(sub(d[0], red(dbl(dbl(dbl(t2))), l), l), l);
+    r.y = red(sub(d[0], dbl(dbl(dbl(t2))), l), l);
     r.x = x;
     r.z = z;
     c.c1 = d[1];
