@@ -80,12 +80,13 @@ int pa_set_device(int device);
 int pa_synchronize(void);
 /* Tuning knob: which kernels run the Miller loop / final exponentiation
  * (identical results):
- *   0 = default, by batch size n: n <= PA_COOP_MAX (2304) on the
+ *   0 = default, by batch size n: n <= PA_PQ_MIN (1024) on the
  *       cooperative kernels (a four-wave quad-VM workgroup per pairing,
- *       kernels_coop.hip: the verifier shape, ~1.6 ms) except n in
- *       (PA_PQ_MIN, PA_PQ_MAX] = (1024, 2048] on the lane-group kernels
- *       (round 6, kernels_pair_quad.hip: one pairing per 32 lanes, ~3.8 ms
- *       for up to 2048 pairings), n <= PA_PAIR_MAX
+ *       kernels_coop.hip: the verifier shape, ~1.6 ms), n <= PA_PQ_MAX
+ *       (4096) on the lane-group kernels (round 6, kernels_pair_quad.hip:
+ *       one pairing per 32 lanes, rounds of up to 2048 pairings at ~3.8 ms;
+ *       with PA_PQ_MAX = 0 the cooperative kernels run up to PA_COOP_MAX
+ *       = 2304), n <= PA_PAIR_MAX
  *       (32768) on the generated kernels with a lane pair per pairing
  *       (~8.6-9.3 ms), n <= PA_PAIR_MAX + PA_TAIL_MAX (34048; round 6)
  *       as the first 32768 on lane pairs and the tail on the cooperative

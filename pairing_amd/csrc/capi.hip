@@ -24,12 +24,15 @@ namespace {
 thread_local std::string g_last_error;
 // Pairing kernel selection (pa_set_pairing_kernel).  0 (default) by batch
 // size, each where it is fastest (round 5, profiles/r05_regimes.txt):
-//   n <= coop_max() (2304): the cooperative kernels (kernels_coop.hip, a
-//      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms), except
-//      (pq_min(), pq_max()] = (1024, 2048] on the lane-group kernels (round 6,
-//      kernels_pair_quad.hip: one pairing per 32 lanes, ~4.5 ms);
+//   n <= pq_min() (1024): the cooperative kernels (kernels_coop.hip, a
+//      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
+//   n <= pq_max() (4096; round 6): the lane-group kernels
+//      (kernels_pair_quad.hip: one pairing per 32 lanes, rounds of 2048 at
+//      ~3.8 ms -- 2048 pairs 3.78 ms, 4096 7.55, where the quad VM took 7.63 /
+//      the lane pairs 8.41);
 //   n <= pair_max() (32768): the generated kernels with a lane pair per
-//      pairing, at most one wave per SIMD: 8.6-9.3 ms whatever n;
+//      pairing, at most one wave per SIMD: 8.4-9.3 ms whatever n (the
+//      cooperative kernels up to coop_max() = 2304 when lane groups are off);
 //   n <= pair_max() + tail_max() (34048; round 6): the first 32768 on lane
 //      pairs and the tail on the cooperative kernels on a forked stream
 //      (split_head below; 32769: 10.8 ms instead of 15.7);
@@ -79,17 +82,17 @@ bool use_coop(size_t n) {
     return v == 2 || v == 4 || (v == 0 && n <= coop_max());
 }
 // the lane-group kernels (kernels_pair_quad.hip, one pairing per 32 lanes):
-// variant 5 every size; the default in (PA_PQ_MIN, PA_PQ_MAX] = (1024, 2048],
-// inside the cooperative range, where one round of them (~4.5 ms, at most
-// 2048 pairings at one wave per SIMD, ~3.8 ms) beats the quad VM's ~270 k
-// pairings/s (1024: 3.72 vs 3.96 ms, 2048: 3.78 vs 7.63; the quad VM steps up
-// after 1024 pairings, its rounds of workgroups; profiles/r06_lane_groups.txt)
+// variant 5 every size; the default in (PA_PQ_MIN, PA_PQ_MAX] = (1024, 4096]:
+// a round of them (at most 2048 pairings at one wave per SIMD) takes ~3.8 ms,
+// against the quad VM's ~270 k pairings/s (1024: 3.72 vs 3.96 ms, 2048: 3.78
+// vs 7.63; the quad VM steps up after 1024 pairings) and the lane pairs'
+// ~8.4 ms (two rounds, 4096: 7.55 vs 8.41); profiles/r06_lane_groups.txt
 size_t pq_min() {
     static const size_t v = env_size("PA_PQ_MIN", 1024);
     return v;
 }
 size_t pq_max() {
-    static const size_t v = env_size("PA_PQ_MAX", 2048);
+    static const size_t v = env_size("PA_PQ_MAX", 4096);
     return v;
 }
 bool use_pq(size_t n) {
