@@ -101,3 +101,4 @@ def test_default_selection_lane_group_window_edges(gpu, oracle, n):
     pdev.pairing(_dev(p), _dev(q), out, scratch)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_host(out), oracle.pairing(p, q, _threads()))
+
