@@ -86,7 +86,8 @@ bool use_coop(size_t n) {
 // a round of them (at most 2048 pairings at one wave per SIMD) takes ~3.8 ms,
 // against the quad VM's ~270 k pairings/s (1024: 3.72 vs 3.96 ms, 2048: 3.78
 // vs 7.63; the quad VM steps up after 1024 pairings) and the lane pairs'
-// ~8.4 ms (two rounds, 4096: 7.55 vs 8.41); profiles/r06_lane_groups.txt
+// ~8.4 ms (4096: 6.99 vs 8.41, the Miller loop at two waves per SIMD);
+// profiles/r06_lane_groups.txt
 size_t pq_min() {
     static const size_t v = env_size("PA_PQ_MIN", 1024);
     return v;

@@ -102,3 +102,22 @@ def test_default_selection_lane_group_window_edges(gpu, oracle, n):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_host(out), oracle.pairing(p, q, _threads()))
 
+
+
+def test_lane_group_miller_loop_points_outside_the_subgroups(lane_groups, oracle):
+    """the Miller loop is defined for any curve points (mod.rs:40-102 does no
+    subgroup check): G1 and G2 points with small-order components give the
+    oracle's Miller values bit for bit"""
+    import torch
+    import decode_cases as D
+    import pairing_amd.device as pdev
+    p1, _ = D.subgroup_points(1, seed=93, n=2)
+    p2, _ = D.subgroup_points(2, seed=94, n=2)
+    m = min(len(p1), len(p2))
+    p = np.array([D.aff_record(1, P) for P in p1[:m]], np.uint64)
+    q = np.array([D.aff_record(2, P) for P in p2[:m]], np.uint64)
+    f = pdev.empty_records(m, 72, "cuda:0")
+    pdev.miller_loop(_dev(p), _dev(q), f)
+    torch.cuda.synchronize()
+    want = oracle.miller_loop_batch(p, oracle.g2_prepare(q))
+    np.testing.assert_array_equal(_host(f), want)
