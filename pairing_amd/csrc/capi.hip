@@ -28,7 +28,7 @@ thread_local std::string g_last_error;
 //      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
 //   n <= pq_max() (4096; round 6): the lane-group kernels
 //      (kernels_pair_quad.hip: one pairing per 32 lanes, rounds of 2048 at
-//      ~3.8 ms -- 2048 pairs 3.78 ms, 4096 7.55, where the quad VM took 7.63 /
+//      ~3.8 ms -- 2048 pairs 3.78 ms, 4096 6.99, where the quad VM took 7.63 /
 //      the lane pairs 8.41);
 //   n <= pair_max() (32768): the generated kernels with a lane pair per
 //      pairing, at most one wave per SIMD: 8.4-9.3 ms whatever n (the
