@@ -28,7 +28,7 @@ thread_local std::string g_last_error;
 //      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
 //   n <= pq_max() (4096; round 6): the lane-group kernels
 //      (kernels_pair_quad.hip: one pairing per 32 lanes, rounds of 2048 at
-//      ~3.8 ms -- 2048 pairs 3.78 ms, 4096 6.99, where the quad VM took 7.63 /
+//      ~3.8 ms -- 2048 pairs 3.78 ms, 4096 6.45, where the quad VM took 7.63 /
 //      the lane pairs 8.41);
 //   n <= pair_max() (32768): the generated kernels with a lane pair per
 //      pairing, at most one wave per SIMD: 8.4-9.3 ms whatever n (the
@@ -86,7 +86,7 @@ bool use_coop(size_t n) {
 // a round of them (at most 2048 pairings at one wave per SIMD) takes ~3.8 ms,
 // against the quad VM's ~270 k pairings/s (1024: 3.72 vs 3.96 ms, 2048: 3.78
 // vs 7.63; the quad VM steps up after 1024 pairings) and the lane pairs'
-// ~8.4 ms (4096: 6.99 vs 8.41, the Miller loop at two waves per SIMD);
+// ~8.4 ms (4096: 6.45 vs 8.41, both kernels at two waves per SIMD above 2048);
 // profiles/r06_lane_groups.txt
 size_t pq_min() {
     static const size_t v = env_size("PA_PQ_MIN", 1024);
