@@ -12,7 +12,7 @@ namespace {
 // an infinity side gives one (mod.rs:50-54).  Held to 256 registers (two waves
 // per SIMD, 96 B of scratch): 4096 pairings' Miller loops in 2.67 ms instead of
 // two rounds of 1.63 (profiles/r06_lane_groups.txt, session 7); the final
-// exponentiation needs 512 registers and stays at one wave per SIMD
+// exponentiation comes in both forms below
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_pq_miller_loop(const uint64_t* __restrict__ p_aff,
                                                        const uint64_t* __restrict__ q_aff,
                                                        uint64_t* __restrict__ out, size_t n) {
