@@ -88,11 +88,13 @@ int pa_synchronize(void);
  *       with PA_PQ_MAX = 0 the cooperative kernels run up to PA_COOP_MAX
  *       = 2304), n <= PA_PAIR_MAX
  *       (32768) on the generated kernels with a lane pair per pairing
- *       (~8.6-9.3 ms), n <= PA_PAIR_MAX + PA_TAIL_MAX (34048; round 6)
- *       as the first 32768 on lane pairs and the tail on the cooperative
- *       kernels on a stream forked from the caller's (32769 pairs in
- *       ~10.8 ms; not under stream capture, where the one-pairing-per-lane
- *       kernels run the window, ~15.7 ms), larger batches on lane
+ *       (~8.6-9.3 ms), n <= PA_PAIR_MAX + PA_TAIL_MAX (34816; round 6)
+ *       as the first 32768 on lane pairs and the tail on a stream forked
+ *       from the caller's -- on the cooperative kernels up to 1024 tail
+ *       pairings, the lane-group kernels above (32769 pairs in ~10.8 ms,
+ *       34816 in ~13.0; not under stream capture, where the
+ *       one-pairing-per-lane kernels run up to 34048, ~15.7 ms), larger
+ *       batches on lane
  *       pairs again, two waves per SIMD (2^16 in ~15.7 ms; tools/pgen: own
  *       register allocation, code objects lib/pa_gen_*.hsaco, each loaded
  *       at its first use).  e(P, Q) entries (pa_pairing_batch, multi_pairing)

@@ -33,9 +33,10 @@ thread_local std::string g_last_error;
 //   n <= pair_max() (32768): the generated kernels with a lane pair per
 //      pairing, at most one wave per SIMD: 8.4-9.3 ms whatever n (the
 //      cooperative kernels up to coop_max() = 2304 when lane groups are off);
-//   n <= pair_max() + tail_max() (34048; round 6): the first 32768 on lane
-//      pairs and the tail on the cooperative kernels on a forked stream
-//      (split_head below; 32769: 10.8 ms instead of 15.7);
+//   n <= pair_max() + tail_max() (34816; round 6): the first 32768 on lane
+//      pairs and the tail on a forked stream, on the cooperative kernels up
+//      to 1024 tail pairings and the lane groups above (split_head below;
+//      32769: 10.8 ms, 34816: 13.0, instead of 15.7);
 //   n <= one_max() (34048): one lane per pairing (one wave per SIMD at most:
 //      ~15.7 ms, where a second lane-pair wave on a few SIMDs costs 15.6-16.7;
 //      with the pairing-only lane-pair Miller loop lane pairs win from ~34 000
@@ -130,11 +131,22 @@ constexpr int kMaxWnafWindow = 62;
 // stream capture (the side stream would join the graph); PA_TAIL_MAX=0 turns
 // it off, PA_TAIL_SERIAL=1 runs the tail on the caller's stream (A/B).
 size_t tail_max() {
-    // profiles/r06_tail/: the forked cooperative tail beats a second lane-pair wave
-    // (15.6-15.7 ms) up to ~1300 pairs: 32769 10.8 ms, 33024 10.6, 33792 13.1,
-    // 34048 14.4, 34816 17.1 (serial tail 10.7 / 10.5 / 19.5 / 20.7 / 23.1)
-    static const size_t v = env_size("PA_TAIL_MAX", 1280);
+    // profiles/r06_tail/: the forked tail beats a second lane-pair wave (15.6-15.7
+    // ms) up to ~2000 tail pairs: 32769 10.8 ms, 33024 10.6, 33792 13.1 (the
+    // cooperative kernels), 34048 12.9, 34816 13.0 (the lane groups); 35840
+    // 15.7 -- no better than no split
+    static const size_t v = env_size("PA_TAIL_MAX", 2048);
     return v;
+}
+// the tail's kernels: the cooperative ones up to 1024 tail pairings, the lane
+// groups above (33024: 10.6 vs 11.6 ms; 34048: 14.2 vs 12.9; 34816: 17.1 vs
+// 13.0; profiles/r06_tail/); PA_TAIL_KIND=coop / pq forces one (A/B)
+bool tail_pq(size_t tail) {
+    static const int v = [] {
+        const char* e = getenv("PA_TAIL_KIND");
+        return !e ? 0 : strcmp(e, "pq") == 0 ? 1 : strcmp(e, "coop") == 0 ? 2 : 0;
+    }();
+    return v == 1 || (v == 0 && tail > 1024);
 }
 struct TailFork {
     int dev = -1;
@@ -233,8 +245,10 @@ hipError_t pairing_ml_launch(const uint64_t* p, const uint64_t* q, uint64_t* out
         hipError_t e = pa::launch_miller_loop_pairing_gen(2, p, q, out, h, s);
         if (e == hipSuccess) e = tail_begin(s, &f);
         if (e == hipSuccess)
-            e = pa::launch_coop_miller_loop(p + h * kG1Words, q + h * kG2Words, out + h * kF12Words, n - h,
-                                            f ? f->side : s, coop_vm());
+            e = tail_pq(n - h) ? pa::launch_pq_miller_loop(p + h * kG1Words, q + h * kG2Words, out + h * kF12Words, n - h,
+                                                      f ? f->side : s)
+                          : pa::launch_coop_miller_loop(p + h * kG1Words, q + h * kG2Words, out + h * kF12Words,
+                                                        n - h, f ? f->side : s, coop_vm());
         const hipError_t j = tail_end(s, f);
         return e != hipSuccess ? e : j;
     }
@@ -249,8 +263,10 @@ hipError_t fe_launch(const uint64_t* in, uint64_t* out, uint8_t* ok, size_t n, h
         hipError_t e = pa::launch_final_exp_gen(2, in, out, ok, h, s);
         if (e == hipSuccess) e = tail_begin(s, &f);
         if (e == hipSuccess)
-            e = pa::launch_coop_final_exp(in + h * kF12Words, out + h * kF12Words, ok ? ok + h : nullptr, n - h,
-                                          f ? f->side : s, coop_vm());
+            e = tail_pq(n - h) ? pa::launch_pq_final_exp(in + h * kF12Words, out + h * kF12Words, ok ? ok + h : nullptr,
+                                                    n - h, f ? f->side : s)
+                          : pa::launch_coop_final_exp(in + h * kF12Words, out + h * kF12Words, ok ? ok + h : nullptr,
+                                                      n - h, f ? f->side : s, coop_vm());
         const hipError_t j = tail_end(s, f);
         return e != hipSuccess ? e : j;
     }

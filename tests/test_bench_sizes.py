@@ -112,13 +112,14 @@ def test_pairing_device_bit_exact_at_bench_size(gpu, oracle, variant):
     assert (got[inf] == one).all()
 
 
-@pytest.mark.parametrize("n", [2305, 32768, 32769, 33792, 34048, 34049])
+@pytest.mark.parametrize("n", [2305, 32768, 32769, 33792, 33793, 34816, 34817])
 def test_pairing_default_mid_size_batches(gpu, oracle, n):
-    """The default selection's regime boundaries (PA_COOP_MAX < n <= PA_PAIR_MAX:
+    """The default selection's regime boundaries (PA_PQ_MAX < n <= PA_PAIR_MAX:
     lane pairs at one wave per SIMD; PA_PAIR_MAX < n <= PA_PAIR_MAX + PA_TAIL_MAX
-    (34048): the first PA_PAIR_MAX on lane pairs and the tail on the cooperative
-    kernels, on a forked stream; above: lane pairs at two waves per SIMD) on
-    both sides, every pairing against the oracle"""
+    (34816): the first PA_PAIR_MAX on lane pairs and the tail on a forked stream,
+    on the cooperative kernels up to 1024 tail pairs (33792) and the lane groups
+    above; above: lane pairs at two waves per SIMD) on both sides, every pairing
+    against the oracle"""
     import torch
     import bench
     import pairing_amd.device as pdev
@@ -130,17 +131,18 @@ def test_pairing_default_mid_size_batches(gpu, oracle, n):
     np.testing.assert_array_equal(_host(out), oracle.pairing(p_np, q_np, _threads()))
 
 
-def test_split_batch_stages_with_zeros_and_infinity(gpu, oracle):
+@pytest.mark.parametrize("tail", [300, 1500], ids=["coop_tail", "lane_group_tail"])
+def test_split_batch_stages_with_zeros_and_infinity(gpu, oracle, tail):
     """A batch just above PA_PAIR_MAX through the two stages apart: the Miller
-    loop stage (lane pairs for the head, the cooperative kernel on the forked
-    stream for the tail) then the final exponentiation (split the same way) ==
+    loop stage (lane pairs for the head; on the forked stream the cooperative
+    kernel for a tail of up to 1024, the lane groups above) then the final exponentiation (split the same way) ==
     the oracle's pairing, with infinity Q on both sides of the split; and the
     final exponentiation alone over such a batch with zero Miller values in the
     head and in the tail: ok = 0 / zero output exactly there, in place too"""
     import torch
     import bench
     import pairing_amd.device as pdev
-    n = 32768 + 300
+    n = 32768 + tail
     p_np, q_np = bench.make_pairs(n, 0, seed=31)
     for k in (7, 32768 + 3, n - 1):
         q_np[k, :24] = 0
@@ -153,7 +155,7 @@ def test_split_batch_stages_with_zeros_and_infinity(gpu, oracle):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_host(out), oracle.pairing(p_np, q_np, _threads()))
     fv = _host(f)
-    zeros = [11, 32768, 32768 + 299]
+    zeros = [11, 32768, 32768 + tail - 1]
     fv[zeros] = 0
     exp, ok_exp = oracle.final_exponentiation(fv, _threads())
     d = _dev(fv)
