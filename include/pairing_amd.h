@@ -90,7 +90,7 @@ int pa_synchronize(void);
  *       (32768) on the generated kernels with a lane pair per pairing
  *       (~8.6-9.3 ms), n <= PA_PAIR_MAX + PA_TAIL_MAX (34816; round 6)
  *       as the first 32768 on lane pairs and the tail on a stream forked
- *       from the caller's -- on the cooperative kernels up to 1024 tail
+ *       from the caller's -- on the cooperative kernels up to 832 tail
  *       pairings, the lane-group kernels above (32769 pairs in ~10.8 ms,
  *       34816 in ~13.0; not under stream capture, where the
  *       one-pairing-per-lane kernels run up to 34048, ~15.7 ms), larger

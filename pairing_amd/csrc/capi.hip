@@ -35,7 +35,7 @@ thread_local std::string g_last_error;
 //      cooperative kernels up to coop_max() = 2304 when lane groups are off);
 //   n <= pair_max() + tail_max() (34816; round 6): the first 32768 on lane
 //      pairs and the tail on a forked stream, on the cooperative kernels up
-//      to 1024 tail pairings and the lane groups above (split_head below;
+//      to 832 tail pairings and the lane groups above (split_head below;
 //      32769: 10.8 ms, 34816: 13.0, instead of 15.7);
 //   n <= one_max() (34048): one lane per pairing (one wave per SIMD at most:
 //      ~15.7 ms, where a second lane-pair wave on a few SIMDs costs 15.6-16.7;
@@ -138,15 +138,15 @@ size_t tail_max() {
     static const size_t v = env_size("PA_TAIL_MAX", 2048);
     return v;
 }
-// the tail's kernels: the cooperative ones up to 1024 tail pairings, the lane
-// groups above (33024: 10.6 vs 11.6 ms; 34048: 14.2 vs 12.9; 34816: 17.1 vs
+// the tail's kernels: the cooperative ones up to 832 tail pairings, the lane
+// groups above (33536: 12.3 vs 13.1 ms; 33664: 13.2 vs 12.9; 34816: 17.1 vs
 // 13.0; profiles/r06_tail/); PA_TAIL_KIND=coop / pq forces one (A/B)
 bool tail_pq(size_t tail) {
     static const int v = [] {
         const char* e = getenv("PA_TAIL_KIND");
         return !e ? 0 : strcmp(e, "pq") == 0 ? 1 : strcmp(e, "coop") == 0 ? 2 : 0;
     }();
-    return v == 1 || (v == 0 && tail > 1024);
+    return v == 1 || (v == 0 && tail > 832);
 }
 struct TailFork {
     int dev = -1;

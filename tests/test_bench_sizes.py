@@ -112,12 +112,12 @@ def test_pairing_device_bit_exact_at_bench_size(gpu, oracle, variant):
     assert (got[inf] == one).all()
 
 
-@pytest.mark.parametrize("n", [2305, 32768, 32769, 33792, 33793, 34816, 34817])
+@pytest.mark.parametrize("n", [2305, 32768, 32769, 33600, 33601, 34816, 34817])
 def test_pairing_default_mid_size_batches(gpu, oracle, n):
     """The default selection's regime boundaries (PA_PQ_MAX < n <= PA_PAIR_MAX:
     lane pairs at one wave per SIMD; PA_PAIR_MAX < n <= PA_PAIR_MAX + PA_TAIL_MAX
     (34816): the first PA_PAIR_MAX on lane pairs and the tail on a forked stream,
-    on the cooperative kernels up to 1024 tail pairs (33792) and the lane groups
+    on the cooperative kernels up to 832 tail pairs (33600) and the lane groups
     above; above: lane pairs at two waves per SIMD) on both sides, every pairing
     against the oracle"""
     import torch
