@@ -156,7 +156,7 @@ def kernel_variant_label(n):
     generated one lane, else lane pairs again; 1 lane pairs, 2 quad VM, 3 one lane, 4 one-wave VM)"""
     v = int(os.environ.get("PA_PAIRING_KERNEL", "0"))
     if v == 0:
-        if int(os.environ.get("PA_PQ_MIN", "1024")) < n <= int(os.environ.get("PA_PQ_MAX", "4096")):
+        if int(os.environ.get("PA_PQ_MIN", "768")) < n <= int(os.environ.get("PA_PQ_MAX", "4096")):
             return "lane_groups"
         if n <= int(os.environ.get("PA_COOP_MAX", "2304")):
             return "coop"

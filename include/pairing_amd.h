@@ -80,7 +80,7 @@ int pa_set_device(int device);
 int pa_synchronize(void);
 /* Tuning knob: which kernels run the Miller loop / final exponentiation
  * (identical results):
- *   0 = default, by batch size n: n <= PA_PQ_MIN (1024) on the
+ *   0 = default, by batch size n: n <= PA_PQ_MIN (768) on the
  *       cooperative kernels (a four-wave quad-VM workgroup per pairing,
  *       kernels_coop.hip: the verifier shape, ~1.6 ms), n <= PA_PQ_MAX
  *       (4096) on the lane-group kernels (round 6, kernels_pair_quad.hip:

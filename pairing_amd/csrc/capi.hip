@@ -24,7 +24,7 @@ namespace {
 thread_local std::string g_last_error;
 // Pairing kernel selection (pa_set_pairing_kernel).  0 (default) by batch
 // size, each where it is fastest (round 5, profiles/r05_regimes.txt):
-//   n <= pq_min() (1024): the cooperative kernels (kernels_coop.hip, a
+//   n <= pq_min() (768): the cooperative kernels (kernels_coop.hip, a
 //      quad-VM workgroup per pairing, ~270 k pairings/s from 1.6 ms);
 //   n <= pq_max() (4096; round 6): the lane-group kernels
 //      (kernels_pair_quad.hip: one pairing per 32 lanes, rounds of 2048 at
@@ -83,14 +83,14 @@ bool use_coop(size_t n) {
     return v == 2 || v == 4 || (v == 0 && n <= coop_max());
 }
 // the lane-group kernels (kernels_pair_quad.hip, one pairing per 32 lanes):
-// variant 5 every size; the default in (PA_PQ_MIN, PA_PQ_MAX] = (1024, 4096]:
+// variant 5 every size; the default in (PA_PQ_MIN, PA_PQ_MAX] = (768, 4096]:
 // a round of them (at most 2048 pairings at one wave per SIMD) takes ~3.8 ms,
-// against the quad VM's ~270 k pairings/s (1024: 3.72 vs 3.96 ms, 2048: 3.78
-// vs 7.63; the quad VM steps up after 1024 pairings) and the lane pairs'
+// against the quad VM's ~270 k pairings/s (800: 3.70 vs 3.94 ms, 2048: 3.78
+// vs 7.63; the quad VM steps up after 768 pairings) and the lane pairs'
 // ~8.4 ms (4096: 6.45 vs 8.41, both kernels at two waves per SIMD above 2048);
 // profiles/r06_lane_groups.txt
 size_t pq_min() {
-    static const size_t v = env_size("PA_PQ_MIN", 1024);
+    static const size_t v = env_size("PA_PQ_MIN", 768);
     return v;
 }
 size_t pq_max() {

@@ -88,9 +88,9 @@ def test_lane_group_multi_pairing(lane_groups, oracle):
     np.testing.assert_array_equal(np.asarray(got).reshape(-1), exp.reshape(-1))
 
 
-@pytest.mark.parametrize("n", [1024, 1025, 4096, 4097])
+@pytest.mark.parametrize("n", [768, 769, 4096, 4097])
 def test_default_selection_lane_group_window_edges(gpu, oracle, n):
-    """the default selection runs (PA_PQ_MIN, PA_PQ_MAX] = (1024, 4096] on the
+    """the default selection runs (PA_PQ_MIN, PA_PQ_MAX] = (768, 4096] on the
     lane-group kernels and the cooperative ones on both sides: bit-exact
     pairings either side of both edges"""
     import torch
