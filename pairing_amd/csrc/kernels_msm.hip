@@ -574,15 +574,16 @@ PA_DEV void msm_flush_fl(uint32_t key, const FlJac& acc, bool untouched, size_t 
 }
 
 // ... and k_msm_chunk_acc<1> with the lazy mixed addition (curve_fl.h);
-// bucket pieces leave in the ABI form the later phases read.
-__global__ void __launch_bounds__(64) PA_MSM_ACC_ATTR k_msm_chunk_acc_fl(const uint64_t* __restrict__ bases,
-                                                         const uint32_t* __restrict__ basefl,
-                                                         const uint32_t* __restrict__ keys,
-                                                         const uint32_t* __restrict__ vals,
-                                                         const uint32_t* __restrict__ start,
-                                                         const uint32_t* __restrict__ wtot, uint32_t w0, uint32_t w1,
-                                                         uint32_t T, uint32_t sentinel, uint64_t* __restrict__ buckets,
-                                                         uint64_t* __restrict__ cont) {
+// bucket pieces leave in the ABI form the later phases read.  PREFETCH: the
+// next item's base is gathered while the current addition runs (the one-wave
+// kernel's latency hiding); without it the two-wave kernel's other wave hides
+// the gathers and the 28 registers go to the addition.
+template <bool PREFETCH>
+PA_DEV void chunk_acc_fl_body(const uint32_t* __restrict__ basefl, const uint32_t* __restrict__ keys,
+                                              const uint32_t* __restrict__ vals, const uint32_t* __restrict__ start,
+                                              const uint32_t* __restrict__ wtot, uint32_t w0, uint32_t w1,
+                                              uint32_t T, uint32_t sentinel, uint64_t* __restrict__ buckets,
+                                              uint64_t* __restrict__ cont) {
     size_t k, j0, j1;
     if (!chunk_range((size_t)blockIdx.x * blockDim.x + threadIdx.x, wtot, w0, w1, T, k, j0, j1)) return;
     uint32_t cur = keys[j0];
@@ -625,7 +626,7 @@ __global__ void __launch_bounds__(64) PA_MSM_ACC_ATTR k_msm_chunk_acc_fl(const u
     fetch(j0 + 1, key1, v1);
     F<1> tx, ty;
     bool inf;
-    gather(key0, v0, tx, ty, inf);
+    if (PREFETCH) gather(key0, v0, tx, ty, inf);
 #pragma unroll 1
     for (size_t j = j0; j < j1; j++) {
         if (key0 >= sentinel) break;
@@ -633,7 +634,8 @@ __global__ void __launch_bounds__(64) PA_MSM_ACC_ATTR k_msm_chunk_acc_fl(const u
         fetch(j + 2, key2, v2);
         F<1> nx, ny;
         bool ninf;
-        gather(key1, v1, nx, ny, ninf);
+        if (PREFETCH) gather(key1, v1, nx, ny, ninf);
+        else gather(key0, v0, tx, ty, inf);
         if (key0 != cur) {
             msm_flush_fl(cur, acc, untouched, j0, k, start, buckets, cont);
             untouched = true;
@@ -647,11 +649,30 @@ __global__ void __launch_bounds__(64) PA_MSM_ACC_ATTR k_msm_chunk_acc_fl(const u
         v0 = v1;
         key1 = key2;
         v1 = v2;
-        tx = nx;
-        ty = ny;
-        inf = ninf;
+        if (PREFETCH) {
+            tx = nx;
+            ty = ny;
+            inf = ninf;
+        }
     }
     msm_flush_fl(cur, acc, untouched, j0, k, start, buckets, cont);
+}
+#define PA_CHUNK_ACC_FL_ARGS                                                                                   \
+    const uint32_t *__restrict__ basefl, const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, \
+        const uint32_t *__restrict__ start, const uint32_t *__restrict__ wtot, uint32_t w0, uint32_t w1,      \
+        uint32_t T, uint32_t sentinel, uint64_t *__restrict__ buckets, uint64_t *__restrict__ cont
+// one wave per SIMD (256 VGPRs + 75 AGPRs), the base prefetched
+__global__ void __launch_bounds__(64) PA_MSM_ACC_ATTR k_msm_chunk_acc_fl(PA_CHUNK_ACC_FL_ARGS) {
+    chunk_acc_fl_body<true>(basefl, keys, vals, start, wtot, w0, w1, T, sentinel, buckets, cont);
+}
+// two waves per SIMD (256 registers), the gathers hidden by the other wave
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_msm_chunk_acc_fl_2w(PA_CHUNK_ACC_FL_ARGS) {
+    chunk_acc_fl_body<false>(basefl, keys, vals, start, wtot, w0, w1, T, sentinel, buckets, cont);
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_msm_chunk_acc_fl_2wp(PA_CHUNK_ACC_FL_ARGS) {
+    chunk_acc_fl_body<true>(basefl, keys, vals, start, wtot, w0, w1, T, sentinel, buckets, cont);
 }
 
 
@@ -1264,11 +1285,19 @@ static hipError_t msm_run(const uint64_t* bases, const uint64_t* scalars, size_t
 
     // the windows' throughput kernels of one part (windows [w0, w1))
     // (the part's item range is on the device, wtot: lanes for the most it can hold)
+    // the G1 bucket accumulation's kernel: PA_MSM_ACC=0 one wave per SIMD with
+    // the base prefetch, 1 two waves without it, 2 two waves with it (A/B)
+    static const int acc_kind = [] {
+        const char* e = getenv("PA_MSM_ACC");
+        return e ? atoi(e) : 0;
+    }();
     auto accumulate = [&](uint32_t w0, uint32_t w1, hipStream_t st) {
         const size_t chunks = ((size_t)(w1 - w0) * n + p.T - 1) / p.T + 1;
         if constexpr (G == 1)
-            hipLaunchKernelGGL(k_msm_chunk_acc_fl, dim3(msm_blocks(chunks, 64)), dim3(64), 0, st, bases, basefl,
-                               keys_out, vals_out, start, wtot, w0, w1, p.T, p.W * p.B, buckets, cont);
+            hipLaunchKernelGGL(acc_kind == 1 ? k_msm_chunk_acc_fl_2w
+                                             : (acc_kind == 2 ? k_msm_chunk_acc_fl_2wp : k_msm_chunk_acc_fl),
+                               dim3(msm_blocks(chunks, 64)), dim3(64), 0, st, basefl, keys_out, vals_out, start, wtot,
+                               w0, w1, p.T, p.W * p.B, buckets, cont);
         else if (g2_lazy)
             hipLaunchKernelGGL(k_msm_chunk_acc_fl2, dim3(msm_blocks(chunks, 64)), dim3(64), 0, st, basefl, keys_out,
                                vals_out, start, wtot, w0, w1, p.T, p.W * p.B, buckets, cont);
