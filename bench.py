@@ -152,15 +152,24 @@ def make_pairs(n, rank, seed=0, span=None):
 
 def kernel_variant_label(n):
     """the pairing kernels a batch of n per GPU runs on (capi.hip: PA_PAIRING_KERNEL 0 = by
-    batch size: <= PA_COOP_MAX cooperative quad VM, <= PA_PAIR_MAX generated lane pairs, <= PA_ONE_MAX
-    generated one lane, else lane pairs again; 1 lane pairs, 2 quad VM, 3 one lane, 4 one-wave VM)"""
-    v = int(os.environ.get("PA_PAIRING_KERNEL", "0"))
+    batch size: (PA_PQ_MIN, PA_PQ_MAX] lane groups, <= PA_COOP_MAX cooperative quad VM,
+    <= PA_PAIR_MAX generated lane pairs, <= PA_PAIR_MAX + PA_TAIL_MAX lane pairs for the head
+    and the tail on the quad VM (<= 832 tail pairs, PA_TAIL_KIND) or the lane groups, <= PA_ONE_MAX
+    generated one lane, else lane pairs again; 1 lane pairs, 2 quad VM, 3 one lane, 4 one-wave VM,
+    5 lane groups)"""
+    env = lambda k, d: int(os.environ.get(k, d))
+    v = env("PA_PAIRING_KERNEL", "0")
     if v == 0:
-        if int(os.environ.get("PA_PQ_MIN", "768")) < n <= int(os.environ.get("PA_PQ_MAX", "4096")):
+        if env("PA_PQ_MIN", "768") < n <= env("PA_PQ_MAX", "4096"):
             return "lane_groups"
-        if n <= int(os.environ.get("PA_COOP_MAX", "2304")):
+        if n <= env("PA_COOP_MAX", "2304"):
             return "coop"
-        one = int(os.environ.get("PA_PAIR_MAX", "32768")) < n <= int(os.environ.get("PA_ONE_MAX", "34048"))
+        pair_max = env("PA_PAIR_MAX", "32768")
+        if pair_max < n <= pair_max + env("PA_TAIL_MAX", "2048"):
+            kind = os.environ.get("PA_TAIL_KIND", "")
+            pq = kind == "pq" or (kind != "coop" and n - pair_max > 832)
+            return "gen2+%s_tail" % ("lane_group" if pq else "coop")
+        one = pair_max < n <= env("PA_ONE_MAX", "34048")
         return "gen" if one else "gen2"
     return {1: "gen2", 2: "coop", 3: "gen", 4: "coop1", 5: "lane_groups"}.get(v, "variant%d" % v)
 

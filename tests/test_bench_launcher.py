@@ -74,3 +74,23 @@ def test_bench_global_batch_ragged_shards():
     assert r.returncode == 0, r.stderr[-3000:]
     line = _json_lines(r.stdout)[0]
     assert line["config"]["global_batch"] == 7 and line["config"]["batch_per_gpu"] == 4
+
+
+def test_kernel_variant_label_follows_the_default_selection(monkeypatch):
+    """bench.kernel_variant_label mirrors capi.hip's default selection (lane groups
+    in (768, 4096], the quad VM below, lane pairs, split batches up to 34816 with
+    the quad VM tail up to 832 tail pairs and the lane groups above) and the
+    PA_PAIRING_KERNEL / PA_TAIL_KIND overrides"""
+    sys.path.insert(0, ROOT)
+    import bench
+    for k in ("PA_PAIRING_KERNEL", "PA_PQ_MIN", "PA_PQ_MAX", "PA_COOP_MAX", "PA_PAIR_MAX",
+              "PA_TAIL_MAX", "PA_TAIL_KIND", "PA_ONE_MAX"):
+        monkeypatch.delenv(k, raising=False)
+    want = {1: "coop", 768: "coop", 769: "lane_groups", 4096: "lane_groups", 4097: "gen2",
+            32768: "gen2", 32769: "gen2+coop_tail", 33600: "gen2+coop_tail",
+            33601: "gen2+lane_group_tail", 34816: "gen2+lane_group_tail", 34817: "gen2", 65536: "gen2"}
+    assert {n: bench.kernel_variant_label(n) for n in want} == want
+    monkeypatch.setenv("PA_TAIL_KIND", "pq")
+    assert bench.kernel_variant_label(32769) == "gen2+lane_group_tail"
+    monkeypatch.setenv("PA_PAIRING_KERNEL", "5")
+    assert bench.kernel_variant_label(65536) == "lane_groups"
