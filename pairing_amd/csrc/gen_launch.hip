@@ -43,6 +43,11 @@ struct GenDevice {
     hipModule_t mod[kKernels] = {};
     hipFunction_t fn[kKernels] = {};
     std::vector<Workspace> pool;
+    // a non-blocking stream of the library's own for the load-time symbol read:
+    // a copy on the legacy stream would join a caller's stream capture
+    // (hipStreamCaptureModeRelaxed) and invalidate it
+    hipStream_t load_stream = nullptr;
+    std::vector<void*> graph_ws;   // workspaces of captured launches (never reused)
 };
 
 std::mutex g_mu;
@@ -110,7 +115,9 @@ hipError_t load(GenDevice& d, int k) {
         uint32_t need = 0;
         const std::string sym = std::string(kName[k]) + "_mem_slots";
         if ((e = hipModuleGetGlobal(&gp, &gb, d.mod[k], sym.c_str())) != hipSuccess || gb != 4 ||
-            (e = hipMemcpyDtoH(&need, gp, 4)) != hipSuccess) {
+            (!d.load_stream && (e = hipStreamCreateWithFlags(&d.load_stream, hipStreamNonBlocking)) != hipSuccess) ||
+            (e = hipMemcpyDtoHAsync(&need, gp, 4, d.load_stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(d.load_stream)) != hipSuccess) {
             if (e == hipSuccess) e = hipErrorInvalidImage;
             g_detail = "workspace size symbol " + sym + " in " + path;
         } else if ((size_t)need * kSlotBytes > wave_bytes()) {
@@ -206,12 +213,25 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
     const size_t blocks = (n * kLanes[which] + 63) / 64;
     if (blocks > 0xffffffffull) return hipErrorInvalidValue;
     const size_t table_at = (blocks * wave_bytes() + 255) & ~(size_t)255;
+    const size_t need = which == 4 ? table_at + kSharedTableAlloc : blocks * wave_bytes();
+    // under stream capture the workspace goes into the caller's graph, which may
+    // replay it at any later time: a dedicated allocation that the pool never
+    // hands out again (kept for the process's lifetime), and no event query or
+    // record on the capturing stream
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if ((e = hipStreamIsCapturing(stream, &cs)) != hipSuccess) return e;
+    const bool captured = cs != hipStreamCaptureStatusNone;
     Workspace* ws = nullptr;
-    if ((e = acquire(d, which == 4 ? table_at + kSharedTableAlloc : blocks * wave_bytes(), stream, &ws)) !=
-        hipSuccess)
-        return e;
+    void* wsp = nullptr;
+    if (captured) {
+        if ((e = hipMalloc(&wsp, need)) != hipSuccess) return e;
+        d.graph_ws.push_back(wsp);
+    } else {
+        if ((e = acquire(d, need, stream, &ws)) != hipSuccess) return e;
+        wsp = ws->p;
+    }
     if (which == 4) {
-        uint32_t* table = reinterpret_cast<uint32_t*>(static_cast<char*>(ws->p) + table_at);
+        uint32_t* table = reinterpret_cast<uint32_t*>(static_cast<char*>(wsp) + table_at);
         if ((e = launch_shared_line_table(static_cast<const uint64_t*>(a1), table, stream)) != hipSuccess) return e;
         a1 = table;
     }
@@ -221,13 +241,14 @@ hipError_t launch(int which, const void* a0, const void* a1, const void* a2, siz
         const void* a2;
         uint64_t n;
         void* ws;
-    } args{a0, a1, a2, (uint64_t)n, ws->p};
+    } args{a0, a1, a2, (uint64_t)n, wsp};
     size_t size = sizeof(args);
     void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                       HIP_LAUNCH_PARAM_END};
     if ((e = hipModuleLaunchKernel(d.fn[which], (unsigned)blocks, 1, 1, 64, 1, 1, 0, stream, nullptr, config)) !=
         hipSuccess)
         return e;
+    if (captured) return hipSuccess;
     ws->last = stream;
     return hipEventRecord(ws->done, stream);
 }
